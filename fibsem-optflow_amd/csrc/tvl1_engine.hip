@@ -1,0 +1,491 @@
+// tvl1_engine.hip — host side of the MI355X TV-L1 engine + the C-ABI of include/tvl1.h.
+//
+// Replaces the reference's solver boundary /root/reference/src/optflow.cpp:516-520
+// (TVL1_solve -> cv::cuda::OpticalFlowDual_TVL1::create(...)->calc(...)).  The
+// host loop below restates OpenCV 3.4.1 calcImpl/procOneScale
+// and launches the gfx950 kernels of tvl1_kernels.hpp.  There is no CPU path:
+// every stage runs on the device; the only device->host traffic inside a solve is
+// the residual of "check" iterations, read exactly where OpenCV reads it.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/tvl1.h"
+#include "tvl1_kernels.hpp"
+
+using namespace tvl1k;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+constexpr int kStripRows = 32;   // rows per wave strip in k_iterate
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct Geometry {
+  int W = 0, H = 0, L = 0;
+  int ws[TVL1_MAX_LEVELS], hs[TVL1_MAX_LEVELS], ps[TVL1_MAX_LEVELS];
+  bool gamma = false;
+};
+
+}  // namespace
+
+struct tvl1_ctx {
+  int device = 0;
+  tvl1_params prm{};
+  std::string err;
+  hipStream_t own_stream = nullptr;
+
+  // arena
+  char *arena = nullptr;
+  size_t arena_bytes = 0;
+  Geometry geo;
+  bool geo_valid = false;
+
+  float *I0s[TVL1_MAX_LEVELS] = {};
+  float *I1s[TVL1_MAX_LEVELS] = {};
+  float4 *G = nullptr;
+  float *U[2][3] = {};   // u1, u2, u3
+  float *Pd[2][6] = {};  // p11, p12, p21, p22, p31, p32
+  float *C[3] = {};      // I1wx, I1wy, rho_c
+  uint8_t *in0 = nullptr, *in1 = nullptr;   // staging for tvl1_calc_host
+  float *outu = nullptr, *outv = nullptr;
+  double *partials = nullptr;
+  int partials_cap = 0;
+  double *red = nullptr;
+  double *pinned = nullptr;  // host-pinned residual landing slot
+};
+
+static tvl1_status set_err(tvl1_ctx *c, tvl1_status st, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c)
+    c->err = buf;
+  else
+    g_create_error = buf;
+  return st;
+}
+
+#define HIP_TRY(ctx, expr)                                                              \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return set_err((ctx), TVL1_EHIP, "%s failed: %s (%s:%d)", #expr,                 \
+                     hipGetErrorString(e_), __FILE__, __LINE__);                        \
+  } while (0)
+
+static tvl1_status check_params(tvl1_ctx *c, const tvl1_params *p) {
+  if (!p) return set_err(c, TVL1_EINVAL, "params is NULL");
+  // CV_Assert(nscales_ > 0) in calcImpl
+  if (p->nscales <= 0) return set_err(c, TVL1_EINVAL, "nscales must be > 0 (got %d)", p->nscales);
+  if (p->warps < 0) return set_err(c, TVL1_EINVAL, "warps must be >= 0");
+  if (p->iterations < 0) return set_err(c, TVL1_EINVAL, "iterations must be >= 0");
+  if (!(p->theta != 0.0)) return set_err(c, TVL1_EINVAL, "theta must be non-zero (tau/theta)");
+  if (!(p->scale_step > 0.0 && p->scale_step <= 1.0))
+    return set_err(c, TVL1_EINVAL, "scaleStep must be in (0, 1]");
+  if (p->median_filtering > 1 && p->median_filtering != 3 && p->median_filtering != 5)
+    return set_err(c, TVL1_EINVAL, "medianFiltering must be 1 (off), 3 or 5");
+  return TVL1_OK;
+}
+
+// Pyramid sizes exactly as calcImpl: round-half-even(cols*step), stop < 16.
+static int pyramid_sizes(int w, int h, int nscales, double step, int *ws, int *hs) {
+  int L = nscales < TVL1_MAX_LEVELS ? nscales : TVL1_MAX_LEVELS;
+  ws[0] = w;
+  hs[0] = h;
+  for (int s = 1; s < L; ++s) {
+    const int nw = (int)std::lrint((double)ws[s - 1] * step);
+    const int nh = (int)std::lrint((double)hs[s - 1] * step);
+    if (nw < 16 || nh < 16) return s;
+    ws[s] = nw;
+    hs[s] = nh;
+  }
+  return L;
+}
+
+static int iterate_blocks(int W, int H) {
+  const int segs = (W + kSegPx - 1) / kSegPx;
+  const int strips = (H + kStripRows - 1) / kStripRows;
+  const int waves = segs * strips;
+  return (waves + 3) / 4;
+}
+
+// Carve the arena for a geometry; grows (never shrinks) the device allocation.
+static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
+  Geometry g;
+  g.W = W;
+  g.H = H;
+  g.gamma = c->prm.gamma != 0.0;
+  g.L = pyramid_sizes(W, H, c->prm.nscales, c->prm.scale_step, g.ws, g.hs);
+  for (int s = 0; s < g.L; ++s) g.ps[s] = (int)align_up((size_t)g.ws[s], 64);
+  if (c->geo_valid && g.W == c->geo.W && g.H == c->geo.H && g.L == c->geo.L &&
+      g.gamma == c->geo.gamma && !memcmp(g.ws, c->geo.ws, sizeof(int) * g.L) &&
+      !memcmp(g.hs, c->geo.hs, sizeof(int) * g.L))
+    return TVL1_OK;
+
+  const size_t P0 = (size_t)g.ps[0];
+  const size_t plane = P0 * (size_t)H * sizeof(float);
+  size_t bytes = 0;
+  for (int s = 0; s < g.L; ++s) bytes += 2 * (size_t)g.ps[s] * g.hs[s] * sizeof(float);
+  bytes += 4 * plane;                       // G (float4)
+  bytes += 2 * 3 * plane;                   // U[2][3]
+  bytes += 2 * 6 * plane;                   // Pd[2][6]
+  bytes += 3 * plane;                       // C
+  bytes += 2 * align_up(P0 * H, 256);       // in0, in1 (u8)
+  bytes += 2 * plane;                       // outu, outv
+  const int nblk = iterate_blocks(W, H) + 64;
+  bytes += align_up((size_t)nblk * sizeof(double), 256) + 256;
+  bytes += 4096;                            // alignment slack
+
+  if (bytes > c->arena_bytes) {
+    if (c->arena) {
+      (void)hipStreamSynchronize(c->own_stream);
+      (void)hipFree(c->arena);
+      c->arena = nullptr;
+      c->arena_bytes = 0;
+    }
+    hipError_t e = hipMalloc((void **)&c->arena, bytes);
+    if (e != hipSuccess)
+      return set_err(c, TVL1_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    c->arena_bytes = bytes;
+    // Zero once: pitch padding then holds finite values forever.
+    HIP_TRY(c, hipMemset(c->arena, 0, bytes));
+  }
+  char *p = c->arena;
+  auto take = [&](size_t n) {
+    char *r = p;
+    p += align_up(n, 256);
+    return r;
+  };
+  for (int s = 0; s < TVL1_MAX_LEVELS; ++s) c->I0s[s] = c->I1s[s] = nullptr;
+  for (int s = 0; s < g.L; ++s) {
+    const size_t n = (size_t)g.ps[s] * g.hs[s] * sizeof(float);
+    c->I0s[s] = (float *)take(n);
+    c->I1s[s] = (float *)take(n);
+  }
+  c->G = (float4 *)take(4 * plane);
+  for (int b = 0; b < 2; ++b)
+    for (int k = 0; k < 3; ++k) c->U[b][k] = (float *)take(plane);
+  for (int b = 0; b < 2; ++b)
+    for (int k = 0; k < 6; ++k) c->Pd[b][k] = (float *)take(plane);
+  for (int k = 0; k < 3; ++k) c->C[k] = (float *)take(plane);
+  c->in0 = (uint8_t *)take(P0 * H);
+  c->in1 = (uint8_t *)take(P0 * H);
+  c->outu = (float *)take(plane);
+  c->outv = (float *)take(plane);
+  c->partials = (double *)take((size_t)nblk * sizeof(double));
+  c->partials_cap = nblk;
+  c->red = (double *)take(256);
+  c->geo = g;
+  c->geo_valid = true;
+  return TVL1_OK;
+}
+
+static inline dim3 grid2(int w, int h, int z = 1) {
+  return dim3((unsigned)((w + 63) / 64), (unsigned)((h + 3) / 4), (unsigned)z);
+}
+static const dim3 kBlk2(64, 4, 1);
+
+// SURVEY 8(d) byte model with executed iteration counts (reported in stats).
+static double survey_bytes(const Geometry &g, int warps, const int64_t *iters) {
+  double B = 0.0;
+  for (int l = 0; l < g.L; ++l) {
+    const double N = (double)g.ws[l] * g.hs[l];
+    B += N * (12.0 + 16.0 + 40.0 * warps + 64.0 * (double)iters[l]);
+    if (l >= 1) B += N * 8.0;
+    if (l < g.L - 1) B += N * 8.0;
+  }
+  const double N0 = (double)g.ws[0] * g.hs[0];
+  B += N0 * (2.0 + 8.0) + N0 * 8.0;
+  return B;
+}
+
+// calcImpl + procOneScale on device inputs already in the arena
+// or caller memory.  Result left in caller's u, v.
+static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8_t *I1,
+                         size_t pitch1, int W, int H, float *u, float *v, size_t fpitch,
+                         tvl1_stats *stats, hipStream_t st) {
+  const tvl1_params &prm = c->prm;
+  const Geometry &g = c->geo;
+  const int L = g.L;
+  const bool gam = g.gamma;
+
+  // [A.1] convertTo
+  hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 2), kBlk2, 0, st, I0, pitch0, I1, pitch1,
+                     c->I0s[0], c->I1s[0], W, H, g.ps[0]);
+  // [A.2] pyramid, kernel step = float(1/scaleStep)
+  const float fdown = (float)(1.0 / prm.scale_step);
+  for (int s = 1; s < L; ++s)
+    hipLaunchKernelGGL(k_resize_down2, grid2(g.ws[s], g.hs[s], 2), kBlk2, 0, st, c->I0s[s - 1],
+                       c->I1s[s - 1], g.ws[s - 1], g.hs[s - 1], g.ps[s - 1], c->I0s[s],
+                       c->I1s[s], g.ws[s], g.hs[s], g.ps[s], fdown, fdown);
+  HIP_TRY(c, hipGetLastError());
+
+  int ui = 0, pi = 0;  // ping-pong indices of the u and p buffer sets
+  {                    // u = 0 at the coarsest level (no initial flow)
+    const int s = L - 1;
+    const size_t n = (size_t)g.ps[s] * g.hs[s] * sizeof(float);
+    HIP_TRY(c, hipMemsetAsync(c->U[ui][0], 0, n, st));
+    HIP_TRY(c, hipMemsetAsync(c->U[ui][1], 0, n, st));
+    if (gam) HIP_TRY(c, hipMemsetAsync(c->U[ui][2], 0, n, st));
+  }
+
+  const float l_t = (float)(prm.lambda * prm.theta);
+  const float taut = (float)(prm.tau / prm.theta);
+  const float theta_f = (float)prm.theta;
+  const float gamma_f = (float)prm.gamma;
+  const float upmul = (float)(1.0 / prm.scale_step);
+
+  int64_t level_iters[TVL1_MAX_LEVELS] = {};
+  int64_t checks = 0;
+
+  for (int s = L - 1; s >= 0; --s) {
+    const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
+    const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
+    hipLaunchKernelGGL(k_gradient, grid2(lw, lh), kBlk2, 0, st, c->I1s[s], lw, lh, P, c->G);
+    bool p_zero = true;  // p = 0 at the start of every level (setTo(0) in procOneScale)
+
+    IterArgs a{};
+    a.I1wx = c->C[0];
+    a.I1wy = c->C[1];
+    a.rho = c->C[2];
+    a.W = lw;
+    a.H = lh;
+    a.P = P;
+    a.segs = (lw + kSegPx - 1) / kSegPx;
+    a.strip_rows = kStripRows;
+    a.l_t = l_t;
+    a.theta = theta_f;
+    a.gamma = gamma_f;
+    a.taut = taut;
+    a.partials = c->partials;
+    const int nblk = iterate_blocks(lw, lh);
+
+    for (int wp = 0; wp < prm.warps; ++wp) {
+      if (prm.median_filtering > 1) {
+        hipLaunchKernelGGL(k_median, grid2(lw, lh, 2), kBlk2, 0, st, c->U[ui][0], c->U[ui][1],
+                           lw, lh, P, prm.median_filtering, c->U[ui ^ 1][0], c->U[ui ^ 1][1]);
+        if (gam) {
+          const size_t n = (size_t)P * lh * sizeof(float);
+          HIP_TRY(c, hipMemcpyAsync(c->U[ui ^ 1][2], c->U[ui][2], n, hipMemcpyDeviceToDevice, st));
+        }
+        ui ^= 1;
+      }
+      hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[ui][0],
+                         c->U[ui][1], lw, lh, P, c->C[0], c->C[1], c->C[2]);
+      double error = DBL_MAX;
+      double prevError = 0.0;
+      int n;
+      for (n = 0; error > scaledEps && n < prm.iterations; ++n) {
+        const bool calcError = (prm.epsilon > 0) && (n & 1) && (prevError < scaledEps);
+        a.u1s = c->U[ui][0]; a.u2s = c->U[ui][1]; a.u3s = c->U[ui][2];
+        a.u1d = c->U[ui ^ 1][0]; a.u2d = c->U[ui ^ 1][1]; a.u3d = c->U[ui ^ 1][2];
+        a.p11s = c->Pd[pi][0]; a.p12s = c->Pd[pi][1]; a.p21s = c->Pd[pi][2];
+        a.p22s = c->Pd[pi][3]; a.p31s = c->Pd[pi][4]; a.p32s = c->Pd[pi][5];
+        a.p11d = c->Pd[pi ^ 1][0]; a.p12d = c->Pd[pi ^ 1][1]; a.p21d = c->Pd[pi ^ 1][2];
+        a.p22d = c->Pd[pi ^ 1][3]; a.p31d = c->Pd[pi ^ 1][4]; a.p32d = c->Pd[pi ^ 1][5];
+        a.calc_err = calcError ? 1 : 0;
+        a.p_zero = p_zero ? 1 : 0;
+        if (gam)
+          hipLaunchKernelGGL(k_iterate<true>, dim3(nblk), dim3(kBlock), 0, st, a);
+        else
+          hipLaunchKernelGGL(k_iterate<false>, dim3(nblk), dim3(kBlock), 0, st, a);
+        p_zero = false;
+        ui ^= 1;
+        pi ^= 1;
+        if (calcError) {
+          hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, nblk, c->red);
+          HIP_TRY(c, hipMemcpyAsync(c->pinned, c->red, sizeof(double), hipMemcpyDeviceToHost, st));
+          HIP_TRY(c, hipStreamSynchronize(st));  // the cuda::sum -> host read of procOneScale
+          error = *c->pinned;
+          prevError = error;
+          ++checks;
+        } else {
+          error = DBL_MAX;
+          prevError -= scaledEps;
+        }
+      }
+      level_iters[s] += n;
+      if (stats && stats->warp_iterations && s * prm.warps + wp < stats->warp_iterations_capacity)
+        stats->warp_iterations[s * prm.warps + wp] = n;
+    }
+    HIP_TRY(c, hipGetLastError());
+    if (s == 0) break;
+    // zoom the flow to the next finer level, then scale by 1/scaleStep
+    const int dw = g.ws[s - 1], dh = g.hs[s - 1];
+    const float fxu = (float)(1.0 / ((double)dw / lw));
+    const float fyu = (float)(1.0 / ((double)dh / lh));
+    hipLaunchKernelGGL(k_upsample, grid2(dw, dh, gam ? 3 : 2), kBlk2, 0, st, c->U[ui][0],
+                       c->U[ui][1], c->U[ui][2], lw, lh, P, c->U[ui ^ 1][0], c->U[ui ^ 1][1],
+                       c->U[ui ^ 1][2], dw, dh, g.ps[s - 1], fxu, fyu, upmul);
+    ui ^= 1;
+  }
+  hipLaunchKernelGGL(k_output, grid2(W, H), kBlk2, 0, st, c->U[ui][0], c->U[ui][1], W, H,
+                     g.ps[0], u, v, fpitch);
+  HIP_TRY(c, hipGetLastError());
+
+  if (stats) {
+    stats->levels = L;
+    int64_t tot = 0;
+    for (int s = 0; s < TVL1_MAX_LEVELS; ++s) {
+      stats->level_width[s] = s < L ? g.ws[s] : 0;
+      stats->level_height[s] = s < L ? g.hs[s] : 0;
+      stats->level_iterations[s] = s < L ? level_iters[s] : 0;
+      tot += s < L ? level_iters[s] : 0;
+    }
+    stats->iterations_total = tot;
+    stats->checks_total = checks;
+    stats->algorithmic_bytes = survey_bytes(g, prm.warps, level_iters);
+  }
+  return TVL1_OK;
+}
+
+extern "C" {
+
+void tvl1_params_default(tvl1_params *p) {
+  if (!p) return;
+  // generate_TV_args, optflow.cpp:503-512
+  p->tau = 0.25;
+  p->lambda = 0.05;
+  p->theta = 0.3;
+  p->nscales = 10;
+  p->warps = 5;
+  p->epsilon = 0.01;
+  p->iterations = 300;
+  p->scale_step = 0.8;
+  p->gamma = 0.0;
+  p->use_initial_flow = 0;
+  p->median_filtering = 1;
+}
+
+int32_t tvl1_abi_version(void) { return TVL1_ABI_VERSION; }
+
+int32_t tvl1_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
+  if (!out) return set_err(nullptr, TVL1_EINVAL, "out is NULL");
+  *out = nullptr;
+  tvl1_status s = check_params(nullptr, params);
+  if (s != TVL1_OK) return s;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    return set_err(nullptr, TVL1_ENODEV, "no HIP device visible");
+  if (device < 0 || device >= n)
+    return set_err(nullptr, TVL1_ENODEV, "device %d out of range (have %d)", device, n);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+    return set_err(nullptr, TVL1_ENODEV, "hipGetDeviceProperties failed");
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(nullptr, TVL1_ENODEV, "device %d is %s; this build targets gfx950 only",
+                   device, prop.gcnArchName);
+  tvl1_ctx *c = new (std::nothrow) tvl1_ctx();
+  if (!c) return set_err(nullptr, TVL1_ENOMEM, "out of host memory");
+  c->device = device;
+  c->prm = *params;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void **)&c->pinned, sizeof(double) * 8, hipHostMallocDefault) != hipSuccess) {
+    delete c;
+    return set_err(nullptr, TVL1_EHIP, "HIP initialisation failed on device %d", device);
+  }
+  *out = c;
+  return TVL1_OK;
+}
+
+tvl1_status tvl1_set_params(tvl1_ctx *c, const tvl1_params *params) {
+  if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  tvl1_status s = check_params(c, params);
+  if (s != TVL1_OK) return s;
+  c->prm = *params;
+  c->geo_valid = false;  // pyramid depth may change
+  return TVL1_OK;
+}
+
+static tvl1_status check_call(tvl1_ctx *c, const void *I0, size_t p0, const void *I1, size_t p1,
+                              int W, int H, const void *u, const void *v, size_t fp) {
+  if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  if (!I0 || !I1 || !u || !v) return set_err(c, TVL1_EINVAL, "null image or flow pointer");
+  if (W <= 0 || H <= 0) return set_err(c, TVL1_ESIZE, "bad size %dx%d", W, H);
+  if ((size_t)W * (size_t)H > (size_t)1 << 31)
+    return set_err(c, TVL1_ESIZE, "image %dx%d too large", W, H);
+  if (p0 < (size_t)W || p1 < (size_t)W) return set_err(c, TVL1_EINVAL, "input pitch < width");
+  if (fp < sizeof(float) * (size_t)W || fp % sizeof(float))
+    return set_err(c, TVL1_EINVAL, "flow pitch must be >= 4*width and a multiple of 4");
+  return TVL1_OK;
+}
+
+tvl1_status tvl1_calc(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8_t *I1,
+                      size_t pitch1, int32_t W, int32_t H, float *u, float *v, size_t fpitch,
+                      tvl1_stats *stats, void *stream) {
+  tvl1_status s = check_call(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch);
+  if (s != TVL1_OK) return s;
+  HIP_TRY(c, hipSetDevice(c->device));
+  s = ensure_geometry(c, W, H);
+  if (s != TVL1_OK) return s;
+  return solve(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch, stats, (hipStream_t)stream);
+}
+
+tvl1_status tvl1_calc_host(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8_t *I1,
+                           size_t pitch1, int32_t W, int32_t H, float *u, float *v,
+                           size_t fpitch, tvl1_stats *stats) {
+  tvl1_status s = check_call(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch);
+  if (s != TVL1_OK) return s;
+  HIP_TRY(c, hipSetDevice(c->device));
+  s = ensure_geometry(c, W, H);
+  if (s != TVL1_OK) return s;
+  hipStream_t st = c->own_stream;
+  const size_t P0 = (size_t)c->geo.ps[0];
+  // GpuMat::upload (optflow.cpp:315-316)
+  HIP_TRY(c, hipMemcpy2DAsync(c->in0, P0, I0, pitch0, W, H, hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpy2DAsync(c->in1, P0, I1, pitch1, W, H, hipMemcpyHostToDevice, st));
+  s = solve(c, c->in0, P0, c->in1, P0, W, H, c->outu, c->outv, P0 * sizeof(float), stats, st);
+  if (s != TVL1_OK) return s;
+  // download (optflow.cpp:475-476)
+  HIP_TRY(c, hipMemcpy2DAsync(u, fpitch, c->outu, P0 * sizeof(float), W * sizeof(float), H,
+                              hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpy2DAsync(v, fpitch, c->outv, P0 * sizeof(float), W * sizeof(float), H,
+                              hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  return TVL1_OK;
+}
+
+tvl1_status tvl1_postprocess(tvl1_ctx *c, float *u, float *v, size_t fpitch, const uint8_t *I1,
+                             size_t pitch1, int32_t W, int32_t H, int32_t mode, void *stream) {
+  tvl1_status s = check_call(c, I1, pitch1, I1, pitch1, W, H, u, v, fpitch);
+  if (s != TVL1_OK) return s;
+  if (mode != 0 && mode != 1) return set_err(c, TVL1_EINVAL, "mode must be 0 (flow) or 1 (map)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(k_postprocess, grid2(W, H), kBlk2, 0, (hipStream_t)stream, u, v, fpitch, I1,
+                     pitch1, W, H, mode);
+  HIP_TRY(c, hipGetLastError());
+  return TVL1_OK;
+}
+
+void tvl1_destroy(tvl1_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+  if (c->arena) (void)hipFree(c->arena);
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+const char *tvl1_last_error(const tvl1_ctx *c) {
+  return c ? c->err.c_str() : g_create_error.c_str();
+}
+
+}  // extern "C"

@@ -1,0 +1,472 @@
+// tvl1_kernels.hpp — device kernels of the MI355X TV-L1 engine (gfx950, wave64).
+//
+// Each kernel restates one stage of the solver the reference calls at
+// /root/reference/src/optflow.cpp:518-519 (OpenCV 3.4.1 cv::cuda::OpticalFlowDual_TVL1,
+// semantics in SURVEY.md Appendix A; kernel inventory SURVEY 2.1 K1..K12).
+// The arithmetic (float32, expression order, no FMA contraction: the library is
+// compiled with -ffp-contract=off) is identical to oracle/tvl1_oracle.c so the
+// two agree bit for bit; the data layout and fusion are MI355X-first:
+//
+//   * every f32 plane is pitched to a multiple of 64 floats (256 B rows);
+//   * the gradient of I1 is stored interleaved as float4 (I1, I1x, I1y, 0) so each
+//     bicubic tap of warpBackward is ONE 16-byte gather instead of three;
+//   * estimateU (K6) and estimateDualVariables (K8) are FUSED into one pass
+//     (k_iterate): a wave owns a 248-px-wide column segment (62 lanes x float4, plus
+//     one halo lane on each side) and rolls down a strip of rows, so the
+//     backward-difference divergence and forward-difference gradient stencils are
+//     wavefront shuffles (x) and register rotation (y); no LDS, one HBM pass;
+//   * the state (u, p) ping-pongs between two buffer sets (Jacobi), so strips and
+//     segments never race on their halos;
+//   * grad = I1wx^2 + I1wy^2 is recomputed from I1wx, I1wy (same IEEE ops as K5)
+//     instead of being stored and re-read every iteration (-4 B/px/iteration);
+//   * the residual sum (K7) is fused into the iteration as per-block double partials
+//     reduced by one tiny kernel in a fixed order (deterministic).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tvl1k {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;                 // 4 waves
+constexpr int kSegPx = (kWave - 2) * 4;     // 248 useful px per wave (lanes 1..62)
+constexpr float kFltEps = 1.1920928955078125e-07f;  // numeric_limits<float>::epsilon()
+
+__device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+
+// ---------------------------------------------------------------- K1 convert
+// GpuMat::convertTo(CV_32F, 1.0) for both frames (blockIdx.z selects the frame).
+__global__ void k_convert_u8(const uint8_t *__restrict__ s0, size_t sp0,
+                             const uint8_t *__restrict__ s1, size_t sp1,
+                             float *__restrict__ d0, float *__restrict__ d1, int W, int H,
+                             int P) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  if (blockIdx.z == 0)
+    d0[(size_t)y * P + x] = (float)s0[(size_t)y * sp0 + x];
+  else
+    d1[(size_t)y * P + x] = (float)s1[(size_t)y * sp1 + x];
+}
+
+// ---------------------------------------------------------------- K2 / K9 resize
+// cuda::resize INTER_LINEAR: corner-aligned, src = dst * f, +1 taps clamped.
+__device__ __forceinline__ float resize_px(const float *__restrict__ src, int sw, int sh,
+                                           int sp, int dx, int dy, float fx, float fy) {
+  const float src_x = (float)dx * fx;
+  const float src_y = (float)dy * fy;
+  const int x1 = (int)floorf(src_x);
+  const int y1 = (int)floorf(src_y);
+  const int x2 = x1 + 1;
+  const int y2 = y1 + 1;
+  const int x2r = imin(x2, sw - 1);
+  const int y2r = imin(y2, sh - 1);
+  float out = 0.0f;
+  out = out + src[(size_t)y1 * sp + x1] * (((float)x2 - src_x) * ((float)y2 - src_y));
+  out = out + src[(size_t)y1 * sp + x2r] * ((src_x - (float)x1) * ((float)y2 - src_y));
+  out = out + src[(size_t)y2r * sp + x1] * (((float)x2 - src_x) * (src_y - (float)y1));
+  out = out + src[(size_t)y2r * sp + x2r] * ((src_x - (float)x1) * (src_y - (float)y1));
+  return out;
+}
+
+// Pyramid step for both frames at once (blockIdx.z selects the frame).
+__global__ void k_resize_down2(const float *__restrict__ a0, const float *__restrict__ a1,
+                               int sw, int sh, int sp, float *__restrict__ b0,
+                               float *__restrict__ b1, int dw, int dh, int dp, float fx,
+                               float fy) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= dw || y >= dh) return;
+  const float *src = blockIdx.z == 0 ? a0 : a1;
+  float *dst = blockIdx.z == 0 ? b0 : b1;
+  dst[(size_t)y * dp + x] = resize_px(src, sw, sh, sp, x, y, fx, fy);
+}
+
+// Flow upsample to the next finer level + cuda::multiply(1/scaleStep) on u1, u2
+// (u3 is resized but not scaled, as in calcImpl).  blockIdx.z = component.
+__global__ void k_upsample(const float *__restrict__ s1, const float *__restrict__ s2,
+                           const float *__restrict__ s3, int sw, int sh, int sp,
+                           float *__restrict__ d1, float *__restrict__ d2,
+                           float *__restrict__ d3, int dw, int dh, int dp, float fx, float fy,
+                           float mul) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= dw || y >= dh) return;
+  const int c = blockIdx.z;
+  const float *src = c == 0 ? s1 : (c == 1 ? s2 : s3);
+  float *dst = c == 0 ? d1 : (c == 1 ? d2 : d3);
+  const float r = resize_px(src, sw, sh, sp, x, y, fx, fy);
+  dst[(size_t)y * dp + x] = c < 2 ? r * mul : r;
+}
+
+// ---------------------------------------------------------------- K3 gradient
+// centeredGradient of I1, written interleaved (I1, I1x, I1y, 0) for the K5 gather.
+__global__ void k_gradient(const float *__restrict__ I, int W, int H, int P,
+                           float4 *__restrict__ G) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const float *row = I + (size_t)y * P;
+  const float c = row[x];
+  const float gx = 0.5f * (row[imin(x + 1, W - 1)] - row[imax(x - 1, 0)]);
+  const float gy = 0.5f * (I[(size_t)imin(y + 1, H - 1) * P + x] - I[(size_t)imax(y - 1, 0) * P + x]);
+  G[(size_t)y * P + x] = make_float4(c, gx, gy, 0.0f);
+}
+
+// ---------------------------------------------------------------- K5 warp
+__device__ __forceinline__ float cubic(float x) {
+  x = fabsf(x);
+  if (x <= 1.0f) return x * x * (1.5f * x - 2.5f) + 1.0f;
+  if (x < 2.0f) return x * (x * (-0.5f * x + 2.5f) - 4.0f) + 2.0f;
+  return 0.0f;
+}
+
+// warpBackward: Keys-cubic (a=-0.5) gather at (x+u1, y+u2), texture clamp,
+// weight-normalised.  Writes I1wx, I1wy, rho_c (I1w and grad are not stored).
+__global__ void k_warp(const float *__restrict__ I0, const float4 *__restrict__ G,
+                       const float *__restrict__ u1, const float *__restrict__ u2, int W,
+                       int H, int P, float *__restrict__ I1wx, float *__restrict__ I1wy,
+                       float *__restrict__ rho) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const size_t i = (size_t)y * P + x;
+  const float u1v = u1[i];
+  const float u2v = u2[i];
+  const float wx = (float)x + u1v;
+  const float wy = (float)y + u2v;
+  const int xmin = (int)ceilf(wx - 2.0f);
+  const int xmax = (int)floorf(wx + 2.0f);
+  const int ymin = (int)ceilf(wy - 2.0f);
+  const int ymax = (int)floorf(wy + 2.0f);
+  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
+  for (int cy = ymin; cy <= ymax; ++cy) {
+    const int ry = imin(imax(cy, 0), H - 1);
+    const float wyk = cubic(wy - (float)cy);
+    for (int cx = xmin; cx <= xmax; ++cx) {
+      const int rx = imin(imax(cx, 0), W - 1);
+      const float w = cubic(wx - (float)cx) * wyk;
+      const float4 g = G[(size_t)ry * P + rx];
+      sum = sum + w * g.x;
+      sumx = sumx + w * g.y;
+      sumy = sumy + w * g.z;
+      wsum = wsum + w;
+    }
+  }
+  const float coeff = 1.0f / wsum;
+  const float I1wv = sum * coeff;
+  const float I1wxv = sumx * coeff;
+  const float I1wyv = sumy * coeff;
+  I1wx[i] = I1wxv;
+  I1wy[i] = I1wyv;
+  rho[i] = I1wv - I1wxv * u1v - I1wyv * u2v - I0[i];
+}
+
+// ---------------------------------------------------------------- K6+K8 fused
+struct IterArgs {
+  const float *I1wx, *I1wy, *rho;                                  // warp constants
+  const float *u1s, *u2s, *u3s;                                    // state in
+  const float *p11s, *p12s, *p21s, *p22s, *p31s, *p32s;
+  float *u1d, *u2d, *u3d;                                          // state out
+  float *p11d, *p12d, *p21d, *p22d, *p31d, *p32d;
+  double *partials;                                                // per-block residual sums
+  int W, H, P;                                                     // P = pitch in floats
+  int segs, strip_rows;
+  float l_t, theta, gamma, taut;
+  int calc_err, p_zero;
+};
+
+template <bool G>
+struct Row {
+  float wx[4], wy[4], rh[4], u1[4], u2[4], p11[4], p12[4], p21[4], p22[4];
+  float u3[4], p31[4], p32[4];  // used only when G (dead otherwise)
+};
+
+__device__ __forceinline__ void ld4(float (&d)[4], const float *__restrict__ base, size_t off) {
+  const float4 t = *reinterpret_cast<const float4 *>(base + off);
+  d[0] = t.x; d[1] = t.y; d[2] = t.z; d[3] = t.w;
+}
+__device__ __forceinline__ void st4(float *__restrict__ base, size_t off, const float (&s)[4]) {
+  *reinterpret_cast<float4 *>(base + off) = make_float4(s[0], s[1], s[2], s[3]);
+}
+__device__ __forceinline__ void zero4(float (&d)[4]) { d[0] = d[1] = d[2] = d[3] = 0.0f; }
+
+template <bool G>
+__device__ __forceinline__ void load_row(Row<G> &r, const IterArgs &a, size_t off) {
+  ld4(r.wx, a.I1wx, off);
+  ld4(r.wy, a.I1wy, off);
+  ld4(r.rh, a.rho, off);
+  ld4(r.u1, a.u1s, off);
+  ld4(r.u2, a.u2s, off);
+  if (G) ld4(r.u3, a.u3s, off);
+  if (a.p_zero) {
+    zero4(r.p11); zero4(r.p12); zero4(r.p21); zero4(r.p22);
+    if (G) { zero4(r.p31); zero4(r.p32); }
+  } else {
+    ld4(r.p11, a.p11s, off);
+    ld4(r.p12, a.p12s, off);
+    ld4(r.p21, a.p21s, off);
+    ld4(r.p22, a.p22s, off);
+    if (G) { ld4(r.p31, a.p31s, off); ld4(r.p32, a.p32s, off); }
+  }
+}
+
+// OpenCV `divergence` (tvl1flow.cu) at px k of this lane; pl = p1 at x-1, pu = p2 at y-1.
+__device__ __forceinline__ float divergence(float p1, float p1l, float p2, float p2u, int x,
+                                            int y) {
+  if (x > 0 && y > 0) return (p1 - p1l) + (p2 - p2u);
+  if (y > 0) return p1 + p2 - p2u;
+  if (x > 0) return p1 - p1l + p2;
+  return p1 + p2;
+}
+
+// estimateU for the 4 px of this lane on row y.  up* = p12/p22/p32 of row y-1.
+template <bool G>
+__device__ __forceinline__ void estimate_u(const Row<G> &r, const float (&up12)[4],
+                                           const float (&up22)[4], const float (&up32)[4],
+                                           int X0, int y, const IterArgs &a, float (&n1)[4],
+                                           float (&n2)[4], float (&n3)[4]) {
+  float l11[4], l21[4], l31[4];
+  l11[0] = __shfl_up(r.p11[3], 1);
+  l21[0] = __shfl_up(r.p21[3], 1);
+  if (G) l31[0] = __shfl_up(r.p31[3], 1);
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    l11[k] = r.p11[k - 1];
+    l21[k] = r.p21[k - 1];
+    if (G) l31[k] = r.p31[k - 1];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int x = X0 + k;
+    const float I1wxv = r.wx[k];
+    const float I1wyv = r.wy[k];
+    const float Ix2 = I1wxv * I1wxv;
+    const float Iy2 = I1wyv * I1wyv;
+    const float gradv = Ix2 + Iy2;
+    const float u1o = r.u1[k];
+    const float u2o = r.u2[k];
+    const float u3o = G ? r.u3[k] : 0.0f;
+    const float rho = r.rh[k] + (I1wxv * u1o + I1wyv * u2o) + a.gamma * u3o;
+    float d1 = 0.0f, d2 = 0.0f, d3 = 0.0f;
+    if (rho < -a.l_t * gradv) {
+      d1 = a.l_t * I1wxv;
+      d2 = a.l_t * I1wyv;
+      if (G) d3 = a.theta * a.gamma;
+    } else if (rho > a.l_t * gradv) {
+      d1 = -a.l_t * I1wxv;
+      d2 = -a.l_t * I1wyv;
+      if (G) d3 = -a.theta * a.gamma;
+    } else if (gradv > kFltEps) {
+      const float fi = -rho / gradv;
+      d1 = fi * I1wxv;
+      d2 = fi * I1wyv;
+      if (G) d3 = fi * a.gamma;
+    }
+    const float v1 = u1o + d1;
+    const float v2 = u2o + d2;
+    const float div1 = divergence(r.p11[k], l11[k], r.p12[k], up12[k], x, y);
+    const float div2 = divergence(r.p21[k], l21[k], r.p22[k], up22[k], x, y);
+    n1[k] = v1 + a.theta * div1;
+    n2[k] = v2 + a.theta * div2;
+    if (G) {
+      const float v3 = u3o + d3;
+      const float div3 = divergence(r.p31[k], l31[k], r.p32[k], up32[k], x, y);
+      n3[k] = v3 + a.theta * div3;
+    }
+  }
+}
+
+__device__ __forceinline__ float hypot_f(float a, float b) { return sqrtf(a * a + b * b); }
+
+// One projection component: p' = (p + taut * du) / ng, du from u at (x+1) and (y+1).
+__device__ __forceinline__ void dual_component(const float (&uc)[4], const float (&un)[4],
+                                               bool has_down, int X0, int W, float taut,
+                                               const float (&pa)[4], const float (&pb)[4],
+                                               float (&oa)[4], float (&ob)[4]) {
+  float ur[4];
+  ur[3] = __shfl_down(uc[0], 1);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) ur[k] = uc[k + 1];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int x = X0 + k;
+    const float right = (x + 1 < W) ? ur[k] : uc[k];
+    const float down = has_down ? un[k] : uc[k];
+    const float ux = right - uc[k];
+    const float uy = down - uc[k];
+    const float g = hypot_f(ux, uy);
+    const float ng = 1.0f + taut * g;
+    oa[k] = (pa[k] + taut * ux) / ng;
+    ob[k] = (pb[k] + taut * uy) / ng;
+  }
+}
+
+template <bool G>
+__global__ __launch_bounds__(kBlock) void k_iterate(IterArgs a) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+  const int seg = wave % a.segs;
+  const int strip = wave / a.segs;
+  const int y0 = strip * a.strip_rows;
+  double acc = 0.0;
+  if (y0 < a.H) {
+    const int y1 = imin(y0 + a.strip_rows, a.H);
+    const int X0 = seg * kSegPx - 4 + lane * 4;        // first px of this lane
+    const int xa = imin(imax(X0, 0), a.P - 4);         // clamped, 16-B aligned load column
+    const bool writer = lane >= 1 && lane <= kWave - 2 && X0 < a.W;
+
+    float up12[4], up22[4], up32[4];
+    if (y0 > 0 && !a.p_zero) {
+      const size_t off = (size_t)(y0 - 1) * a.P + xa;
+      ld4(up12, a.p12s, off);
+      ld4(up22, a.p22s, off);
+      if (G) ld4(up32, a.p32s, off);
+      else zero4(up32);
+    } else {
+      zero4(up12); zero4(up22); zero4(up32);
+    }
+    Row<G> cur;
+    load_row<G>(cur, a, (size_t)y0 * a.P + xa);
+    float c1[4], c2[4], c3[4];
+    estimate_u<G>(cur, up12, up22, up32, X0, y0, a, c1, c2, c3);
+
+    for (int y = y0; y < y1; ++y) {
+      const bool has_down = y + 1 < a.H;
+      Row<G> nxt;
+      float n1[4], n2[4], n3[4];
+      if (has_down) {
+        load_row<G>(nxt, a, (size_t)(y + 1) * a.P + xa);
+        estimate_u<G>(nxt, cur.p12, cur.p22, cur.p32, X0, y + 1, a, n1, n2, n3);
+      } else {  // last image row: forward difference in y is 0 (clamp)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { n1[k] = c1[k]; n2[k] = c2[k]; n3[k] = c3[k]; }
+      }
+      float q11[4], q12[4], q21[4], q22[4], q31[4], q32[4];
+      dual_component(c1, n1, has_down, X0, a.W, a.taut, cur.p11, cur.p12, q11, q12);
+      dual_component(c2, n2, has_down, X0, a.W, a.taut, cur.p21, cur.p22, q21, q22);
+      if (G) dual_component(c3, n3, has_down, X0, a.W, a.taut, cur.p31, cur.p32, q31, q32);
+      if (writer) {
+        const size_t off = (size_t)y * a.P + xa;
+        st4(a.u1d, off, c1);
+        st4(a.u2d, off, c2);
+        st4(a.p11d, off, q11);
+        st4(a.p12d, off, q12);
+        st4(a.p21d, off, q21);
+        st4(a.p22d, off, q22);
+        if (G) {
+          st4(a.u3d, off, c3);
+          st4(a.p31d, off, q31);
+          st4(a.p32d, off, q32);
+        }
+        if (a.calc_err) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (X0 + k < a.W) {
+              const float e1 = (cur.u1[k] - c1[k]) * (cur.u1[k] - c1[k]);
+              const float e2 = (cur.u2[k] - c2[k]) * (cur.u2[k] - c2[k]);
+              acc += (double)(e1 + e2);
+            }
+          }
+        }
+      }
+      if (has_down) {
+        cur = nxt;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { c1[k] = n1[k]; c2[k] = n2[k]; if (G) c3[k] = n3[k]; }
+      }
+    }
+  }
+  if (a.calc_err) {
+    __shared__ double red[kBlock / kWave];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+      for (int i = 0; i < kBlock / kWave; ++i) s += red[i];
+      a.partials[blockIdx.x] = s;
+    }
+  }
+}
+
+// K7: fixed-order sum of the per-block partials (one block).
+__global__ void k_reduce(const double *__restrict__ partials, int n, double *__restrict__ out) {
+  __shared__ double s[kBlock];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += kBlock) acc += partials[i];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = kBlock / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = s[0];
+}
+
+// ---------------------------------------------------------------- misc
+// Build-only median (cv::medianBlur CV_32F, ksize 3 or 5, BORDER_REPLICATE); blockIdx.z = component.
+__global__ void k_median(const float *__restrict__ s1, const float *__restrict__ s2, int W,
+                         int H, int P, int ksize, float *__restrict__ d1,
+                         float *__restrict__ d2) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const float *src = blockIdx.z == 0 ? s1 : s2;
+  float *dst = blockIdx.z == 0 ? d1 : d2;
+  const int r = ksize / 2;
+  float v[25];
+  int n = 0;
+  for (int dy = -r; dy <= r; ++dy)
+    for (int dx = -r; dx <= r; ++dx)
+      v[n++] = src[(size_t)imin(imax(y + dy, 0), H - 1) * P + imin(imax(x + dx, 0), W - 1)];
+  for (int i = 1; i < n; ++i) {
+    const float t = v[i];
+    int j = i - 1;
+    while (j >= 0 && v[j] > t) {
+      v[j + 1] = v[j];
+      --j;
+    }
+    v[j + 1] = t;
+  }
+  dst[(size_t)y * P + x] = v[n / 2];
+}
+
+// Final flow (u1[0], u2[0]) -> caller's pitched planar outputs (A.4 + cuda::split).
+__global__ void k_output(const float *__restrict__ u1, const float *__restrict__ u2, int W,
+                         int H, int P, float *__restrict__ ou, float *__restrict__ ov,
+                         size_t opitch) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  reinterpret_cast<float *>(reinterpret_cast<char *>(ou) + (size_t)y * opitch)[x] = u1[(size_t)y * P + x];
+  reinterpret_cast<float *>(reinterpret_cast<char *>(ov) + (size_t)y * opitch)[x] = u2[(size_t)y * P + x];
+}
+
+// solve_wrapper post-ops (optflow.cpp:445-473): map = flow + (x, y) (mode 1), then
+// zero where I1 <= 1 (threshold THRESH_BINARY_INV + setTo(0, mask)).
+__global__ void k_postprocess(float *__restrict__ u, float *__restrict__ v, size_t fp,
+                              const uint8_t *__restrict__ I1, size_t p1, int W, int H,
+                              int mode) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  float *ur = reinterpret_cast<float *>(reinterpret_cast<char *>(u) + (size_t)y * fp);
+  float *vr = reinterpret_cast<float *>(reinterpret_cast<char *>(v) + (size_t)y * fp);
+  float a = ur[x], b = vr[x];
+  if (mode == 1) {
+    a = a + (float)x;
+    b = b + (float)y;
+  }
+  if (I1[(size_t)y * p1 + x] <= 1) {
+    a = 0.0f;
+    b = 0.0f;
+  }
+  ur[x] = a;
+  vr[x] = b;
+}
+
+}  // namespace tvl1k

@@ -1,0 +1,262 @@
+"""ctypes mirror of include/tvl1.h (the C-ABI boundary).
+
+This is the binding a Python caller (tests, bench.py) uses; the production
+caller is the C++ `optflow` CLI (fibsem-optflow_amd/cli/optflow.cpp), which
+links the same library.  Mirrors the reference boundary
+/root/reference/src/optflow.cpp:516-520 (TVL1_solve) — see include/tvl1.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # fibsem-optflow_amd/
+REPO_ROOT = PKG_ROOT.parent
+ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
+ORACLE_SO = REPO_ROOT / "oracle" / "liboracle_tvl1.so"
+
+TVL1_MAX_LEVELS = 32
+STATUS = {0: "TVL1_OK", 1: "TVL1_EINVAL", 2: "TVL1_ESIZE", 3: "TVL1_EHIP",
+          4: "TVL1_ENOMEM", 5: "TVL1_ENODEV"}
+
+
+class TVL1Params(C.Structure):
+    _fields_ = [
+        ("tau", C.c_double),
+        ("lambda_", C.c_double),
+        ("theta", C.c_double),
+        ("nscales", C.c_int32),
+        ("warps", C.c_int32),
+        ("epsilon", C.c_double),
+        ("iterations", C.c_int32),
+        ("scale_step", C.c_double),
+        ("gamma", C.c_double),
+        ("use_initial_flow", C.c_int32),
+        ("median_filtering", C.c_int32),
+    ]
+
+
+class TVL1Stats(C.Structure):
+    _fields_ = [
+        ("levels", C.c_int32),
+        ("level_width", C.c_int32 * TVL1_MAX_LEVELS),
+        ("level_height", C.c_int32 * TVL1_MAX_LEVELS),
+        ("level_iterations", C.c_int64 * TVL1_MAX_LEVELS),
+        ("iterations_total", C.c_int64),
+        ("checks_total", C.c_int64),
+        ("algorithmic_bytes", C.c_double),
+        ("warp_iterations", C.POINTER(C.c_int32)),
+        ("warp_iterations_capacity", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+# generate_TV_args defaults, /root/reference/src/optflow.cpp:503-512
+DEFAULTS = dict(tau=0.25, lambda_=0.05, theta=0.3, nscales=10, warps=5, epsilon=0.01,
+                iterations=300, scale_step=0.8, gamma=0.0, use_initial_flow=0,
+                median_filtering=1)
+
+# JSON key -> struct field (JSON keys are the reference's, optflow.cpp:503-512)
+JSON_KEYS = {"tau": "tau", "lambda": "lambda_", "theta": "theta", "nscales": "nscales",
+             "warps": "warps", "epsilon": "epsilon", "iterations": "iterations",
+             "scaleStep": "scale_step", "gamma": "gamma", "useInitialFlow": "use_initial_flow",
+             "medianFiltering": "median_filtering"}
+
+
+def make_params(**kw) -> TVL1Params:
+    d = dict(DEFAULTS)
+    for k, v in kw.items():
+        k = JSON_KEYS.get(k, k)
+        if k == "lambda":
+            k = "lambda_"
+        if k not in d:
+            raise KeyError(f"unknown TV-L1 parameter {k!r}")
+        d[k] = v
+    p = TVL1Params()
+    for k, v in d.items():
+        setattr(p, k, v)
+    return p
+
+
+def stats_dict(st: TVL1Stats, warps: int | None = None) -> dict:
+    L = st.levels
+    out = {
+        "levels": L,
+        "sizes": [(st.level_width[i], st.level_height[i]) for i in range(L)],
+        "level_iterations": [int(st.level_iterations[i]) for i in range(L)],
+        "iterations_total": int(st.iterations_total),
+        "checks_total": int(st.checks_total),
+        "algorithmic_bytes": float(st.algorithmic_bytes),
+    }
+    return out
+
+
+def _u8_ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def _f32_ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class Library:
+    """Loads either the HIP engine or the oracle behind the same host call."""
+
+    def __init__(self, path: Path):
+        if not Path(path).exists():
+            raise FileNotFoundError(f"{path} not built (run __graft_entry__.build())")
+        self.path = Path(path)
+        self.lib = C.CDLL(str(path))
+
+
+def load_oracle() -> C.CDLL:
+    """TEST INFRASTRUCTURE: the CPU restatement (oracle/).  Only tests, smoke()
+    and bench.py's cpu_baseline leg call this."""
+    lib = Library(ORACLE_SO).lib
+    lib.orc_tvl1_calc.restype = C.c_int
+    lib.orc_tvl1_calc.argtypes = [C.POINTER(TVL1Params), C.POINTER(C.c_uint8), C.c_size_t,
+                                  C.POINTER(C.c_uint8), C.c_size_t, C.c_int, C.c_int,
+                                  C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_size_t,
+                                  C.POINTER(TVL1Stats)]
+    lib.orc_num_threads.restype = C.c_int
+    lib.orc_set_num_threads.argtypes = [C.c_int]
+    return lib
+
+
+def load_engine() -> C.CDLL:
+    """The product: libtvl1_hip.so (HIP kernels for gfx950 + C-ABI).  Raises
+    if it was not built — there is no CPU fallback."""
+    lib = Library(ENGINE_SO).lib
+    lib.tvl1_params_default.argtypes = [C.POINTER(TVL1Params)]
+    lib.tvl1_params_default.restype = None
+    lib.tvl1_create.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.POINTER(TVL1Params)]
+    lib.tvl1_create.restype = C.c_int
+    lib.tvl1_set_params.argtypes = [C.c_void_p, C.POINTER(TVL1Params)]
+    lib.tvl1_set_params.restype = C.c_int
+    lib.tvl1_calc.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                              C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_size_t,
+                              C.POINTER(TVL1Stats), C.c_void_p]
+    lib.tvl1_calc.restype = C.c_int
+    lib.tvl1_calc_host.argtypes = [C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t,
+                                   C.POINTER(C.c_uint8), C.c_size_t, C.c_int32, C.c_int32,
+                                   C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_size_t,
+                                   C.POINTER(TVL1Stats)]
+    lib.tvl1_calc_host.restype = C.c_int
+    lib.tvl1_postprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                     C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, C.c_int32,
+                                     C.c_void_p]
+    lib.tvl1_postprocess.restype = C.c_int
+    lib.tvl1_destroy.argtypes = [C.c_void_p]
+    lib.tvl1_destroy.restype = None
+    lib.tvl1_last_error.argtypes = [C.c_void_p]
+    lib.tvl1_last_error.restype = C.c_char_p
+    lib.tvl1_abi_version.restype = C.c_int32
+    lib.tvl1_device_count.restype = C.c_int32
+    return lib
+
+
+class TVL1Error(RuntimeError):
+    pass
+
+
+def oracle_calc(I0: np.ndarray, I1: np.ndarray, params: TVL1Params | None = None,
+                warp_iters: bool = True, threads: int | None = None):
+    """Run the CPU restatement on host u8 images; returns (u, v, stats, warp_iters)."""
+    lib = load_oracle()
+    if threads:
+        lib.orc_set_num_threads(int(threads))
+    params = params or make_params()
+    I0 = np.ascontiguousarray(I0, dtype=np.uint8)
+    I1 = np.ascontiguousarray(I1, dtype=np.uint8)
+    h, w = I0.shape
+    u = np.zeros((h, w), np.float32)
+    v = np.zeros((h, w), np.float32)
+    st = TVL1Stats()
+    wi = None
+    if warp_iters:
+        cap = TVL1_MAX_LEVELS * max(1, params.warps)
+        wi = np.full(cap, -1, np.int32)
+        st.warp_iterations = wi.ctypes.data_as(C.POINTER(C.c_int32))
+        st.warp_iterations_capacity = cap
+    rc = lib.orc_tvl1_calc(C.byref(params), _u8_ptr(I0), w, _u8_ptr(I1), w, w, h,
+                           _f32_ptr(u), _f32_ptr(v), 4 * w, C.byref(st))
+    if rc != 0:
+        raise TVL1Error(f"oracle: {STATUS.get(rc, rc)}")
+    sd = stats_dict(st)
+    if wi is not None:
+        wi = wi[: sd["levels"] * params.warps].reshape(sd["levels"], params.warps)
+    return u, v, sd, wi
+
+
+class Engine:
+    """Host-side handle on the HIP engine (one ctx per device)."""
+
+    def __init__(self, params: TVL1Params | None = None, device: int = 0):
+        self.lib = load_engine()
+        self.params = params or make_params()
+        self.ctx = C.c_void_p()
+        rc = self.lib.tvl1_create(C.byref(self.ctx), int(device), C.byref(self.params))
+        if rc != 0:
+            raise TVL1Error(f"tvl1_create: {STATUS.get(rc, rc)}: "
+                            f"{self.lib.tvl1_last_error(None).decode()}")
+
+    def set_params(self, params: TVL1Params):
+        self.params = params
+        self._check(self.lib.tvl1_set_params(self.ctx, C.byref(params)), "tvl1_set_params")
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.tvl1_last_error(self.ctx)
+            raise TVL1Error(f"{what}: {STATUS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    def calc_host(self, I0: np.ndarray, I1: np.ndarray, warp_iters: bool = True):
+        I0 = np.ascontiguousarray(I0, dtype=np.uint8)
+        I1 = np.ascontiguousarray(I1, dtype=np.uint8)
+        h, w = I0.shape
+        if I1.shape != I0.shape:
+            raise ValueError("I0 and I1 must have the same size")
+        u = np.zeros((h, w), np.float32)
+        v = np.zeros((h, w), np.float32)
+        st = TVL1Stats()
+        wi = None
+        if warp_iters:
+            cap = TVL1_MAX_LEVELS * max(1, self.params.warps)
+            wi = np.full(cap, -1, np.int32)
+            st.warp_iterations = wi.ctypes.data_as(C.POINTER(C.c_int32))
+            st.warp_iterations_capacity = cap
+        rc = self.lib.tvl1_calc_host(self.ctx, _u8_ptr(I0), w, _u8_ptr(I1), w, w, h,
+                                     _f32_ptr(u), _f32_ptr(v), 4 * w, C.byref(st))
+        self._check(rc, "tvl1_calc_host")
+        sd = stats_dict(st)
+        if wi is not None:
+            wi = wi[: sd["levels"] * self.params.warps].reshape(sd["levels"], self.params.warps)
+        return u, v, sd, wi
+
+    def calc_device(self, dI0: int, pitch0: int, dI1: int, pitch1: int, w: int, h: int,
+                    du: int, dv: int, flow_pitch: int, stream: int = 0, stats: bool = True):
+        st = TVL1Stats() if stats else None
+        rc = self.lib.tvl1_calc(self.ctx, C.c_void_p(dI0), pitch0, C.c_void_p(dI1), pitch1,
+                                w, h, C.c_void_p(du), C.c_void_p(dv), flow_pitch,
+                                C.byref(st) if st is not None else None,
+                                C.c_void_p(stream) if stream else None)
+        self._check(rc, "tvl1_calc")
+        return stats_dict(st) if st is not None else None
+
+    def close(self):
+        if self.ctx:
+            self.lib.tvl1_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def epe(u, v, u_ref, v_ref) -> np.ndarray:
+    """Per-pixel end-point error."""
+    return np.sqrt((u.astype(np.float64) - u_ref) ** 2 + (v.astype(np.float64) - v_ref) ** 2)

@@ -1,0 +1,152 @@
+/*
+ * tvl1.h — C-ABI boundary of the MI355X-native dense TV-L1 optical-flow engine.
+ *
+ * This header is the drop-in replacement for the reference's single solver
+ * call site:
+ *
+ *   reference  src/optflow.h:31 / src/optflow.cpp:516-520
+ *     void TVL1_solve(cv::cuda::GpuMat& frame0, cv::cuda::GpuMat& frame1,
+ *                     cv::cuda::GpuMat& output, const Json::Value& args);
+ *   which does
+ *     cv::cuda::OpticalFlowDual_TVL1::create(tau, lambda, theta, nscales, warps,
+ *                                            epsilon, iterations, scaleStep, gamma)
+ *       ->calc(frame0, frame1, output);                 (OpenCV 3.4.1, not vendored)
+ *
+ * Mapping (one row per reference concept):
+ *   OpticalFlowDual_TVL1::create(...)       -> tvl1_create(&ctx, device, &params)
+ *   solver->calc(I0, I1, flow) on GpuMats   -> tvl1_calc(ctx, dI0, pitch0, dI1, pitch1, w, h,
+ *                                                       du, dv, flow_pitch, &stats, stream)
+ *   cuda::split(flow) (optflow.cpp:404)     -> outputs are already planar (u, v)
+ *   solver destruction                      -> tvl1_destroy(ctx)
+ *   cv::Exception (CV_Assert)               -> tvl1_status return code + tvl1_last_error(ctx)
+ *   post-ops optflow.cpp:445-473            -> tvl1_postprocess(...) (map grid add + I1<=1 mask)
+ *   generate_TV_args defaults :500-514      -> tvl1_params_default(&params)
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no HIP, torch or OpenCV types.  `stream` is a
+ *     hipStream_t passed as void* (NULL = the default stream).
+ *   - All pitches are in BYTES (OpenCV GpuMat::step convention).
+ *   - Inputs are 8-bit unsigned grayscale (CV_8UC1, IMREAD_GRAYSCALE, optflow.cpp:106);
+ *     outputs are planar float32 u (x displacement) and v (y displacement) such
+ *     that I1(x+u, y+v) ~= I0(x, y)  (flow points from frame0=p to frame1=q).
+ *   - Errors never throw across the ABI: every entry point returns tvl1_status.
+ *   - A ctx is not thread-safe.  Distinct ctxs (one per device per host thread)
+ *     are independent.  tvl1_calc is asynchronous w.r.t. the host only where the
+ *     stats say so: the convergence test reads the residual on the host exactly
+ *     where OpenCV does (a device->host read on "check" iterations), so the call
+ *     returns after the solve has been fully enqueued; outputs are valid after a
+ *     stream synchronize (tvl1_calc_host synchronizes for you).
+ */
+#ifndef FIBSEM_OPTFLOW_AMD_TVL1_H
+#define FIBSEM_OPTFLOW_AMD_TVL1_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TVL1_ABI_VERSION 1
+#define TVL1_MAX_LEVELS 32
+
+typedef enum tvl1_status {
+  TVL1_OK = 0,
+  TVL1_EINVAL = 1, /* bad argument (null pointer, nscales <= 0, bad pitch ...)  */
+  TVL1_ESIZE = 2,  /* size mismatch / image smaller than 1x1 / too large       */
+  TVL1_EHIP = 3,   /* a HIP runtime call failed (message in tvl1_last_error)    */
+  TVL1_ENOMEM = 4, /* device or host allocation failed                          */
+  TVL1_ENODEV = 5  /* no usable gfx950 device / extension not built             */
+} tvl1_status;
+
+/* The nine cv::cuda::OpticalFlowDual_TVL1::create() arguments (optflow.cpp:518)
+ * plus the two build-only additions listed in SURVEY Appendix B. */
+typedef struct tvl1_params {
+  double tau;          /* 0.25  optflow.cpp:503 */
+  double lambda;       /* 0.05  optflow.cpp:504 */
+  double theta;        /* 0.3   optflow.cpp:505 */
+  int32_t nscales;     /* 10    optflow.cpp:506 */
+  int32_t warps;       /* 5     optflow.cpp:507 */
+  double epsilon;      /* 0.01  optflow.cpp:508 */
+  int32_t iterations;  /* 300   optflow.cpp:509 */
+  double scale_step;   /* 0.8   optflow.cpp:510 */
+  double gamma;        /* 0.0   optflow.cpp:511 */
+  int32_t use_initial_flow; /* read at optflow.cpp:512 but NOT passed to create() (:518): ignored, as in the reference */
+  int32_t median_filtering; /* build-only: 1 = off (reference behaviour); 3 or 5 = median of u,v before each warp */
+} tvl1_params;
+
+/* Per-call statistics.  Valid after tvl1_calc returns (host-side counters). */
+typedef struct tvl1_stats {
+  int32_t levels;                           /* effective pyramid depth (OpenCV mutates nscales_) */
+  int32_t level_width[TVL1_MAX_LEVELS];
+  int32_t level_height[TVL1_MAX_LEVELS];
+  int64_t level_iterations[TVL1_MAX_LEVELS]; /* executed iterations summed over warps */
+  int64_t iterations_total;
+  int64_t checks_total;                     /* iterations that evaluated the residual (cuda::sum) */
+  double algorithmic_bytes;                 /* SURVEY 8(d) byte model with executed counts */
+  /* Optional caller-owned buffer: executed iterations per (level, warp), indexed
+   * [level * warps + warp], level 0 = finest.  Left untouched when NULL. */
+  int32_t *warp_iterations;
+  int32_t warp_iterations_capacity;         /* number of int32 slots in warp_iterations */
+  int32_t reserved;
+} tvl1_stats;
+
+typedef struct tvl1_ctx tvl1_ctx;
+
+/* Fill params with the reference defaults of generate_TV_args (optflow.cpp:500-514). */
+void tvl1_params_default(tvl1_params *params);
+
+/* Create a solver bound to HIP device `device` (ordinal).  Replaces
+ * OpticalFlowDual_TVL1::create (optflow.cpp:518).  Scratch grows on demand. */
+tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params);
+
+/* Replace the solver parameters of an existing ctx (the reference re-creates the
+ * solver per call, optflow.cpp:518; this avoids re-allocating scratch). */
+tvl1_status tvl1_set_params(tvl1_ctx *ctx, const tvl1_params *params);
+
+/* Solve I0 -> I1 on DEVICE memory.  Replaces solver->calc(frame0, frame1, flow)
+ * (optflow.cpp:519) followed by cuda::split (optflow.cpp:404).
+ *   I0, I1 : device u8 images, row pitch pitch0/pitch1 bytes (ROI views allowed)
+ *   u, v   : device f32 outputs, row pitch flow_pitch bytes
+ *   stats  : may be NULL
+ *   stream : hipStream_t as void*, NULL = default stream            */
+tvl1_status tvl1_calc(tvl1_ctx *ctx,
+                      const uint8_t *I0, size_t pitch0,
+                      const uint8_t *I1, size_t pitch1,
+                      int32_t width, int32_t height,
+                      float *u, float *v, size_t flow_pitch,
+                      tvl1_stats *stats, void *stream);
+
+/* Same on HOST memory: upload, solve, download, synchronize.
+ * (GpuMat::upload optflow.cpp:315-316 ... download :475-476) */
+tvl1_status tvl1_calc_host(tvl1_ctx *ctx,
+                           const uint8_t *I0, size_t pitch0,
+                           const uint8_t *I1, size_t pitch1,
+                           int32_t width, int32_t height,
+                           float *u, float *v, size_t flow_pitch,
+                           tvl1_stats *stats);
+
+/* Output post-processing of solve_wrapper (optflow.cpp:445-473), in place on
+ * device u, v:  mode 0 = "flow" (unchanged), 1 = "map" (u += x, v += y);
+ * then u = v = 0 wherever I1 <= 1 (cuda::threshold THRESH_BINARY_INV + setTo). */
+tvl1_status tvl1_postprocess(tvl1_ctx *ctx, float *u, float *v, size_t flow_pitch,
+                             const uint8_t *I1, size_t pitch1,
+                             int32_t width, int32_t height, int32_t mode, void *stream);
+
+/* Destroy a ctx and free its device scratch. */
+void tvl1_destroy(tvl1_ctx *ctx);
+
+/* Last error message of ctx (or of the last failed tvl1_create when ctx==NULL). */
+const char *tvl1_last_error(const tvl1_ctx *ctx);
+
+/* ABI version (TVL1_ABI_VERSION) — lets an FFI binding check what it loaded. */
+int32_t tvl1_abi_version(void);
+
+/* Number of visible HIP devices (0 when no GPU); never initialises a context. */
+int32_t tvl1_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FIBSEM_OPTFLOW_AMD_TVL1_H */

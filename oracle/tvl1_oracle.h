@@ -1,0 +1,78 @@
+/*
+ * tvl1_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's solver path: the
+ * OpenCV 3.4.1 `cv::cuda::OpticalFlowDual_TVL1` called at
+ * /root/reference/src/optflow.cpp:516-520 plus the solve_wrapper post-ops
+ * (optflow.cpp:445-473).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library; the product path never does.
+ *
+ * PARITY UNPINNED: the reference ships no tests, fixtures or golden vectors and
+ * OpenCV 3.4.1 (a third-party dependency pinned at singularity/optflow.def:22-23)
+ * is absent from this image, so this restatement is pinned only by the
+ * known-answer tests in tests/ and by fixtures it generated itself.
+ */
+#ifndef TVL1_ORACLE_H
+#define TVL1_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../include/tvl1.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- stage functions (packed row-major buffers, pitch == width) ---- */
+
+/* K1 GpuMat::convertTo(CV_32F, 1.0) */
+void orc_convert_u8(const uint8_t *src, size_t pitch, int w, int h, float *dst);
+
+/* K2/K9 cuda::resize INTER_LINEAR, corner-aligned (fx, fy = src/dst step as float) */
+void orc_resize_linear(const float *src, int sw, int sh, float *dst, int dw, int dh,
+                       float fx, float fy);
+
+/* pyramid sizes exactly as calcImpl builds them; returns effective level count */
+int orc_pyramid_sizes(int w, int h, int nscales, double scale_step, int *ws, int *hs);
+
+/* K3 centeredGradient */
+void orc_centered_gradient(const float *I, int w, int h, float *Ix, float *Iy);
+
+/* K5 warpBackward (I1w is not produced: nothing downstream reads it) */
+void orc_warp_backward(const float *I0, const float *I1, const float *I1x, const float *I1y,
+                       const float *u1, const float *u2, int w, int h,
+                       float *I1wx, float *I1wy, float *grad, float *rho_c);
+
+/* K6 estimateU (in place on u1,u2[,u3]); returns sum(diff) in double when calc_error */
+double orc_estimate_u(const float *I1wx, const float *I1wy, const float *grad,
+                      const float *rho_c, const float *p11, const float *p12,
+                      const float *p21, const float *p22, const float *p31,
+                      const float *p32, float *u1, float *u2, float *u3, int w, int h,
+                      float l_t, float theta, float gamma, int calc_error);
+
+/* K8 estimateDualVariables (in place on p) */
+void orc_estimate_dual(const float *u1, const float *u2, const float *u3, float *p11,
+                       float *p12, float *p21, float *p22, float *p31, float *p32, int w,
+                       int h, float taut, float gamma);
+
+/* build-only median filter (cv::medianBlur semantics, BORDER_REPLICATE, k = 3 or 5) */
+void orc_median(const float *src, int w, int h, int k, float *dst);
+
+/* ---- whole solve: same contract as tvl1_calc_host (include/tvl1.h) ---- */
+int orc_tvl1_calc(const tvl1_params *params, const uint8_t *I0, size_t pitch0,
+                  const uint8_t *I1, size_t pitch1, int w, int h, float *u, float *v,
+                  size_t flow_pitch, tvl1_stats *stats);
+
+/* solve_wrapper post-ops (optflow.cpp:445-473) on host buffers */
+void orc_postprocess(float *u, float *v, size_t flow_pitch, const uint8_t *I1, size_t pitch1,
+                     int w, int h, int mode);
+
+/* number of OpenMP threads the oracle uses (1 when built without OpenMP) */
+int orc_num_threads(void);
+void orc_set_num_threads(int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,67 @@
+"""HIP engine vs the oracle (CPU restatement of OpenCV 3.4.1 CUDA TV-L1).
+
+Bar: identical per-warp iteration counts (the data-dependent stopping rule of
+procOneScale) and EPE <= 1e-3 px (north_star tolerance); in practice the two
+evaluate the same IEEE float32 operations and agree bit for bit.
+"""
+import numpy as np
+import pytest
+
+from optflow_amd import capi, synth
+
+pytestmark = pytest.mark.gpu
+
+EPE_TOL = 1e-3  # px, BASELINE.json north_star
+
+
+@pytest.fixture(scope="module")
+def engine(built):
+    return capi.Engine(capi.make_params())
+
+
+CASES = [
+    # (W, H, seed, params)
+    (64, 48, 1, dict(nscales=5, warps=3)),
+    (17, 16, 2, dict(nscales=3, warps=2)),
+    (33, 19, 3, dict(nscales=4, warps=3)),
+    (128, 96, 4, dict()),                        # reference defaults (nscales 10, warps 5)
+    (250, 131, 5, dict(nscales=5, warps=5)),     # odd width, > one wave segment
+    (512, 512, 6, dict(nscales=5, warps=30)),    # benchmark parameters, small frame
+    (300, 77, 7, dict(epsilon=0.0, iterations=7, nscales=3, warps=2)),  # fixed-work mode
+    (96, 64, 8, dict(gamma=0.2, nscales=4, warps=3)),                  # gamma != 0 (A.5)
+    (96, 64, 9, dict(median_filtering=5, nscales=4, warps=3)),         # build-only median
+    (96, 64, 10, dict(median_filtering=3, nscales=4, warps=3)),
+]
+
+
+@pytest.mark.parametrize("W,H,seed,kw", CASES)
+def test_engine_matches_oracle(engine, W, H, seed, kw):
+    I0, I1 = synth.gen_pair(W, H, seed=seed)
+    p = capi.make_params(**kw)
+    engine.set_params(p)
+    u, v, st, wi = engine.calc_host(I0, I1)
+    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    assert st["levels"] == sr["levels"]
+    assert st["sizes"] == sr["sizes"]
+    np.testing.assert_array_equal(wi, wr)
+    e = capi.epe(u, v, ur, vr)
+    assert float(e.max()) <= EPE_TOL, f"max EPE {e.max()}"
+    # bit-exactness is expected (same IEEE ops, no FMA); report if it ever drifts
+    assert np.array_equal(u, ur) and np.array_equal(v, vr), \
+        f"not bit-exact: max|du|={np.abs(u-ur).max()} max|dv|={np.abs(v-vr).max()}"
+
+
+def test_identity_pair_gives_zero_flow(engine):
+    I0, _ = synth.gen_pair(80, 60, seed=3)
+    engine.set_params(capi.make_params(nscales=4, warps=3))
+    u, v, st, wi = engine.calc_host(I0, I0)
+    assert np.all(u == 0) and np.all(v == 0)
+    assert np.all(wi == 2)   # error 0 at the first check (n = 1)
+
+
+def test_constant_images_give_zero_flow(engine):
+    I0 = np.full((40, 70), 100, np.uint8)
+    I1 = np.full((40, 70), 140, np.uint8)
+    engine.set_params(capi.make_params(nscales=3, warps=2))
+    u, v, _, _ = engine.calc_host(I0, I1)
+    assert np.all(u == 0) and np.all(v == 0)
