@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""bench.py — slice-pairs/s of the MI355X TV-L1 engine on BASELINE.json's workload.
+
+Workload (BASELINE.json configs[1], SURVEY 8(d) "C2"): one synthetic 6144x4096 u8
+slice pair, nscales 5, warps 30, iterations 300, epsilon 0.01 (other TV-L1
+parameters at the reference defaults, optflow.cpp:503-512).  A "step" is one full
+solve of that pair through the C-ABI (tvl1_calc on device buffers): pyramid,
+30 warps per level, the data-dependent primal-dual iterations and the final flow.
+Inputs are resident in HBM before the timed region starts.
+
+Multi-GPU: slice pairs are independent, so each rank (one process
+per GPU) solves its own pair every step: weak scaling, no data-path collective.
+torch.distributed (nccl = RCCL) is used only for the start/stop barrier and the
+max-over-ranks reduction of the elapsed time.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+  roofline: dominant kernel = the fused primal-dual iteration (k_iterate).
+            achieved = its algorithmic bytes (planes each launch must move, see
+            DESIGN.md) / its HIP-event time, summed over every launch in the
+            timed region; peak = 8000 GB/s (MI355X HBM3E spec).
+  cpu_baseline: the oracle (CPU restatement, oracle/) timed on this host on a
+            bounded sample (a 3072x2048 crop of the same pair, same parameters),
+            extrapolated to the full frame by pixel count.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "fibsem-optflow_amd"))
+
+HBM_PEAK_GBS = 8000.0
+METRIC = "slice-pairs/sec (6k×4k, 5 scales, 30 warps) at 1/2/4/8 GPUs; % HBM roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=6144)
+    ap.add_argument("--height", type=int, default=4096)
+    ap.add_argument("--nscales", type=int, default=5)
+    ap.add_argument("--warps", type=int, default=30)
+    ap.add_argument("--iterations", type=int, default=300)
+    ap.add_argument("--epsilon", type=float, default=0.01)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", default="3072x2048")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="skip per-kernel HIP events (roofline fields become null)")
+    return ap.parse_args()
+
+
+def cpu_baseline(I0, I1, params, sample: str):
+    """Oracle (CPU restatement of OpenCV 3.4.1 CUDA TV-L1) on a bounded crop."""
+    import numpy as np
+    from optflow_amd import capi
+    sw, sh = (int(t) for t in sample.lower().split("x"))
+    H, W = I0.shape
+    sw, sh = min(sw, W), min(sh, H)
+    a = np.ascontiguousarray(I0[:sh, :sw])
+    b = np.ascontiguousarray(I1[:sh, :sw])
+    lib = capi.load_oracle()
+    threads = int(lib.orc_num_threads())
+    t0 = time.perf_counter()
+    _, _, st, _ = capi.oracle_calc(a, b, params, warp_iters=False)
+    dt = time.perf_counter() - t0
+    scale = (W * H) / float(sw * sh)
+    return {
+        "value": 1.0 / (dt * scale),
+        "unit": "slice-pairs/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle/ CPU restatement, {threads} OpenMP threads, one {sw}x{sh} crop of "
+                   f"the benchmark pair, same TV-L1 parameters ({st['iterations_total']} "
+                   f"iterations over {st['levels']} levels) in {dt:.2f} s, extrapolated "
+                   f"x{scale:.2f} by pixel count to one {W}x{H} pair"),
+    }
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(local_rank)
+
+    from optflow_amd import capi, synth
+
+    W, H = args.width, args.height
+    params = capi.make_params(nscales=args.nscales, warps=args.warps,
+                              iterations=args.iterations, epsilon=args.epsilon)
+    # each rank gets its own slice pair of the synthetic stack (z = rank+1 vs base)
+    I0h, I1h = synth.gen_pair(W, H, seed=0x5EED, z=1 + rank)
+    dev = torch.device("cuda", local_rank)
+    I0 = torch.from_numpy(I0h).to(dev)
+    I1 = torch.from_numpy(I1h).to(dev)
+    u = torch.empty((H, W), dtype=torch.float32, device=dev)
+    v = torch.empty((H, W), dtype=torch.float32, device=dev)
+
+    eng = capi.Engine(params, device=local_rank)
+    eng.set_profiling(not args.no_kernel_timing)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        return eng.calc_device(I0.data_ptr(), W, I1.data_ptr(), W, W, H, u.data_ptr(),
+                               v.data_ptr(), 4 * W, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        stats.append(step())
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # aggregate per-kernel timing of this rank (rank 0 reports its own kernel roofline)
+    k_ms = sum(s["kernel_ms"][0] for s in stats)
+    k_bytes = sum(s["kernel_bytes"][0] for s in stats)
+    k_launch = sum(s["kernel_launches"][0] for s in stats)
+    pair_bytes = sum(s["algorithmic_bytes"] for s in stats) / len(stats)
+    iters = [s["iterations_total"] for s in stats]
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    value = world * args.steps / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+    roof = None
+    if k_ms > 0:
+        achieved = k_bytes / (k_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_iterate (fused estimateU + estimateDualVariables + residual partials)",
+                "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
+                "algorithmic_bytes_per_launch": round(k_bytes / k_launch),
+                "kernel_share_of_step": round(k_ms / (1e3 * elapsed), 4)}
+    out = {
+        "metric": METRIC,
+        "value": round(value, 4),
+        "unit": "slice-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": (f"C2: one {W}x{H} u8 slice pair per GPU per step, nscales "
+                         f"{args.nscales}, warps {args.warps}, iterations {args.iterations}, "
+                         f"epsilon {args.epsilon} (reference defaults otherwise)"),
+            "pair": f"{W}x{H}",
+            "parallelism": f"pairs sharded over {world} GPU(s), no data-path collective",
+            "iterations_per_pair": iters[0],
+            "pair_algorithmic_GB": round(pair_bytes / 1e9, 2),
+            # SURVEY 8(d) whole-pair byte model / step time, per GPU
+            "pair_roofline_frac": round(pair_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4),
+        },
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(I0h, I1h, params, args.cpu_sample)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

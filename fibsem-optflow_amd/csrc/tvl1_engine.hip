@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/tvl1.h"
 #include "tvl1_kernels.hpp"
@@ -60,7 +61,40 @@ struct tvl1_ctx {
   int partials_cap = 0;
   double *red = nullptr;
   double *pinned = nullptr;  // host-pinned residual landing slot
+
+  // optional per-kernel-class HIP-event timing (tvl1_set_profiling)
+  bool profiling = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  struct Mark {
+    int cls;
+    size_t a, b;
+    double bytes;
+  };
+  std::vector<Mark> marks;
 };
+
+static size_t prof_begin(tvl1_ctx *c, hipStream_t st) {
+  if (!c->profiling) return 0;
+  if (c->ev_used + 2 > c->ev_pool.size()) {
+    for (int i = 0; i < 64; ++i) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) break;
+      c->ev_pool.push_back(e);
+    }
+  }
+  if (c->ev_used + 2 > c->ev_pool.size()) return 0;
+  const size_t a = c->ev_used++;
+  (void)hipEventRecord(c->ev_pool[a], st);
+  return a + 1;  // 0 = not recording
+}
+
+static void prof_end(tvl1_ctx *c, hipStream_t st, size_t tok, int cls, double bytes) {
+  if (!c->profiling || tok == 0) return;
+  const size_t b = c->ev_used++;
+  (void)hipEventRecord(c->ev_pool[b], st);
+  c->marks.push_back({cls, tok - 1, b, bytes});
+}
 
 static tvl1_status set_err(tvl1_ctx *c, tvl1_status st, const char *fmt, ...) {
   char buf[512];
@@ -219,6 +253,11 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   const int L = g.L;
   const bool gam = g.gamma;
 
+  if (c->profiling) {
+    c->ev_used = 0;
+    c->marks.clear();
+  }
+  size_t tk = prof_begin(c, st);
   // [A.1] convertTo
   hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 2), kBlk2, 0, st, I0, pitch0, I1, pitch1,
                      c->I0s[0], c->I1s[0], W, H, g.ps[0]);
@@ -228,6 +267,11 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     hipLaunchKernelGGL(k_resize_down2, grid2(g.ws[s], g.hs[s], 2), kBlk2, 0, st, c->I0s[s - 1],
                        c->I1s[s - 1], g.ws[s - 1], g.hs[s - 1], g.ps[s - 1], c->I0s[s],
                        c->I1s[s], g.ws[s], g.hs[s], g.ps[s], fdown, fdown);
+  {
+    double b = (double)W * H * (2 + 8);
+    for (int s = 1; s < L; ++s) b += (double)g.ws[s] * g.hs[s] * 8 + (double)g.ws[s - 1] * g.hs[s - 1] * 8;
+    prof_end(c, st, tk, 2, b);
+  }
   HIP_TRY(c, hipGetLastError());
 
   int ui = 0, pi = 0;  // ping-pong indices of the u and p buffer sets
@@ -251,7 +295,10 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   for (int s = L - 1; s >= 0; --s) {
     const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
     const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
+    const double Nl = (double)lw * lh;
+    tk = prof_begin(c, st);
     hipLaunchKernelGGL(k_gradient, grid2(lw, lh), kBlk2, 0, st, c->I1s[s], lw, lh, P, c->G);
+    prof_end(c, st, tk, 2, Nl * (4 + 16));
     bool p_zero = true;  // p = 0 at the start of every level (setTo(0) in procOneScale)
 
     IterArgs a{};
@@ -280,8 +327,10 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         }
         ui ^= 1;
       }
+      tk = prof_begin(c, st);
       hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[ui][0],
                          c->U[ui][1], lw, lh, P, c->C[0], c->C[1], c->C[2]);
+      prof_end(c, st, tk, 1, Nl * 40.0);  // u1,u2,I0 + one 16-B tap neighbourhood + 3 outputs
       double error = DBL_MAX;
       double prevError = 0.0;
       int n;
@@ -295,10 +344,16 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         a.p22d = c->Pd[pi ^ 1][3]; a.p31d = c->Pd[pi ^ 1][4]; a.p32d = c->Pd[pi ^ 1][5];
         a.calc_err = calcError ? 1 : 0;
         a.p_zero = p_zero ? 1 : 0;
+        tk = prof_begin(c, st);
         if (gam)
           hipLaunchKernelGGL(k_iterate<true>, dim3(nblk), dim3(kBlock), 0, st, a);
         else
           hipLaunchKernelGGL(k_iterate<false>, dim3(nblk), dim3(kBlock), 0, st, a);
+        {  // planes read: I1wx, I1wy, rho, u (+p unless p == 0); written: u, p
+          const int nu = gam ? 3 : 2, np = gam ? 6 : 4;
+          const int planes = 3 + nu + (p_zero ? 0 : np) + nu + np;
+          prof_end(c, st, tk, 0, Nl * 4.0 * planes);
+        }
         p_zero = false;
         ui ^= 1;
         pi ^= 1;
@@ -324,14 +379,38 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     const int dw = g.ws[s - 1], dh = g.hs[s - 1];
     const float fxu = (float)(1.0 / ((double)dw / lw));
     const float fyu = (float)(1.0 / ((double)dh / lh));
+    tk = prof_begin(c, st);
     hipLaunchKernelGGL(k_upsample, grid2(dw, dh, gam ? 3 : 2), kBlk2, 0, st, c->U[ui][0],
                        c->U[ui][1], c->U[ui][2], lw, lh, P, c->U[ui ^ 1][0], c->U[ui ^ 1][1],
                        c->U[ui ^ 1][2], dw, dh, g.ps[s - 1], fxu, fyu, upmul);
+    prof_end(c, st, tk, 2, Nl * 8.0 + (double)dw * dh * 8.0);
     ui ^= 1;
   }
+  tk = prof_begin(c, st);
   hipLaunchKernelGGL(k_output, grid2(W, H), kBlk2, 0, st, c->U[ui][0], c->U[ui][1], W, H,
                      g.ps[0], u, v, fpitch);
+  prof_end(c, st, tk, 2, (double)W * H * 16.0);
   HIP_TRY(c, hipGetLastError());
+
+  if (stats) {
+    for (int k = 0; k < 4; ++k) {
+      stats->kernel_ms[k] = 0.0;
+      stats->kernel_launches[k] = 0;
+      stats->kernel_bytes[k] = 0.0;
+    }
+  }
+  if (c->profiling && !c->marks.empty()) {
+    HIP_TRY(c, hipEventSynchronize(c->ev_pool[c->marks.back().b]));
+    for (const auto &m : c->marks) {
+      float ms = 0.f;
+      HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_pool[m.a], c->ev_pool[m.b]));
+      if (stats) {
+        stats->kernel_ms[m.cls] += ms;
+        stats->kernel_launches[m.cls] += 1;
+        stats->kernel_bytes[m.cls] += m.bytes;
+      }
+    }
+  }
 
   if (stats) {
     stats->levels = L;
@@ -474,8 +553,15 @@ tvl1_status tvl1_postprocess(tvl1_ctx *c, float *u, float *v, size_t fpitch, con
   return TVL1_OK;
 }
 
+tvl1_status tvl1_set_profiling(tvl1_ctx *c, int32_t enable) {
+  if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  c->profiling = enable != 0;
+  return TVL1_OK;
+}
+
 void tvl1_destroy(tvl1_ctx *c) {
   if (!c) return;
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipSetDevice(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   if (c->arena) (void)hipFree(c->arena);

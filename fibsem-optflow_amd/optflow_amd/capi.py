@@ -51,6 +51,9 @@ class TVL1Stats(C.Structure):
         ("warp_iterations", C.POINTER(C.c_int32)),
         ("warp_iterations_capacity", C.c_int32),
         ("reserved", C.c_int32),
+        ("kernel_ms", C.c_double * 4),
+        ("kernel_launches", C.c_int64 * 4),
+        ("kernel_bytes", C.c_double * 4),
     ]
 
 
@@ -90,6 +93,9 @@ def stats_dict(st: TVL1Stats, warps: int | None = None) -> dict:
         "iterations_total": int(st.iterations_total),
         "checks_total": int(st.checks_total),
         "algorithmic_bytes": float(st.algorithmic_bytes),
+        "kernel_ms": [float(st.kernel_ms[i]) for i in range(4)],
+        "kernel_launches": [int(st.kernel_launches[i]) for i in range(4)],
+        "kernel_bytes": [float(st.kernel_bytes[i]) for i in range(4)],
     }
     return out
 
@@ -149,6 +155,8 @@ def load_engine() -> C.CDLL:
                                      C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, C.c_int32,
                                      C.c_void_p]
     lib.tvl1_postprocess.restype = C.c_int
+    lib.tvl1_set_profiling.argtypes = [C.c_void_p, C.c_int32]
+    lib.tvl1_set_profiling.restype = C.c_int
     lib.tvl1_destroy.argtypes = [C.c_void_p]
     lib.tvl1_destroy.restype = None
     lib.tvl1_last_error.argtypes = [C.c_void_p]
@@ -206,6 +214,9 @@ class Engine:
     def set_params(self, params: TVL1Params):
         self.params = params
         self._check(self.lib.tvl1_set_params(self.ctx, C.byref(params)), "tvl1_set_params")
+
+    def set_profiling(self, on: bool):
+        self._check(self.lib.tvl1_set_profiling(self.ctx, 1 if on else 0), "tvl1_set_profiling")
 
     def _check(self, rc, what):
         if rc != 0:

@@ -89,6 +89,13 @@ typedef struct tvl1_stats {
   int32_t *warp_iterations;
   int32_t warp_iterations_capacity;         /* number of int32 slots in warp_iterations */
   int32_t reserved;
+  /* Filled only when profiling is enabled (tvl1_set_profiling): HIP-event time,
+   * launch count and algorithmic bytes per kernel class, on the solve's stream.
+   * Class 0 = fused primal-dual iteration (K6+K8+K7 partials), 1 = warpBackward
+   * (K5), 2 = everything else (convert, pyramid, gradient, upsample, output). */
+  double kernel_ms[4];
+  int64_t kernel_launches[4];
+  double kernel_bytes[4];
 } tvl1_stats;
 
 typedef struct tvl1_ctx tvl1_ctx;
@@ -132,6 +139,9 @@ tvl1_status tvl1_calc_host(tvl1_ctx *ctx,
 tvl1_status tvl1_postprocess(tvl1_ctx *ctx, float *u, float *v, size_t flow_pitch,
                              const uint8_t *I1, size_t pitch1,
                              int32_t width, int32_t height, int32_t mode, void *stream);
+
+/* Enable (1) / disable (0) per-kernel-class HIP-event timing into tvl1_stats. */
+tvl1_status tvl1_set_profiling(tvl1_ctx *ctx, int32_t enable);
 
 /* Destroy a ctx and free its device scratch. */
 void tvl1_destroy(tvl1_ctx *ctx);
