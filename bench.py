@@ -147,6 +147,7 @@ def main():
     k_bytes = sum(s["kernel_bytes"][0] for s in stats)
     k_launch = sum(s["kernel_launches"][0] for s in stats)
     pair_bytes = sum(s["algorithmic_bytes"] for s in stats) / len(stats)
+    cls_ms = [sum(s["kernel_ms"][i] for s in stats) / len(stats) for i in range(3)]
     iters = [s["iterations_total"] for s in stats]
 
     if rank != 0:
@@ -190,6 +191,10 @@ def main():
             "pair_roofline_frac": round(pair_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4),
         },
         "roofline": roof,
+        "step_breakdown_ms": None if k_ms <= 0 else {
+            "iterate": round(cls_ms[0], 2), "warp": round(cls_ms[1], 2),
+            "other_kernels": round(cls_ms[2], 2),
+            "host_sync_and_gaps": round(ms_per_step - sum(cls_ms), 2)},
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -26,6 +27,7 @@ namespace {
 thread_local std::string g_create_error;
 
 constexpr int kStripRows = 32;   // rows per wave strip in k_iterate
+constexpr int kTbMax = 4;        // max iterations fused per pass in k_iterate_tb
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -61,6 +63,8 @@ struct tvl1_ctx {
   int partials_cap = 0;
   double *red = nullptr;
   double *pinned = nullptr;  // host-pinned residual landing slot
+  int iter_mode = 0;         // 0 = temporally blocked passes, 1 = one iteration per launch
+  int tb_cfg = 0;            // k_iterate_tb shape: 0 = 64x32/512 thr, 1 = 64x32/256 thr, 2 = 64x64/1024 thr
 
   // optional per-kernel-class HIP-event timing (tvl1_set_profiling)
   bool profiling = false;
@@ -176,7 +180,8 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
   bytes += 3 * plane;                       // C
   bytes += 2 * align_up(P0 * H, 256);       // in0, in1 (u8)
   bytes += 2 * plane;                       // outu, outv
-  const int nblk = iterate_blocks(W, H) + 64;
+  const int tb_blocks = ((W + 55) / 56) * ((H + 23) / 24);   // RH 32 at 4 iterations
+  const int nblk = (iterate_blocks(W, H) > tb_blocks ? iterate_blocks(W, H) : tb_blocks) + 64;
   bytes += align_up((size_t)nblk * sizeof(double), 256) + 256;
   bytes += 4096;                            // alignment slack
 
@@ -331,34 +336,79 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[ui][0],
                          c->U[ui][1], lw, lh, P, c->C[0], c->C[1], c->C[2]);
       prof_end(c, st, tk, 1, Nl * 40.0);  // u1,u2,I0 + one 16-B tap neighbourhood + 3 outputs
+      // procOneScale's inner loop.  The stopping rule
+      //   for (n = 0; error > scaledEps && n < iterations; ++n)
+      //     calcError = eps > 0 && (n & 1) && prevError < scaledEps
+      // is known on the host for every iteration up to and including the next
+      // check, so those iterations run as ONE temporally blocked pass (<= kTbMax);
+      // the residual of the check iteration is then read exactly where OpenCV
+      // reads it (device -> host), and the schedule continues.
       double error = DBL_MAX;
       double prevError = 0.0;
-      int n;
-      for (n = 0; error > scaledEps && n < prm.iterations; ++n) {
-        const bool calcError = (prm.epsilon > 0) && (n & 1) && (prevError < scaledEps);
+      int n = 0;
+      while (error > scaledEps && n < prm.iterations) {
+        int k = 0;
+        bool calc_end = false;
+        double prev_sim = prevError;
+        const int kmax = c->iter_mode == 1 ? 1 : kTbMax;
+        while (k < kmax && n + k < prm.iterations) {
+          const bool calcError = (prm.epsilon > 0) && ((n + k) & 1) && (prev_sim < scaledEps);
+          ++k;
+          if (calcError) {
+            calc_end = true;
+            break;
+          }
+          prev_sim -= scaledEps;
+        }
         a.u1s = c->U[ui][0]; a.u2s = c->U[ui][1]; a.u3s = c->U[ui][2];
         a.u1d = c->U[ui ^ 1][0]; a.u2d = c->U[ui ^ 1][1]; a.u3d = c->U[ui ^ 1][2];
         a.p11s = c->Pd[pi][0]; a.p12s = c->Pd[pi][1]; a.p21s = c->Pd[pi][2];
         a.p22s = c->Pd[pi][3]; a.p31s = c->Pd[pi][4]; a.p32s = c->Pd[pi][5];
         a.p11d = c->Pd[pi ^ 1][0]; a.p12d = c->Pd[pi ^ 1][1]; a.p21d = c->Pd[pi ^ 1][2];
         a.p22d = c->Pd[pi ^ 1][3]; a.p31d = c->Pd[pi ^ 1][4]; a.p32d = c->Pd[pi ^ 1][5];
-        a.calc_err = calcError ? 1 : 0;
+        a.calc_err = calc_end ? 1 : 0;
         a.p_zero = p_zero ? 1 : 0;
+        int blocks = nblk;
         tk = prof_begin(c, st);
-        if (gam)
-          hipLaunchKernelGGL(k_iterate<true>, dim3(nblk), dim3(kBlock), 0, st, a);
-        else
-          hipLaunchKernelGGL(k_iterate<false>, dim3(nblk), dim3(kBlock), 0, st, a);
-        {  // planes read: I1wx, I1wy, rho, u (+p unless p == 0); written: u, p
+        if (c->iter_mode == 1) {
+          if (gam)
+            hipLaunchKernelGGL(k_iterate<true>, dim3(nblk), dim3(kBlock), 0, st, a);
+          else
+            hipLaunchKernelGGL(k_iterate<false>, dim3(nblk), dim3(kBlock), 0, st, a);
+        } else {
+          TBArgs t;
+          t.it = a;
+          t.niter = k;
+          t.tiles_x = (lw + 55) / 56;
+          t.out_h = (c->tb_cfg == 2 ? 64 : 32) - 2 * k;
+          const int tiles_y = (lh + t.out_h - 1) / t.out_h;
+          blocks = t.tiles_x * tiles_y;
+          if (blocks > c->partials_cap)
+            return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
+                           c->partials_cap);
+          switch (c->tb_cfg) {
+#define TB_LAUNCH(RH, NG)                                                                   \
+  if (gam)                                                                                  \
+    hipLaunchKernelGGL((k_iterate_tb<true, RH, NG>), dim3(blocks), dim3(16 * RH / NG), 0, st, t); \
+  else                                                                                      \
+    hipLaunchKernelGGL((k_iterate_tb<false, RH, NG>), dim3(blocks), dim3(16 * RH / NG), 0, st, t);
+            case 1: TB_LAUNCH(32, 2) break;
+            case 2: TB_LAUNCH(64, 1) break;
+            default: TB_LAUNCH(32, 1) break;
+#undef TB_LAUNCH
+          }
+        }
+        {  // per iteration: planes read I1wx, I1wy, rho, u (+p unless p == 0); written u, p
           const int nu = gam ? 3 : 2, np = gam ? 6 : 4;
-          const int planes = 3 + nu + (p_zero ? 0 : np) + nu + np;
+          const double planes = (3 + nu + np + nu + np) * (double)k - (p_zero ? np : 0);
           prof_end(c, st, tk, 0, Nl * 4.0 * planes);
         }
         p_zero = false;
         ui ^= 1;
         pi ^= 1;
-        if (calcError) {
-          hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, nblk, c->red);
+        n += k;
+        if (calc_end) {
+          hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, blocks, c->red);
           HIP_TRY(c, hipMemcpyAsync(c->pinned, c->red, sizeof(double), hipMemcpyDeviceToHost, st));
           HIP_TRY(c, hipStreamSynchronize(st));  // the cuda::sum -> host read of procOneScale
           error = *c->pinned;
@@ -366,7 +416,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           ++checks;
         } else {
           error = DBL_MAX;
-          prevError -= scaledEps;
+          prevError = prev_sim;
         }
       }
       level_iters[s] += n;
@@ -474,6 +524,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (!c) return set_err(nullptr, TVL1_ENOMEM, "out of host memory");
   c->device = device;
   c->prm = *params;
+  if (const char *m = getenv("TVL1_ITER_MODE")) c->iter_mode = atoi(m) == 1 ? 1 : 0;
+  if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = atoi(m);
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void **)&c->pinned, sizeof(double) * 8, hipHostMallocDefault) != hipSuccess) {

@@ -393,6 +393,186 @@ __global__ __launch_bounds__(kBlock) void k_iterate(IterArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- K6+K8 temporally blocked
+// k_iterate_tb: runs `niter` (1..4) consecutive primal-dual iterations in ONE HBM pass.
+//
+// A workgroup owns a region of 64 x RH px (16 float4 columns x RH rows; every thread
+// owns NG float4 groups, rows rr, rr + RH/NG, ...).  It loads u, p and the warp
+// constants once, iterates in registers, and stores only the interior that is still
+// exact after niter iterations: each iteration invalidates one px at every internal
+// region edge (u needs p at x-1, y-1; p needs u at x+1, y+1), so the region keeps a
+// 4-px halo in x (float4 alignment) and a niter-px halo in y.  At the image border the
+// clamp / special-divergence forms of OpenCV apply and nothing is invalidated.
+//   x neighbours: wavefront shuffles (16 lanes per row);
+//   y neighbours: 4 LDS planes (p12, p22 for estimateU; u1, u2 for the projection);
+//   per px-iteration HBM traffic: (36 B / efficiency + 24 B) / niter instead of 60 B.
+// Arithmetic is exactly the per-pixel sequence of k_iterate (bit-identical results).
+struct TBArgs {
+  IterArgs it;
+  int niter;        // iterations in this pass (1..4); the residual is of the last one
+  int tiles_x;      // regions per row
+  int out_h;        // output rows per region = RH - 2*niter
+};
+
+template <bool G, int RH, int NG>
+__global__ __launch_bounds__(16 * RH / NG) void k_iterate_tb(TBArgs t) {
+  constexpr int NT = 16 * RH / NG;   // threads; each owns NG float4 groups
+  constexpr int HALF = RH / NG;
+  constexpr int NPL = G ? 6 : 4;                 // LDS planes
+  __shared__ float4 lds[NPL][RH][16];
+  const IterArgs &a = t.it;
+  const int tid = threadIdx.x;
+  const int c4 = tid & 15;
+  const int rr = tid >> 4;
+  const int bx = blockIdx.x % t.tiles_x;
+  const int by = blockIdx.x / t.tiles_x;
+  const int K = t.niter;
+  const int xr0 = bx * 56 - 4;                   // region origin (16-B aligned)
+  const int yr0 = by * t.out_h - K;
+  const int X = xr0 + 4 * c4;                    // first image column of this thread
+  const int xa = imin(imax(X, 0), a.P - 4);
+
+  Row<G> r[NG];
+  int Y[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    Y[g] = yr0 + rr + g * HALF;
+    const int ya = imin(imax(Y[g], 0), a.H - 1);
+    load_row<G>(r[g], a, (size_t)ya * a.P + xa);
+  }
+  // stage the vertically read planes of the initial state
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int row = rr + g * HALF;
+    lds[0][row][c4] = make_float4(r[g].p12[0], r[g].p12[1], r[g].p12[2], r[g].p12[3]);
+    lds[1][row][c4] = make_float4(r[g].p22[0], r[g].p22[1], r[g].p22[2], r[g].p22[3]);
+    if (G) lds[4][row][c4] = make_float4(r[g].p32[0], r[g].p32[1], r[g].p32[2], r[g].p32[3]);
+  }
+  __syncthreads();
+
+  float e1[NG][4], e2[NG][4];   // u before the last iteration (residual)
+  for (int it = 0; it < K; ++it) {
+    const bool last = it == K - 1;
+    // ---- estimateU, one group at a time (keeps the live register set small)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int row = rr + g * HALF;
+      const int rowu = row > 0 ? row - 1 : 0;
+      float up12[4], up22[4], up32[4];
+      const float4 a12 = lds[0][rowu][c4];
+      const float4 a22 = lds[1][rowu][c4];
+      up12[0] = a12.x; up12[1] = a12.y; up12[2] = a12.z; up12[3] = a12.w;
+      up22[0] = a22.x; up22[1] = a22.y; up22[2] = a22.z; up22[3] = a22.w;
+      if (G) {
+        const float4 a32 = lds[4][rowu][c4];
+        up32[0] = a32.x; up32[1] = a32.y; up32[2] = a32.z; up32[3] = a32.w;
+      } else {
+        zero4(up32);
+      }
+      float n1[4], n2[4], n3[4];
+      estimate_u<G>(r[g], up12, up22, up32, X, Y[g], a, n1, n2, n3);
+      if (last) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { e1[g][k] = r[g].u1[k]; e2[g][k] = r[g].u2[k]; }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        r[g].u1[k] = n1[k];
+        r[g].u2[k] = n2[k];
+        if (G) r[g].u3[k] = n3[k];
+      }
+      lds[2][row][c4] = make_float4(n1[0], n1[1], n1[2], n1[3]);
+      lds[3][row][c4] = make_float4(n2[0], n2[1], n2[2], n2[3]);
+      if (G) lds[5][row][c4] = make_float4(n3[0], n3[1], n3[2], n3[3]);
+    }
+    __syncthreads();
+    // ---- estimateDualVariables on both groups
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int row = rr + g * HALF;
+      const int rowd = row < RH - 1 ? row + 1 : RH - 1;
+      const bool has_down = Y[g] + 1 < a.H;
+      float d1[4], d2[4], d3[4];
+      const float4 b1 = lds[2][rowd][c4];
+      const float4 b2 = lds[3][rowd][c4];
+      d1[0] = b1.x; d1[1] = b1.y; d1[2] = b1.z; d1[3] = b1.w;
+      d2[0] = b2.x; d2[1] = b2.y; d2[2] = b2.z; d2[3] = b2.w;
+      float q11[4], q12[4], q21[4], q22[4], q31[4], q32[4];
+      dual_component(r[g].u1, d1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12);
+      dual_component(r[g].u2, d2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22);
+      if (G) {
+        const float4 b3 = lds[5][rowd][c4];
+        d3[0] = b3.x; d3[1] = b3.y; d3[2] = b3.z; d3[3] = b3.w;
+        dual_component(r[g].u3, d3, has_down, X, a.W, a.taut, r[g].p31, r[g].p32, q31, q32);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        r[g].p11[k] = q11[k]; r[g].p12[k] = q12[k];
+        r[g].p21[k] = q21[k]; r[g].p22[k] = q22[k];
+        if (G) { r[g].p31[k] = q31[k]; r[g].p32[k] = q32[k]; }
+      }
+    }
+    if (!last) {
+      // p12/p22 planes are not read during the projection phase: publish the new rows
+      // now; the barrier orders them before the next estimateU and orders this
+      // phase's u1/u2 reads before the next phase's u1/u2 writes.
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const int row = rr + g * HALF;
+        lds[0][row][c4] = make_float4(r[g].p12[0], r[g].p12[1], r[g].p12[2], r[g].p12[3]);
+        lds[1][row][c4] = make_float4(r[g].p22[0], r[g].p22[1], r[g].p22[2], r[g].p22[3]);
+        if (G) lds[4][row][c4] = make_float4(r[g].p32[0], r[g].p32[1], r[g].p32[2], r[g].p32[3]);
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- store the exact interior: region cols 4..59, rows K..RH-K-1, inside the image
+  double acc = 0.0;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int row = rr + g * HALF;
+    const bool ok = c4 >= 1 && c4 <= 14 && row >= K && row < RH - K && Y[g] >= 0 &&
+                    Y[g] < a.H && X < a.W;
+    if (ok) {
+      const size_t off = (size_t)Y[g] * a.P + X;
+      st4(a.u1d, off, r[g].u1);
+      st4(a.u2d, off, r[g].u2);
+      st4(a.p11d, off, r[g].p11);
+      st4(a.p12d, off, r[g].p12);
+      st4(a.p21d, off, r[g].p21);
+      st4(a.p22d, off, r[g].p22);
+      if (G) {
+        st4(a.u3d, off, r[g].u3);
+        st4(a.p31d, off, r[g].p31);
+        st4(a.p32d, off, r[g].p32);
+      }
+      if (a.calc_err) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (X + k < a.W) {
+            const float f1 = (e1[g][k] - r[g].u1[k]) * (e1[g][k] - r[g].u1[k]);
+            const float f2 = (e2[g][k] - r[g].u2[k]) * (e2[g][k] - r[g].u2[k]);
+            acc += (double)(f1 + f2);
+          }
+        }
+      }
+    }
+  }
+  if (a.calc_err) {
+    __shared__ double red[NT / kWave];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((tid & 63) == 0) red[tid >> 6] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      double s = 0.0;
+      for (int i = 0; i < NT / kWave; ++i) s += red[i];
+      a.partials[blockIdx.x] = s;
+    }
+  }
+}
+
 // K7: fixed-order sum of the per-block partials (one block).
 __global__ void k_reduce(const double *__restrict__ partials, int n, double *__restrict__ out) {
   __shared__ double s[kBlock];

@@ -65,3 +65,30 @@ def test_constant_images_give_zero_flow(engine):
     engine.set_params(capi.make_params(nscales=3, warps=2))
     u, v, _, _ = engine.calc_host(I0, I1)
     assert np.all(u == 0) and np.all(v == 0)
+
+
+# Every iteration-kernel configuration must give the same bits (selected by env at
+# tvl1_create): TVL1_ITER_MODE=1 -> one iteration per launch (rolling-strip kernel),
+# TVL1_TB_CFG = 0/1/2 -> temporally blocked regions 64x32/512thr, 64x32/256thr, 64x64/1024thr.
+MODES = [("TVL1_ITER_MODE", "1"), ("TVL1_TB_CFG", "0"), ("TVL1_TB_CFG", "1"),
+         ("TVL1_TB_CFG", "2")]
+
+
+@pytest.mark.parametrize("env", MODES, ids=[f"{k}={v}" for k, v in MODES])
+@pytest.mark.parametrize("W,H,seed,kw", [
+    (250, 131, 21, dict(nscales=5, warps=5)),
+    (97, 201, 22, dict(nscales=4, warps=3, gamma=0.1)),
+    (400, 300, 23, dict(nscales=3, warps=4, epsilon=0.0, iterations=9)),
+])
+def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
+    monkeypatch.delenv("TVL1_ITER_MODE", raising=False)
+    monkeypatch.delenv("TVL1_TB_CFG", raising=False)
+    monkeypatch.setenv(*env)
+    p = capi.make_params(**kw)
+    eng = capi.Engine(p)
+    I0, I1 = synth.gen_pair(W, H, seed=seed)
+    u, v, st, wi = eng.calc_host(I0, I1)
+    eng.close()
+    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    np.testing.assert_array_equal(wi, wr)
+    assert np.array_equal(u, ur) and np.array_equal(v, vr)
