@@ -146,6 +146,7 @@ def main():
     k_ms = sum(s["kernel_ms"][0] for s in stats)
     k_bytes = sum(s["kernel_bytes"][0] for s in stats)
     k_launch = sum(s["kernel_launches"][0] for s in stats)
+    k_hbm = sum(s["kernel_hbm_bytes"][0] for s in stats)
     pair_bytes = sum(s["algorithmic_bytes"] for s in stats) / len(stats)
     cls_ms = [sum(s["kernel_ms"][i] for s in stats) / len(stats) for i in range(3)]
     iters = [s["iterations_total"] for s in stats]
@@ -165,6 +166,12 @@ def main():
                 "kernel": "k_iterate (fused estimateU + estimateDualVariables + residual partials)",
                 "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
                 "algorithmic_bytes_per_launch": round(k_bytes / k_launch),
+                "algorithmic_model": "SURVEY 8(d): 64 B/px per executed iteration",
+                # what this kernel must move with its temporal blocking (tile loads incl.
+                # halos + interior stores), the honest bandwidth-efficiency figure:
+                "compulsory_bytes_per_launch": round(k_hbm / k_launch),
+                "compulsory_GBs": round(k_hbm / (k_ms * 1e-3) / 1e9, 1),
+                "compulsory_frac": round(k_hbm / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "kernel_share_of_step": round(k_ms / (1e3 * elapsed), 4)}
     out = {
         "metric": METRIC,

@@ -64,6 +64,7 @@ struct tvl1_ctx {
   double *red = nullptr;
   double *pinned = nullptr;  // host-pinned residual landing slot
   int iter_mode = 0;         // 0 = temporally blocked passes, 1 = one iteration per launch
+  int warp_mode = 0;         // 0 = LDS-staged gather (k_warp_lds), 1 = global gather (k_warp)
   int tb_cfg = 0;            // k_iterate_tb shape: 0 = 64x32/512 thr, 1 = 64x32/256 thr, 2 = 64x64/1024 thr
 
   // optional per-kernel-class HIP-event timing (tvl1_set_profiling)
@@ -73,7 +74,8 @@ struct tvl1_ctx {
   struct Mark {
     int cls;
     size_t a, b;
-    double bytes;
+    double bytes;      // SURVEY 8(d) algorithmic bytes
+    double hbm_bytes;  // compulsory bytes of this implementation
   };
   std::vector<Mark> marks;
 };
@@ -93,11 +95,12 @@ static size_t prof_begin(tvl1_ctx *c, hipStream_t st) {
   return a + 1;  // 0 = not recording
 }
 
-static void prof_end(tvl1_ctx *c, hipStream_t st, size_t tok, int cls, double bytes) {
+static void prof_end(tvl1_ctx *c, hipStream_t st, size_t tok, int cls, double bytes,
+                     double hbm_bytes = -1.0) {
   if (!c->profiling || tok == 0) return;
   const size_t b = c->ev_used++;
   (void)hipEventRecord(c->ev_pool[b], st);
-  c->marks.push_back({cls, tok - 1, b, bytes});
+  c->marks.push_back({cls, tok - 1, b, bytes, hbm_bytes < 0 ? bytes : hbm_bytes});
 }
 
 static tvl1_status set_err(tvl1_ctx *c, tvl1_status st, const char *fmt, ...) {
@@ -333,8 +336,14 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         ui ^= 1;
       }
       tk = prof_begin(c, st);
-      hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[ui][0],
-                         c->U[ui][1], lw, lh, P, c->C[0], c->C[1], c->C[2]);
+      if (c->warp_mode == 1) {
+        hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[ui][0],
+                           c->U[ui][1], lw, lh, P, c->C[0], c->C[1], c->C[2]);
+      } else {
+        const int tx = (lw + kWarpTW - 1) / kWarpTW, ty = (lh + kWarpTH - 1) / kWarpTH;
+        hipLaunchKernelGGL(k_warp_lds, dim3(tx * ty), dim3(256), 0, st, c->I0s[s], c->G,
+                           c->U[ui][0], c->U[ui][1], lw, lh, P, tx, c->C[0], c->C[1], c->C[2]);
+      }
       prof_end(c, st, tk, 1, Nl * 40.0);  // u1,u2,I0 + one 16-B tap neighbourhood + 3 outputs
       // procOneScale's inner loop.  The stopping rule
       //   for (n = 0; error > scaledEps && n < iterations; ++n)
@@ -398,10 +407,21 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
 #undef TB_LAUNCH
           }
         }
-        {  // per iteration: planes read I1wx, I1wy, rho, u (+p unless p == 0); written u, p
+        {
+          // algorithmic: 64 B/px per executed iteration;
+          // compulsory for this tiling: every staged region cell loads I1wx, I1wy, rho,
+          // u (+p unless p == 0), every px stores u and p once per pass.
           const int nu = gam ? 3 : 2, np = gam ? 6 : 4;
-          const double planes = (3 + nu + np + nu + np) * (double)k - (p_zero ? np : 0);
-          prof_end(c, st, tk, 0, Nl * 4.0 * planes);
+          const double ld_planes = 3 + nu + (p_zero ? 0 : np), st_planes = nu + np;
+          double hbm;
+          if (c->iter_mode == 1) {
+            hbm = Nl * 4.0 * (ld_planes + st_planes);
+          } else {
+            const int rh = c->tb_cfg == 2 ? 64 : 32;
+            const double cells = (double)blocks * 64.0 * rh;
+            hbm = cells * 4.0 * ld_planes + Nl * 4.0 * st_planes;
+          }
+          prof_end(c, st, tk, 0, Nl * 64.0 * k, hbm);
         }
         p_zero = false;
         ui ^= 1;
@@ -447,6 +467,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       stats->kernel_ms[k] = 0.0;
       stats->kernel_launches[k] = 0;
       stats->kernel_bytes[k] = 0.0;
+      stats->kernel_hbm_bytes[k] = 0.0;
     }
   }
   if (c->profiling && !c->marks.empty()) {
@@ -458,6 +479,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         stats->kernel_ms[m.cls] += ms;
         stats->kernel_launches[m.cls] += 1;
         stats->kernel_bytes[m.cls] += m.bytes;
+        stats->kernel_hbm_bytes[m.cls] += m.hbm_bytes;
       }
     }
   }
@@ -526,6 +548,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   c->prm = *params;
   if (const char *m = getenv("TVL1_ITER_MODE")) c->iter_mode = atoi(m) == 1 ? 1 : 0;
   if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = atoi(m);
+  if (const char *m = getenv("TVL1_WARP_MODE")) c->warp_mode = atoi(m) == 1 ? 1 : 0;
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void **)&c->pinned, sizeof(double) * 8, hipHostMallocDefault) != hipSuccess) {

@@ -36,6 +36,25 @@ constexpr float kFltEps = 1.1920928955078125e-07f;  // numeric_limits<float>::ep
 __device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
 __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
 
+// XCD-aware tile order (speed only, never correctness).  The dispatcher deals
+// workgroups round-robin over the 8 XCDs (MI355X_MICROARCH: blocks b and b+8 share an
+// XCD), each with its own 4 MiB L2.  Give every XCD a contiguous run of tile slots and
+// walk the slots in 8-tile-wide column bands, row by row, so a tile's x- and
+// y-neighbours (which re-read its halo lines) run on the same XCD shortly after it.
+constexpr int kXcds = 8, kBand = 8;
+__device__ __forceinline__ void tile_of_block(int bid, int nblocks, int tiles_x, int tiles_y,
+                                              int &bx, int &by) {
+  const int q = nblocks / kXcds, rem = nblocks % kXcds;
+  const int xcd = bid % kXcds, k = bid / kXcds;
+  const int slot = xcd * q + imin(xcd, rem) + k;
+  const int full = tiles_x / kBand;
+  const int band = imin(slot / (kBand * tiles_y), full);
+  const int width = band < full ? kBand : tiles_x - full * kBand;
+  const int in_band = slot - band * kBand * tiles_y;
+  by = in_band / width;
+  bx = band * kBand + (in_band - by * width);
+}
+
 // ---------------------------------------------------------------- K1 convert
 // GpuMat::convertTo(CV_32F, 1.0) for both frames (blockIdx.z selects the frame).
 __global__ void k_convert_u8(const uint8_t *__restrict__ s0, size_t sp0,
@@ -164,6 +183,124 @@ __global__ void k_warp(const float *__restrict__ I0, const float4 *__restrict__ 
   rho[i] = I1wv - I1wxv * u1v - I1wyv * u2v - I0[i];
 }
 
+// warpBackward, LDS-staged: a 64 x 16 px tile stages the (I1, I1x, I1y) window it can
+// reach with |u| <= kWarpHalo - 2 (clamped coordinates, exactly the texture-clamp
+// values) and gathers every bicubic tap from LDS; a pixel whose taps leave the
+// window takes the global-memory path.  Same arithmetic and order as k_warp.
+constexpr int kWarpTW = 64, kWarpTH = 16, kWarpHalo = 6;
+constexpr int kWarpWW = kWarpTW + 2 * kWarpHalo, kWarpWH = kWarpTH + 2 * kWarpHalo;
+
+// Keys kernel pieces: |t| <= 1 and 1 < |t| < 2 (OpenCV `cubic`).
+__device__ __forceinline__ float cubic_in(float x) {
+  x = fabsf(x);
+  return x * x * (1.5f * x - 2.5f) + 1.0f;
+}
+__device__ __forceinline__ float cubic_out(float x) {
+  x = fabsf(x);
+  return x * (x * (-0.5f * x + 2.5f) - 4.0f) + 2.0f;
+}
+
+// Fixed 4x4 form of OpenCV's tap loop (cy in [ceil(wy-2), floor(wy+2)], cx likewise):
+// every tap it visits outside cx in [floor(wx)-1, floor(wx)+2] has weight exactly 0
+// (|t| = 2), and inside that range the tap distances are t0 in [1,2), t1 in [0,1),
+// t2 in [-1,0), t3 in [-2,-1) -- so taps 1,2 always take the |t|<=1 piece and taps
+// 0,3 the outer piece; at the two ends (t0 = 1, |t3| = 2) both pieces evaluate to
+// exactly 0.0f.  Summation order (rows outer, columns inner, ascending) and the
+// weight product cubic(wx-cx) * cubic(wy-cy) are unchanged, so the result is
+// bit-identical to the reference loop while being branch-free and unrollable.
+template <bool LDSPATH>
+__device__ __forceinline__ void warp_gather(const float4 *__restrict__ src, int sp, int ox, int oy,
+                                            int W, int H, float wx, float wy, int fx, int fy,
+                                            float &sum, float &sumx, float &sumy, float &wsum) {
+  float kx[4], ky[4];
+  kx[0] = cubic_out(wx - (float)(fx - 1));
+  kx[1] = cubic_in(wx - (float)fx);
+  kx[2] = cubic_in(wx - (float)(fx + 1));
+  kx[3] = cubic_out(wx - (float)(fx + 2));
+  ky[0] = cubic_out(wy - (float)(fy - 1));
+  ky[1] = cubic_in(wy - (float)fy);
+  ky[2] = cubic_in(wy - (float)(fy + 1));
+  ky[3] = cubic_out(wy - (float)(fy + 2));
+  int cxs[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    cxs[i] = LDSPATH ? fx - 1 + i - ox : imin(imax(fx - 1 + i, 0), W - 1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cy = fy - 1 + j;
+    const int ry = LDSPATH ? cy - oy : imin(imax(cy, 0), H - 1);
+    const float4 *rowp = src + (size_t)ry * sp;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float w = kx[i] * ky[j];
+      const float4 g = rowp[cxs[i]];
+      sum = sum + w * g.x;
+      sumx = sumx + w * g.y;
+      sumy = sumy + w * g.z;
+      wsum = wsum + w;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
+                                                  const float4 *__restrict__ G,
+                                                  const float *__restrict__ u1,
+                                                  const float *__restrict__ u2, int W, int H,
+                                                  int P, int tiles_x, float *__restrict__ I1wx,
+                                                  float *__restrict__ I1wy,
+                                                  float *__restrict__ rho) {
+  __shared__ float4 win[kWarpWH * kWarpWW];
+  int bx, by;
+  tile_of_block(blockIdx.x, gridDim.x, tiles_x, gridDim.x / tiles_x, bx, by);
+  const int x0 = bx * kWarpTW, y0 = by * kWarpTH;
+  const int ox = x0 - kWarpHalo, oy = y0 - kWarpHalo;   // window origin (unclamped coords)
+  // Issue this thread's own loads (u1, u2, I0 of its 4 rows) before the window fill so
+  // their latency overlaps it.
+  constexpr int R = kWarpTH / 4;
+  const int x = x0 + (threadIdx.x & 63);
+  const int xc = imin(x, W - 1);
+  float u1v[R], u2v[R], i0v[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int y = imin(y0 + (threadIdx.x >> 6) + 4 * j, H - 1);
+    const size_t i = (size_t)y * P + xc;
+    u1v[j] = u1[i];
+    u2v[j] = u2[i];
+    i0v[j] = I0[i];
+  }
+  for (int i = threadIdx.x; i < kWarpWH * kWarpWW; i += 256) {
+    const int wy = i / kWarpWW, wx = i - wy * kWarpWW;
+    const int cx = imin(imax(ox + wx, 0), W - 1);
+    const int cy = imin(imax(oy + wy, 0), H - 1);
+    win[i] = G[(size_t)cy * P + cx];
+  }
+  __syncthreads();
+  if (x >= W) return;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int y = y0 + (threadIdx.x >> 6) + 4 * j;
+    if (y >= H) break;
+    const size_t i = (size_t)y * P + x;
+    const float wx = (float)x + u1v[j];
+    const float wy = (float)y + u2v[j];
+    const int fx = (int)floorf(wx);
+    const int fy = (int)floorf(wy);
+    float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
+    const bool inwin = fx - 1 >= ox && fx + 2 < ox + kWarpWW && fy - 1 >= oy && fy + 2 < oy + kWarpWH;
+    if (inwin)
+      warp_gather<true>(win, kWarpWW, ox, oy, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+    else
+      warp_gather<false>(G, P, 0, 0, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+    const float coeff = 1.0f / wsum;
+    const float I1wv = sum * coeff;
+    const float I1wxv = sumx * coeff;
+    const float I1wyv = sumy * coeff;
+    I1wx[i] = I1wxv;
+    I1wy[i] = I1wyv;
+    rho[i] = I1wv - I1wxv * u1v[j] - I1wyv * u2v[j] - i0v[j];
+  }
+}
+
 // ---------------------------------------------------------------- K6+K8 fused
 struct IterArgs {
   const float *I1wx, *I1wy, *rho;                                  // warp constants
@@ -214,12 +351,17 @@ __device__ __forceinline__ void load_row(Row<G> &r, const IterArgs &a, size_t of
 }
 
 // OpenCV `divergence` (tvl1flow.cu) at px k of this lane; pl = p1 at x-1, pu = p2 at y-1.
+// Branch-free: every form is evaluated with its own association and the right one
+// selected (the x == 0, y > 0 form associates differently from the interior one).
 __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float p2u, int x,
                                             int y) {
-  if (x > 0 && y > 0) return (p1 - p1l) + (p2 - p2u);
-  if (y > 0) return p1 + p2 - p2u;
-  if (x > 0) return p1 - p1l + p2;
-  return p1 + p2;
+  const float interior = (p1 - p1l) + (p2 - p2u);
+  const float col0 = p1 + p2 - p2u;      // x == 0, y > 0
+  const float row0 = p1 - p1l + p2;      // y == 0, x > 0
+  const float corner = p1 + p2;          // x == 0, y == 0
+  const float ylo = x > 0 ? row0 : corner;
+  const float yhi = x > 0 ? interior : col0;
+  return y > 0 ? yhi : ylo;
 }
 
 // estimateU for the 4 px of this lane on row y.  up* = p12/p22/p32 of row y-1.
@@ -250,21 +392,21 @@ __device__ __forceinline__ void estimate_u(const Row<G> &r, const float (&up12)[
     const float u2o = r.u2[k];
     const float u3o = G ? r.u3[k] : 0.0f;
     const float rho = r.rh[k] + (I1wxv * u1o + I1wyv * u2o) + a.gamma * u3o;
-    float d1 = 0.0f, d2 = 0.0f, d3 = 0.0f;
-    if (rho < -a.l_t * gradv) {
-      d1 = a.l_t * I1wxv;
-      d2 = a.l_t * I1wyv;
-      if (G) d3 = a.theta * a.gamma;
-    } else if (rho > a.l_t * gradv) {
-      d1 = -a.l_t * I1wxv;
-      d2 = -a.l_t * I1wyv;
-      if (G) d3 = -a.theta * a.gamma;
-    } else if (gradv > kFltEps) {
-      const float fi = -rho / gradv;
-      d1 = fi * I1wxv;
-      d2 = fi * I1wyv;
-      if (G) d3 = fi * a.gamma;
-    }
+    // TH operator, branch-free: the three candidate steps are computed with the
+    // reference's exact expressions and the applicable one selected.
+    const bool lo = rho < -a.l_t * gradv;
+    const bool hi = rho > a.l_t * gradv;
+    const bool mid = gradv > kFltEps;
+    const float fi = -rho / gradv;     // only selected when gradv > FLT_EPSILON
+    float d1 = mid ? fi * I1wxv : 0.0f;
+    float d2 = mid ? fi * I1wyv : 0.0f;
+    float d3 = mid ? fi * a.gamma : 0.0f;
+    d1 = hi ? -a.l_t * I1wxv : d1;
+    d2 = hi ? -a.l_t * I1wyv : d2;
+    d3 = hi ? -a.theta * a.gamma : d3;
+    d1 = lo ? a.l_t * I1wxv : d1;
+    d2 = lo ? a.l_t * I1wyv : d2;
+    d3 = lo ? a.theta * a.gamma : d3;
     const float v1 = u1o + d1;
     const float v2 = u2o + d2;
     const float div1 = divergence(r.p11[k], l11[k], r.p12[k], up12[k], x, y);
@@ -424,8 +566,8 @@ __global__ __launch_bounds__(16 * RH / NG) void k_iterate_tb(TBArgs t) {
   const int tid = threadIdx.x;
   const int c4 = tid & 15;
   const int rr = tid >> 4;
-  const int bx = blockIdx.x % t.tiles_x;
-  const int by = blockIdx.x / t.tiles_x;
+  int bx, by;
+  tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
   const int K = t.niter;
   const int xr0 = bx * 56 - 4;                   // region origin (16-B aligned)
   const int yr0 = by * t.out_h - K;

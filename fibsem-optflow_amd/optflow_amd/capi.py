@@ -54,6 +54,7 @@ class TVL1Stats(C.Structure):
         ("kernel_ms", C.c_double * 4),
         ("kernel_launches", C.c_int64 * 4),
         ("kernel_bytes", C.c_double * 4),
+        ("kernel_hbm_bytes", C.c_double * 4),
     ]
 
 
@@ -96,6 +97,7 @@ def stats_dict(st: TVL1Stats, warps: int | None = None) -> dict:
         "kernel_ms": [float(st.kernel_ms[i]) for i in range(4)],
         "kernel_launches": [int(st.kernel_launches[i]) for i in range(4)],
         "kernel_bytes": [float(st.kernel_bytes[i]) for i in range(4)],
+        "kernel_hbm_bytes": [float(st.kernel_hbm_bytes[i]) for i in range(4)],
     }
     return out
 

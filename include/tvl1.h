@@ -95,7 +95,8 @@ typedef struct tvl1_stats {
    * (K5), 2 = everything else (convert, pyramid, gradient, upsample, output). */
   double kernel_ms[4];
   int64_t kernel_launches[4];
-  double kernel_bytes[4];
+  double kernel_bytes[4];      /* SURVEY 8(d) algorithmic bytes (64 B/px per iteration for class 0) */
+  double kernel_hbm_bytes[4];  /* compulsory HBM bytes of THIS implementation's tiling */
 } tvl1_stats;
 
 typedef struct tvl1_ctx tvl1_ctx;

@@ -71,7 +71,7 @@ def test_constant_images_give_zero_flow(engine):
 # tvl1_create): TVL1_ITER_MODE=1 -> one iteration per launch (rolling-strip kernel),
 # TVL1_TB_CFG = 0/1/2 -> temporally blocked regions 64x32/512thr, 64x32/256thr, 64x64/1024thr.
 MODES = [("TVL1_ITER_MODE", "1"), ("TVL1_TB_CFG", "0"), ("TVL1_TB_CFG", "1"),
-         ("TVL1_TB_CFG", "2")]
+         ("TVL1_TB_CFG", "2"), ("TVL1_WARP_MODE", "1")]
 
 
 @pytest.mark.parametrize("env", MODES, ids=[f"{k}={v}" for k, v in MODES])
@@ -79,10 +79,12 @@ MODES = [("TVL1_ITER_MODE", "1"), ("TVL1_TB_CFG", "0"), ("TVL1_TB_CFG", "1"),
     (250, 131, 21, dict(nscales=5, warps=5)),
     (97, 201, 22, dict(nscales=4, warps=3, gamma=0.1)),
     (400, 300, 23, dict(nscales=3, warps=4, epsilon=0.0, iterations=9)),
+    (300, 200, 24, dict(nscales=1, warps=2)),   # level 0 only: large flow leaves LDS windows
 ])
 def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
     monkeypatch.delenv("TVL1_ITER_MODE", raising=False)
     monkeypatch.delenv("TVL1_TB_CFG", raising=False)
+    monkeypatch.delenv("TVL1_WARP_MODE", raising=False)
     monkeypatch.setenv(*env)
     p = capi.make_params(**kw)
     eng = capi.Engine(p)

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run: per-kernel durations (kernel trace) and PMC
+counters (per-dispatch sums / averages).  FETCH_SIZE is doubled per
+MI355X_MICROARCH.md (gfx950 reports 1/2 of the bytes of wide coalesced streams);
+WRITE_SIZE is taken as is.  Both are in KB in rocprofv3's derived counters.
+Usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [kernel-substring ...]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("tvl1k::", "")
+
+
+def main():
+    d = sys.argv[1]
+    want = sys.argv[2:] or ["k_iterate", "k_warp"]
+    rows = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv"))))
+    dur = defaultdict(list)
+    for r in rows:
+        dur[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    print(f"{'kernel':40s} {'calls':>6s} {'total ms':>9s} {'avg us':>8s}")
+    for k, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
+        print(f"{k:40s} {len(v):6d} {sum(v)/1e6:9.2f} {sum(v)/len(v)/1e3:8.1f}")
+    ctr = defaultdict(lambda: defaultdict(float))
+    calls = defaultdict(lambda: defaultdict(int))
+    for f in glob.glob(os.path.join(d, "pmc_*", "run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            ctr[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            calls[k][r["Counter_Name"]] += 1
+    out = {}
+    for k in ctr:
+        if not any(w in k for w in want):
+            continue
+        c = ctr[k]
+        n = max(calls[k].values())
+        tot_ns = sum(dur.get(k, [0])) or 1
+        avg_ns = tot_ns / max(1, len(dur.get(k, [1])))
+        res = {"dispatches": n, "avg_us_trace": round(avg_ns / 1e3, 2)}
+        if "FETCH_SIZE" in c:
+            fb = 2 * c["FETCH_SIZE"] * 1024 / calls[k]["FETCH_SIZE"]
+            res["fetch_bytes_per_dispatch_x2"] = round(fb)
+        if "WRITE_SIZE" in c:
+            wb = c["WRITE_SIZE"] * 1024 / calls[k]["WRITE_SIZE"]
+            res["write_bytes_per_dispatch"] = round(wb)
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            res["hbm_bytes_per_dispatch"] = round(fb + wb)
+            res["hbm_GBs_at_trace_avg"] = round((fb + wb) / avg_ns, 1)
+        for name in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+                     "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"):
+            if name in c:
+                res[name + "_per_dispatch"] = round(c[name] / calls[k][name])
+        if "SQ_WAVE_CYCLES" in c and "SQ_WAIT_ANY" in c:
+            res["wait_any_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 3)
+        if "SQ_WAVE_CYCLES" in c and "SQ_ACTIVE_INST_VALU" in c:
+            res["valu_active_frac"] = round(c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"], 3)
+        out[k] = res
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
