@@ -1,0 +1,603 @@
+// imageio.cpp — see imageio.hpp.
+#include "imageio.hpp"
+
+#include <zlib.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+namespace ofio {
+
+// ------------------------------------------------------------------ files
+bool read_file(const std::string &path, std::string &out, std::string &err, bool gunzip_if_gz) {
+  out.clear();
+  const bool gz = gunzip_if_gz && path.size() >= 3 && path.compare(path.size() - 3, 3, ".gz") == 0;
+  if (gz) {
+    gzFile f = gzopen(path.c_str(), "rb");
+    if (!f) {
+      err = "cannot open " + path;
+      return false;
+    }
+    char buf[1 << 16];
+    int n;
+    while ((n = gzread(f, buf, sizeof buf)) > 0) out.append(buf, (size_t)n);
+    const bool bad = n < 0;
+    gzclose(f);
+    if (bad) {
+      err = "gzip error reading " + path;
+      return false;
+    }
+    return true;
+  }
+  std::ifstream f(path, std::ios::binary);
+  if (!f) {
+    err = "cannot open " + path;
+    return false;
+  }
+  std::ostringstream ss;
+  ss << f.rdbuf();
+  out = ss.str();
+  return true;
+}
+
+static inline uint32_t be32(const uint8_t *p) {
+  return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+}
+
+// libpng png_set_rgb_to_gray(png, 1, 0.299, 0.587) as OpenCV's PNG decoder requests
+// for IMREAD_GRAYSCALE: 15-bit fixed-point coefficients.
+static inline uint8_t rgb_to_gray_png(unsigned r, unsigned g, unsigned b) {
+  if (r == g && r == b) return (uint8_t)r;
+  const unsigned rc = 9798, gc = 19235, bc = 32768 - 9798 - 19235;
+  return (uint8_t)((rc * r + gc * g + bc * b + 16384) >> 15);
+}
+
+// ------------------------------------------------------------------ PNG
+static bool decode_png(const std::string &buf, Image8 &img, std::string &err) {
+  const uint8_t *p = (const uint8_t *)buf.data();
+  const size_t n = buf.size();
+  size_t off = 8;
+  uint32_t W = 0, H = 0;
+  int depth = 0, ctype = -1, interlace = 0;
+  std::vector<uint8_t> idat, plte;
+  while (off + 12 <= n) {
+    const uint32_t len = be32(p + off);
+    const char *type = (const char *)p + off + 4;
+    if (off + 12 + (size_t)len > n) break;
+    const uint8_t *d = p + off + 8;
+    if (!memcmp(type, "IHDR", 4) && len >= 13) {
+      W = be32(d);
+      H = be32(d + 4);
+      depth = d[8];
+      ctype = d[9];
+      interlace = d[12];
+    } else if (!memcmp(type, "PLTE", 4)) {
+      plte.assign(d, d + len);
+    } else if (!memcmp(type, "IDAT", 4)) {
+      idat.insert(idat.end(), d, d + len);
+    } else if (!memcmp(type, "IEND", 4)) {
+      break;
+    }
+    off += 12 + (size_t)len;
+  }
+  if (!W || !H || ctype < 0) {
+    err = "PNG: missing IHDR";
+    return false;
+  }
+  if (interlace) {
+    err = "PNG: interlaced images are not supported";
+    return false;
+  }
+  int ch;
+  switch (ctype) {
+    case 0: ch = 1; break;
+    case 2: ch = 3; break;
+    case 3: ch = 1; break;
+    case 4: ch = 2; break;
+    case 6: ch = 4; break;
+    default: err = "PNG: bad colour type"; return false;
+  }
+  const size_t rowbytes = ((size_t)W * ch * depth + 7) / 8;
+  const size_t bpp = std::max<size_t>(1, (size_t)ch * depth / 8);
+  std::vector<uint8_t> raw((rowbytes + 1) * H);
+  z_stream zs;
+  memset(&zs, 0, sizeof zs);
+  if (inflateInit(&zs) != Z_OK) {
+    err = "PNG: zlib init failed";
+    return false;
+  }
+  zs.next_in = idat.data();
+  zs.avail_in = (uInt)idat.size();
+  zs.next_out = raw.data();
+  zs.avail_out = (uInt)raw.size();
+  const int zr = inflate(&zs, Z_FINISH);
+  inflateEnd(&zs);
+  if (zr != Z_STREAM_END && zs.avail_out != 0) {
+    err = "PNG: corrupt image data";
+    return false;
+  }
+  // unfilter in place (each row: 1 filter byte + rowbytes)
+  std::vector<uint8_t> prev(rowbytes, 0);
+  std::vector<uint8_t> px((size_t)rowbytes * H);
+  for (uint32_t y = 0; y < H; ++y) {
+    const uint8_t f = raw[y * (rowbytes + 1)];
+    const uint8_t *in = raw.data() + y * (rowbytes + 1) + 1;
+    uint8_t *out = px.data() + (size_t)y * rowbytes;
+    for (size_t i = 0; i < rowbytes; ++i) {
+      const unsigned a = i >= bpp ? out[i - bpp] : 0;
+      const unsigned b = prev[i];
+      const unsigned c = i >= bpp ? prev[i - bpp] : 0;
+      unsigned v = in[i];
+      switch (f) {
+        case 0: break;
+        case 1: v += a; break;
+        case 2: v += b; break;
+        case 3: v += (a + b) >> 1; break;
+        case 4: {
+          const int pp = (int)a + (int)b - (int)c;
+          const int pa = abs(pp - (int)a), pb = abs(pp - (int)b), pc = abs(pp - (int)c);
+          v += (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+          break;
+        }
+        default: err = "PNG: bad filter type"; return false;
+      }
+      out[i] = (uint8_t)v;
+    }
+    memcpy(prev.data(), out, rowbytes);
+  }
+  img.width = (int)W;
+  img.height = (int)H;
+  img.data.assign((size_t)W * H, 0);
+  auto sample = [&](const uint8_t *row, uint32_t x, int c) -> unsigned {
+    // returns an 8-bit sample (16-bit: high byte = png_set_strip_16)
+    const size_t idx = (size_t)x * ch + c;
+    if (depth == 8) return row[idx];
+    if (depth == 16) return row[2 * idx];
+    const size_t bit = idx * depth;
+    const unsigned v = (row[bit / 8] >> (8 - depth - (bit % 8))) & ((1u << depth) - 1);
+    return v;
+  };
+  for (uint32_t y = 0; y < H; ++y) {
+    const uint8_t *row = px.data() + (size_t)y * rowbytes;
+    uint8_t *o = img.row((int)y);
+    for (uint32_t x = 0; x < W; ++x) {
+      switch (ctype) {
+        case 0:
+        case 4: {
+          unsigned v = sample(row, x, 0);
+          if (depth < 8) v = v * (255u / ((1u << depth) - 1));  // expand_gray_1_2_4_to_8
+          o[x] = (uint8_t)v;
+          break;
+        }
+        case 3: {
+          const unsigned i = sample(row, x, 0);
+          if ((size_t)i * 3 + 2 >= plte.size()) {
+            err = "PNG: palette index out of range";
+            return false;
+          }
+          o[x] = rgb_to_gray_png(plte[i * 3], plte[i * 3 + 1], plte[i * 3 + 2]);
+          break;
+        }
+        default:
+          o[x] = rgb_to_gray_png(sample(row, x, 0), sample(row, x, 1), sample(row, x, 2));
+      }
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ TIFF
+namespace {
+struct TiffReader {
+  const uint8_t *p;
+  size_t n;
+  bool le;
+  uint16_t u16(size_t o) const {
+    if (o + 2 > n) return 0;
+    return le ? (uint16_t)(p[o] | p[o + 1] << 8) : (uint16_t)(p[o] << 8 | p[o + 1]);
+  }
+  uint32_t u32(size_t o) const {
+    if (o + 4 > n) return 0;
+    return le ? (uint32_t)p[o] | (uint32_t)p[o + 1] << 8 | (uint32_t)p[o + 2] << 16 |
+                    (uint32_t)p[o + 3] << 24
+              : (uint32_t)p[o] << 24 | (uint32_t)p[o + 1] << 16 | (uint32_t)p[o + 2] << 8 | p[o + 3];
+  }
+};
+
+bool lzw_decode(const uint8_t *in, size_t n, std::vector<uint8_t> &out, size_t expect) {
+  struct Ent {
+    int prefix;
+    uint8_t first, last;
+    int len;
+  };
+  std::vector<Ent> tab(4096);
+  auto reset = [&]() {
+    for (int i = 0; i < 256; ++i) tab[i] = {-1, (uint8_t)i, (uint8_t)i, 1};
+  };
+  reset();
+  int next = 258, width = 9, old = -1;
+  size_t bitpos = 0;
+  auto read = [&](int w) -> int {
+    if (bitpos + w > n * 8) return 257;
+    int v = 0;
+    for (int i = 0; i < w; ++i, ++bitpos) v = (v << 1) | ((in[bitpos >> 3] >> (7 - (bitpos & 7))) & 1);
+    return v;
+  };
+  auto emit = [&](int code) {
+    const size_t start = out.size();
+    out.resize(start + tab[code].len);
+    int c = code;
+    for (int i = tab[code].len - 1; i >= 0; --i) {
+      out[start + i] = tab[c].last;
+      c = tab[c].prefix;
+    }
+  };
+  while (out.size() < expect) {
+    int code = read(width);
+    if (code == 257) break;
+    if (code == 256) {
+      reset();
+      next = 258;
+      width = 9;
+      code = read(width);
+      if (code == 257) break;
+      if (code > 255) return false;
+      emit(code);
+      old = code;
+      continue;
+    }
+    if (old < 0) return false;
+    if (code < next) {
+      emit(code);
+      if (next < 4096) tab[next] = {old, tab[old].first, tab[code].first, tab[old].len + 1}, ++next;
+    } else if (code == next) {
+      if (next < 4096) tab[next] = {old, tab[old].first, tab[old].first, tab[old].len + 1}, ++next;
+      emit(code);
+    } else {
+      return false;
+    }
+    old = code;
+    if (next >= (1 << width) - 1 && width < 12) ++width;  // TIFF "early change"
+  }
+  return true;
+}
+}  // namespace
+
+static bool decode_tiff(const std::string &buf, Image8 &img, std::string &err) {
+  TiffReader t{(const uint8_t *)buf.data(), buf.size(), buf[0] == 'I'};
+  const uint32_t ifd = t.u32(4);
+  const uint16_t nent = t.u16(ifd);
+  uint32_t W = 0, H = 0, bps = 8, comp = 1, photo = 1, spp = 1, rps = 0, planar = 1, pred = 1,
+           fmt = 1;
+  std::vector<uint32_t> offs, cnts;
+  auto values = [&](size_t e, std::vector<uint32_t> &v) {
+    const uint16_t type = t.u16(e + 2);
+    const uint32_t cnt = t.u32(e + 4);
+    const size_t sz = type == 3 ? 2 : 4;
+    const size_t base = cnt * sz <= 4 ? e + 8 : t.u32(e + 8);
+    v.resize(cnt);
+    for (uint32_t i = 0; i < cnt; ++i) v[i] = sz == 2 ? t.u16(base + i * 2) : t.u32(base + i * 4);
+  };
+  for (uint16_t i = 0; i < nent; ++i) {
+    const size_t e = ifd + 2 + (size_t)i * 12;
+    const uint16_t tag = t.u16(e);
+    std::vector<uint32_t> v;
+    values(e, v);
+    const uint32_t v0 = v.empty() ? 0 : v[0];
+    switch (tag) {
+      case 256: W = v0; break;
+      case 257: H = v0; break;
+      case 258: bps = v0; break;
+      case 259: comp = v0; break;
+      case 262: photo = v0; break;
+      case 273: offs = v; break;
+      case 277: spp = v0; break;
+      case 278: rps = v0; break;
+      case 279: cnts = v; break;
+      case 284: planar = v0; break;
+      case 317: pred = v0; break;
+      case 339: fmt = v0; break;
+      default: break;
+    }
+  }
+  if (!W || !H || offs.empty() || offs.size() != cnts.size()) {
+    err = "TIFF: unsupported layout (need strips)";
+    return false;
+  }
+  if ((bps != 8 && bps != 16) || fmt == 3 || (spp != 1 && spp != 3 && spp != 4) || planar != 1) {
+    err = "TIFF: only 8/16-bit integer, 1/3/4 samples, chunky layout supported";
+    return false;
+  }
+  if (!rps) rps = H;
+  const size_t bytes_pp = (size_t)spp * bps / 8;
+  const size_t rowbytes = (size_t)W * bytes_pp;
+  std::vector<uint8_t> px;
+  px.reserve(rowbytes * H);
+  for (size_t s = 0; s < offs.size(); ++s) {
+    if ((size_t)offs[s] + cnts[s] > t.n) {
+      err = "TIFF: strip out of range";
+      return false;
+    }
+    const uint8_t *src = t.p + offs[s];
+    const size_t rows = std::min<size_t>(rps, H - std::min<size_t>(H, s * rps));
+    const size_t expect = rows * rowbytes;
+    std::vector<uint8_t> strip;
+    if (comp == 1) {
+      strip.assign(src, src + std::min<size_t>(cnts[s], expect));
+    } else if (comp == 5) {
+      if (!lzw_decode(src, cnts[s], strip, expect)) {
+        err = "TIFF: corrupt LZW strip";
+        return false;
+      }
+    } else if (comp == 8 || comp == 32946) {
+      strip.resize(expect);
+      uLongf dl = (uLongf)expect;
+      if (uncompress(strip.data(), &dl, src, cnts[s]) != Z_OK) {
+        err = "TIFF: corrupt deflate strip";
+        return false;
+      }
+    } else if (comp == 32773) {  // PackBits
+      size_t i = 0;
+      while (i < cnts[s] && strip.size() < expect) {
+        const int8_t c = (int8_t)src[i++];
+        if (c >= 0) {
+          strip.insert(strip.end(), src + i, src + std::min<size_t>(cnts[s], i + c + 1));
+          i += c + 1;
+        } else if (c != -128) {
+          if (i < cnts[s]) strip.insert(strip.end(), (size_t)(1 - c), src[i]);
+          ++i;
+        }
+      }
+    } else {
+      err = "TIFF: unsupported compression " + std::to_string(comp);
+      return false;
+    }
+    strip.resize(expect, 0);
+    if (pred == 2) {  // horizontal differencing
+      for (size_t r = 0; r < rows; ++r) {
+        uint8_t *row = strip.data() + r * rowbytes;
+        if (bps == 8) {
+          for (size_t i = spp; i < rowbytes; ++i) row[i] = (uint8_t)(row[i] + row[i - spp]);
+        } else {
+          for (size_t i = spp; i < (size_t)W * spp; ++i) {
+            const size_t a = 2 * i, b = 2 * (i - spp);
+            uint16_t cur = t.le ? (uint16_t)(row[a] | row[a + 1] << 8) : (uint16_t)(row[a] << 8 | row[a + 1]);
+            const uint16_t pv = t.le ? (uint16_t)(row[b] | row[b + 1] << 8) : (uint16_t)(row[b] << 8 | row[b + 1]);
+            cur = (uint16_t)(cur + pv);
+            if (t.le) { row[a] = (uint8_t)cur; row[a + 1] = (uint8_t)(cur >> 8); }
+            else { row[a] = (uint8_t)(cur >> 8); row[a + 1] = (uint8_t)cur; }
+          }
+        }
+      }
+    }
+    px.insert(px.end(), strip.begin(), strip.end());
+  }
+  img.width = (int)W;
+  img.height = (int)H;
+  img.data.assign((size_t)W * H, 0);
+  for (uint32_t y = 0; y < H; ++y) {
+    const uint8_t *row = px.data() + (size_t)y * rowbytes;
+    uint8_t *o = img.row((int)y);
+    for (uint32_t x = 0; x < W; ++x) {
+      unsigned s[3];
+      for (uint32_t c = 0; c < std::min<uint32_t>(spp, 3); ++c) {
+        const size_t i = ((size_t)x * spp + c) * (bps / 8);
+        s[c] = bps == 8 ? row[i] : (t.le ? row[i + 1] : row[i]);  // 16-bit: high byte
+      }
+      unsigned v;
+      if (spp == 1) {
+        v = s[0];
+        if (photo == 0) v = 255 - v;  // WhiteIsZero
+      } else {  // cv::cvtColor(RGB2GRAY): 14-bit fixed point
+        v = (s[0] * 4899 + s[1] * 9617 + s[2] * 1868 + (1 << 13)) >> 14;
+      }
+      o[x] = (uint8_t)v;
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ PGM
+static bool decode_pgm(const std::string &buf, Image8 &img, std::string &err) {
+  size_t i = 2;
+  int vals[3];
+  for (int k = 0; k < 3; ++k) {
+    while (i < buf.size()) {
+      if (buf[i] == '#') {
+        while (i < buf.size() && buf[i] != '\n') ++i;
+      } else if (isspace((unsigned char)buf[i])) {
+        ++i;
+      } else {
+        break;
+      }
+    }
+    int v = 0;
+    while (i < buf.size() && isdigit((unsigned char)buf[i])) v = v * 10 + (buf[i++] - '0');
+    vals[k] = v;
+  }
+  ++i;
+  const int W = vals[0], H = vals[1], maxv = vals[2];
+  const size_t bps = maxv > 255 ? 2 : 1;
+  if (W <= 0 || H <= 0 || buf.size() < i + (size_t)W * H * bps) {
+    err = "PGM: truncated";
+    return false;
+  }
+  img.width = W;
+  img.height = H;
+  img.data.resize((size_t)W * H);
+  for (size_t k = 0; k < (size_t)W * H; ++k) img.data[k] = (uint8_t)buf[i + k * bps];
+  return true;
+}
+
+bool read_gray8(const std::string &path, Image8 &img, std::string &err) {
+  std::string buf;
+  img = Image8();
+  if (!read_file(path, buf, err, false)) return false;
+  if (buf.size() >= 8 && !memcmp(buf.data(), "\x89PNG\r\n\x1a\n", 8)) return decode_png(buf, img, err);
+  if (buf.size() >= 8 && (!memcmp(buf.data(), "II*\0", 4) || !memcmp(buf.data(), "MM\0*", 4)))
+    return decode_tiff(buf, img, err);
+  if (buf.size() >= 2 && buf[0] == 'P' && buf[1] == '5') return decode_pgm(buf, img, err);
+  err = "unsupported image format: " + path;
+  return false;
+}
+
+// ------------------------------------------------------------------ resize
+static inline int cv_round(double v) { return (int)std::lrint(v); }
+static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+void resize_u8(const Image8 &src, double fx, double fy, Image8 &dst) {
+  const int sw = src.width, sh = src.height;
+  const int dw = cv_round(sw * fx), dh = cv_round(sh * fy);
+  Image8 out;
+  out.width = dw;
+  out.height = dh;
+  out.data.assign((size_t)dw * dh, 0);
+  if (dw == sw && dh == sh) {
+    out.data = src.data;
+    dst = std::move(out);
+    return;
+  }
+  const double scale_x = 1. / fx, scale_y = 1. / fy;
+  const int iscale_x = cv_round(scale_x), iscale_y = cv_round(scale_y);
+  const bool area_fast = std::abs(scale_x - iscale_x) < DBL_EPSILON &&
+                         std::abs(scale_y - iscale_y) < DBL_EPSILON;
+  if (area_fast && iscale_x == 2 && iscale_y == 2) {
+    // INTER_LINEAR at exactly 1/2 -> INTER_AREA fast path: 2x2 mean.  The vector part
+    // of OpenCV's 8u kernel rounds (s + 2) >> 2, its scalar tail cvRound(s * 0.25f);
+    // partial 2x2 cells at odd borders average the samples that exist.
+    const int dwidth1 = sw / 2;
+    for (int dy = 0; dy < dh; ++dy) {
+      uint8_t *D = out.row(dy);
+      const int sy0 = dy * 2;
+      if (sy0 >= sh) continue;
+      const int w = sy0 + 2 <= sh ? dwidth1 : 0;
+      int dx = 0;
+      const uint8_t *S0 = src.row(sy0);
+      const uint8_t *S1 = sy0 + 1 < sh ? src.row(sy0 + 1) : S0;
+      for (; dx + 8 <= w; dx += 8)
+        for (int k = dx; k < dx + 8; ++k)
+          D[k] = (uint8_t)((S0[2 * k] + S0[2 * k + 1] + S1[2 * k] + S1[2 * k + 1] + 2) >> 2);
+      for (; dx < w; ++dx) {
+        const int s = S0[2 * dx] + S0[2 * dx + 1] + S1[2 * dx] + S1[2 * dx + 1];
+        D[dx] = sat_u8(cv_round((float)s * 0.25f));
+      }
+      for (; dx < dw; ++dx) {
+        int sum = 0, count = 0;
+        const int sx0 = dx * 2;
+        for (int sy = 0; sy < 2 && sy0 + sy < sh; ++sy)
+          for (int sx = 0; sx < 2 && sx0 + sx < sw; ++sx) {
+            sum += src.row(sy0 + sy)[sx0 + sx];
+            ++count;
+          }
+        D[dx] = count ? sat_u8(cv_round((float)sum / count)) : 0;
+      }
+    }
+    dst = std::move(out);
+    return;
+  }
+  // Generic INTER_LINEAR (resizeGeneric_ with 11-bit fixed-point coefficients).
+  constexpr int BITS = 11, SCALE = 1 << BITS;
+  std::vector<int> xofs(dw), yofs(dh);
+  std::vector<short> ax(2 * dw), ay(2 * dh);
+  for (int dx = 0; dx < dw; ++dx) {
+    float f = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = (int)std::floor(f);
+    f -= sx;
+    if (sx < 0) {
+      f = 0, sx = 0;
+    }
+    if (sx >= sw - 1) {
+      f = 0, sx = sw - 1;
+    }
+    xofs[dx] = sx;
+    ax[2 * dx] = (short)cv_round((1.f - f) * SCALE);
+    ax[2 * dx + 1] = (short)(SCALE - ax[2 * dx]);
+  }
+  for (int dy = 0; dy < dh; ++dy) {
+    float f = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = (int)std::floor(f);
+    f -= sy;
+    if (sy < 0) {
+      f = 0, sy = 0;
+    }
+    if (sy >= sh - 1) {
+      f = 0, sy = sh - 1;
+    }
+    yofs[dy] = sy;
+    ay[2 * dy] = (short)cv_round((1.f - f) * SCALE);
+    ay[2 * dy + 1] = (short)(SCALE - ay[2 * dy]);
+  }
+  std::vector<int> h0(dw), h1(dw);
+  auto hres = [&](const uint8_t *S, std::vector<int> &D) {
+    for (int dx = 0; dx < dw; ++dx) {
+      const int sx = xofs[dx];
+      D[dx] = sx + 1 < sw ? S[sx] * ax[2 * dx] + S[sx + 1] * ax[2 * dx + 1] : S[sx] * SCALE;
+    }
+  };
+  for (int dy = 0; dy < dh; ++dy) {
+    const int sy = yofs[dy];
+    hres(src.row(sy), h0);
+    hres(src.row(std::min(sy + 1, sh - 1)), h1);
+    uint8_t *D = out.row(dy);
+    for (int dx = 0; dx < dw; ++dx)
+      D[dx] = sat_u8((ay[2 * dy] * h0[dx] + ay[2 * dy + 1] * h1[dx] + (1 << (2 * BITS - 1))) >> (2 * BITS));
+  }
+  dst = std::move(out);
+}
+
+// ------------------------------------------------------------------ TIFF write
+static bool write_tiff(const std::string &path, const void *data, int W, int H, size_t pitch,
+                       int bps, int fmt, std::string &err) {
+  FILE *f = fopen(path.c_str(), "wb");
+  if (!f) {
+    err = "cannot write " + path;
+    return false;
+  }
+  const uint32_t rowb = (uint32_t)W * (bps / 8);
+  const uint32_t img_bytes = rowb * (uint32_t)H;
+  const uint16_t nent = 10;
+  const uint32_t ifd_off = 8;
+  const uint32_t data_off = ifd_off + 2 + nent * 12 + 4;
+  std::vector<uint8_t> h;
+  auto p16 = [&](uint16_t v) { h.push_back(v & 0xff); h.push_back(v >> 8); };
+  auto p32 = [&](uint32_t v) { for (int i = 0; i < 4; ++i) h.push_back((v >> (8 * i)) & 0xff); };
+  auto ent = [&](uint16_t tag, uint16_t type, uint32_t cnt, uint32_t val) {
+    p16(tag); p16(type); p32(cnt);
+    if (type == 3) { p16((uint16_t)val); p16(0); } else { p32(val); }
+  };
+  h.insert(h.end(), {'I', 'I', 42, 0});
+  p32(ifd_off);
+  p16(nent);
+  ent(256, 4, 1, (uint32_t)W);        // ImageWidth
+  ent(257, 4, 1, (uint32_t)H);        // ImageLength
+  ent(258, 3, 1, (uint32_t)bps);      // BitsPerSample
+  ent(259, 3, 1, 1);                  // Compression: none
+  ent(262, 3, 1, 1);                  // Photometric: BlackIsZero
+  ent(273, 4, 1, data_off);           // StripOffsets
+  ent(277, 3, 1, 1);                  // SamplesPerPixel
+  ent(278, 4, 1, (uint32_t)H);        // RowsPerStrip
+  ent(279, 4, 1, img_bytes);          // StripByteCounts
+  ent(339, 3, 1, (uint32_t)fmt);      // SampleFormat (1 uint, 3 IEEE float)
+  p32(0);                             // next IFD
+  bool ok = fwrite(h.data(), 1, h.size(), f) == h.size();
+  for (int y = 0; y < H && ok; ++y)
+    ok = fwrite((const char *)data + (size_t)y * pitch, 1, rowb, f) == rowb;
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) err = "short write to " + path;
+  return ok;
+}
+
+bool write_tiff_f32(const std::string &path, const float *data, int W, int H, size_t pitch,
+                    std::string &err) {
+  return write_tiff(path, data, W, H, pitch, 32, 3, err);
+}
+
+bool write_tiff_u8(const std::string &path, const Image8 &img, std::string &err) {
+  return write_tiff(path, img.data.data(), img.width, img.height, (size_t)img.width, 8, 1, err);
+}
+
+}  // namespace ofio

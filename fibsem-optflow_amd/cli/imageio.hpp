@@ -1,0 +1,48 @@
+// imageio.hpp — host-side image I/O of the optflow CLI (no OpenCV, no libpng/libtiff).
+//
+// Restates what the reference gets from OpenCV's imgcodecs/imgproc on the host
+// (/root/reference/src/optflow.cpp):
+//   cv::imread(path, IMREAD_GRAYSCALE)            :106, :119  -> read_gray8()
+//   cv::resize(frame, frame, Size(), scale, scale) :113, :125  -> resize_u8()
+//   cv::imwrite(file, CV_32FC1 flow)               :482-483    -> write_tiff_f32()
+// Formats: PNG (gray/RGB/RGBA/palette, 1-16 bit, non-interlaced), baseline TIFF
+// (uncompressed, LZW or deflate; 8/16-bit; 1 or 3 samples), binary PGM (P5).
+// OpenCV's exact colour-to-gray and 16->8-bit conversions are restated from its
+// published sources and are NOT verifiable here (OpenCV is absent):
+// FIB-SEM slices are 8-bit grayscale, for which decoding is exact.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ofio {
+
+struct Image8 {
+  int width = 0, height = 0;
+  std::vector<uint8_t> data;  // row-major, pitch == width
+  uint8_t *row(int y) { return data.data() + (size_t)y * width; }
+  const uint8_t *row(int y) const { return data.data() + (size_t)y * width; }
+};
+
+// Read a whole file; a ".gz" suffix is gunzipped (boost gzip_decompressor at
+// optflow.cpp:43-52).  Returns false and sets err on failure.
+bool read_file(const std::string &path, std::string &out, std::string &err, bool gunzip_if_gz);
+
+// cv::imread(path, IMREAD_GRAYSCALE).  Returns false (empty image) on failure,
+// which the caller reports like optflow.cpp:108-112.
+bool read_gray8(const std::string &path, Image8 &img, std::string &err);
+
+// cv::resize(src, dst, Size(), fx, fy, INTER_LINEAR) for CV_8UC1 on the CPU:
+// dst size = round(src * f) (half-even); an exact 1/2 scale takes OpenCV's
+// INTER_AREA fast path (2x2 mean), other scales half-pixel-centre bilinear with
+// 11-bit fixed-point weights.
+void resize_u8(const Image8 &src, double fx, double fy, Image8 &dst);
+
+// Single-channel float32 TIFF (uncompressed, SampleFormat=IEEE float).
+bool write_tiff_f32(const std::string &path, const float *data, int width, int height,
+                    size_t pitch_bytes, std::string &err);
+// Single-channel 8-bit TIFF (uncompressed).
+bool write_tiff_u8(const std::string &path, const Image8 &img, std::string &err);
+
+}  // namespace ofio

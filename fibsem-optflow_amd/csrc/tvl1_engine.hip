@@ -620,7 +620,8 @@ tvl1_status tvl1_postprocess(tvl1_ctx *c, float *u, float *v, size_t fpitch, con
                              size_t pitch1, int32_t W, int32_t H, int32_t mode, void *stream) {
   tvl1_status s = check_call(c, I1, pitch1, I1, pitch1, W, H, u, v, fpitch);
   if (s != TVL1_OK) return s;
-  if (mode != 0 && mode != 1) return set_err(c, TVL1_EINVAL, "mode must be 0 (flow) or 1 (map)");
+  if (mode < 0 || mode > 2)
+    return set_err(c, TVL1_EINVAL, "mode must be 0 (flow), 1 (map) or 2 (map - grid)");
   HIP_TRY(c, hipSetDevice(c->device));
   hipLaunchKernelGGL(k_postprocess, grid2(W, H), kBlk2, 0, (hipStream_t)stream, u, v, fpitch, I1,
                      pitch1, W, H, mode);

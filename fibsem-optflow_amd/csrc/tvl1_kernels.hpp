@@ -768,8 +768,10 @@ __global__ void k_output(const float *__restrict__ u1, const float *__restrict__
   reinterpret_cast<float *>(reinterpret_cast<char *>(ov) + (size_t)y * opitch)[x] = u2[(size_t)y * P + x];
 }
 
-// solve_wrapper post-ops (optflow.cpp:445-473): map = flow + (x, y) (mode 1), then
-// zero where I1 <= 1 (threshold THRESH_BINARY_INV + setTo(0, mask)).
+// solve_wrapper post-ops (optflow.cpp:411-473): map = flow + (x, y) (mode 1); the
+// features branch with output_type "flow" (mode 2: (flow + grid) warped by the
+// alignment, identity here, minus grid); then zero where I1 <= 1
+// (threshold THRESH_BINARY_INV + setTo(0, mask)).
 __global__ void k_postprocess(float *__restrict__ u, float *__restrict__ v, size_t fp,
                               const uint8_t *__restrict__ I1, size_t p1, int W, int H,
                               int mode) {
@@ -779,9 +781,13 @@ __global__ void k_postprocess(float *__restrict__ u, float *__restrict__ v, size
   float *ur = reinterpret_cast<float *>(reinterpret_cast<char *>(u) + (size_t)y * fp);
   float *vr = reinterpret_cast<float *>(reinterpret_cast<char *>(v) + (size_t)y * fp);
   float a = ur[x], b = vr[x];
-  if (mode == 1) {
+  if (mode >= 1) {  // map = flow + pixel grid
     a = a + (float)x;
     b = b + (float)y;
+  }
+  if (mode == 2) {  // features path with output_type "flow": flow = map - grid
+    a = a - (float)x;
+    b = b - (float)y;
   }
   if (I1[(size_t)y * p1 + x] <= 1) {
     a = 0.0f;

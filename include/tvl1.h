@@ -134,9 +134,11 @@ tvl1_status tvl1_calc_host(tvl1_ctx *ctx,
                            float *u, float *v, size_t flow_pitch,
                            tvl1_stats *stats);
 
-/* Output post-processing of solve_wrapper (optflow.cpp:445-473), in place on
- * device u, v:  mode 0 = "flow" (unchanged), 1 = "map" (u += x, v += y);
- * then u = v = 0 wherever I1 <= 1 (cuda::threshold THRESH_BINARY_INV + setTo). */
+/* Output post-processing of solve_wrapper (optflow.cpp:411-473), in place on
+ * device u, v:  mode 0 = "flow" (unchanged), 1 = "map" (u += x, v += y),
+ * 2 = features branch with output_type "flow" under an identity alignment
+ * (u = (u + x) - x, optflow.cpp:429-437); then u = v = 0 wherever I1 <= 1
+ * (cuda::threshold THRESH_BINARY_INV + setTo). */
 tvl1_status tvl1_postprocess(tvl1_ctx *ctx, float *u, float *v, size_t flow_pitch,
                              const uint8_t *I1, size_t pitch1,
                              int32_t width, int32_t height, int32_t mode, void *stream);

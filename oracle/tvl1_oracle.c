@@ -308,17 +308,22 @@ void orc_median(const float *src, int w, int h, int k, float *dst) {
     }
 }
 
-/* solve_wrapper post-ops (optflow.cpp:445-473): map = flow + (x, y) when mode==1;
- * then zero both fields where I1 <= 1 (threshold THRESH_BINARY_INV + setTo). */
+/* solve_wrapper post-ops (optflow.cpp:411-473): map = flow + (x, y) when mode>=1,
+ * mode 2 subtracts the grid again (features branch, identity alignment); then zero
+ * both fields where I1 <= 1 (threshold THRESH_BINARY_INV + setTo). */
 void orc_postprocess(float *u, float *v, size_t flow_pitch, const uint8_t *I1, size_t pitch1,
                      int w, int h, int mode) {
   for (int y = 0; y < h; ++y) {
     float *ur = (float *)((char *)u + (size_t)y * flow_pitch);
     float *vr = (float *)((char *)v + (size_t)y * flow_pitch);
     for (int x = 0; x < w; ++x) {
-      if (mode == 1) {
+      if (mode >= 1) {
         ur[x] = ur[x] + (float)x;
         vr[x] = vr[x] + (float)y;
+      }
+      if (mode == 2) {
+        ur[x] = ur[x] - (float)x;
+        vr[x] = vr[x] - (float)y;
       }
       if (I1[(size_t)y * pitch1 + x] <= 1) {
         ur[x] = 0.0f;

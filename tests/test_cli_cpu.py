@@ -1,0 +1,185 @@
+"""CPU tests of the optflow CLI surface (reference /root/reference/src/optflow.cpp:29-178,
+228-261, 302-392, 500-514): config precedence, ROI geometry,
+output naming, gz configs, comments, error reporting and image decoding.
+`optflow --plan` resolves everything the pair loop would do without a GPU."""
+import gzip
+import json
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from optflow_amd import capi
+
+OPTFLOW = capi.PKG_ROOT / "bin" / "optflow"
+REF_EXAMPLE = Path("/root/reference/docs/example.json")
+
+
+def run(*args, check=True):
+    r = subprocess.run([str(OPTFLOW), *map(str, args)], capture_output=True, text=True,
+                       timeout=120)
+    if check and r.returncode != 0:
+        raise AssertionError(f"optflow {args} failed ({r.returncode}): {r.stderr}")
+    return r
+
+
+def plan(cfg_path):
+    out = run("--plan", cfg_path).stdout
+    return json.loads(out[out.index("\n[") + 1:] if not out.startswith("[") else out)
+
+
+@pytest.fixture
+def slices(tmp_path, built):
+    rng = np.random.default_rng(3)
+    paths = []
+    for z in range(3):
+        a = rng.integers(0, 256, (61, 83), dtype=np.uint8)
+        p = tmp_path / f"z{z}.png"
+        Image.fromarray(a).save(p)
+        paths.append(p)
+    return paths
+
+
+def write_cfg(tmp_path, cfg, name="cfg.json", gz=False, text=None):
+    p = tmp_path / (name + (".gz" if gz else ""))
+    data = (text if text is not None else json.dumps(cfg)).encode()
+    if gz:
+        with gzip.open(p, "wb") as f:
+            f.write(data)
+    else:
+        p.write_bytes(data)
+    return p
+
+
+def test_help(built):
+    r = run("--help")
+    assert "Usage" in r.stdout
+
+
+def test_defaults_and_precedence(tmp_path, slices):
+    cfg = {"output_dir": str(tmp_path), "nscales": 5, "tau": 0.3,
+           "images": [{"p": str(slices[0]), "q": str(slices[1]), "output_name": "a"},
+                      {"p": str(slices[1]), "q": str(slices[2]), "output_name": "b",
+                       "scale": 1, "tau": 0.2, "warps": 7, "rois": {"top": 10}}]}
+    pl = plan(write_cfg(tmp_path, cfg))
+    a, b = pl
+    # scale default 0.5 (optflow.cpp:92); output = output_dir/output_name_%0.2f (:155-157)
+    assert a["scale"] == 0.5 and a["output"] == f"{tmp_path}/a_0.50"
+    assert a["size0"] == [42, 30]          # round-half-even(83*0.5)=42, round(61*0.5)=30
+    # TV args: per-image -> global -> default (optflow.cpp:503-512)
+    assert a["tv"] == {"tau": 0.3, "lambda": 0.05, "theta": 0.3, "nscales": 5, "warps": 5,
+                       "epsilon": 0.01, "iterations": 300, "scaleStep": 0.8, "gamma": 0.0,
+                       "medianFiltering": 1}
+    assert b["tv"]["tau"] == 0.2 and b["tv"]["warps"] == 7 and b["tv"]["nscales"] == 5
+    assert b["output"] == f"{tmp_path}/b_1.00" and b["size0"] == [83, 61]
+    # no ROI -> "default" full frame (optflow.cpp:147-154); per-image rois honoured
+    assert a["rois"] == {"default": [0, 0, 42, 30]}
+    assert b["rois"] == {"top": [0, 0, 83, 10]}
+    assert a["output_type"] == "map" and a["features"] is False
+
+
+def test_roi_geometry_and_sorted_order(tmp_path, slices):
+    cfg = {"output_dir": str(tmp_path), "scale": 1.0,
+           "rois": {"top": 12, "bottom": 9, "custom": [3, 4, 20, 10]},
+           "images": [{"p": str(slices[0]), "q": str(slices[1]), "output_name": "x"}]}
+    (pl,) = plan(write_cfg(tmp_path, cfg))
+    # get_rois (optflow.cpp:228-261): top=[0,0,cols,top], bottom=[0,rows-b,cols,b]
+    assert pl["rois"] == {"bottom": [0, 52, 83, 9], "custom": [3, 4, 20, 10],
+                          "top": [0, 0, 83, 12]}
+    # keys processed in sorted order; suffix _top/_bottom only (optflow.cpp:343-350)
+    base = f"{tmp_path}/x_1.00"
+    assert pl["files"] == [base + "_bottom", base, base + "_top"]
+
+
+def test_custom_diff(tmp_path, slices):
+    cfg = {"output_dir": str(tmp_path), "scale": 1,
+           "rois": {"custom": {"0": [0, 0, 30, 20], "1": [5, 6, 30, 20]}},
+           "images": [{"p": str(slices[0]), "q": str(slices[1]), "output_name": "c"}]}
+    (pl,) = plan(write_cfg(tmp_path, cfg))
+    assert pl["rois"] == {"custom_diff": {"0": [0, 0, 30, 20], "1": [5, 6, 30, 20]}}
+
+
+def test_gen_cross_style_gz_shard(tmp_path, slices):
+    """The shard format written by support_scripts/gen_cross_file_list.py:75-99."""
+    cfg = {"style": 1, "debug": False, "homo": 4, "ratio": 0.7, "ransac": 5,
+           "hessianThreshold": 1600, "scale": 0.5, "output_dir": str(tmp_path),
+           "rois": {"top": 10, "bottom": 10}, "output_type": "random_points", "npoints": 25,
+           "host": "render", "port": "8080", "matchCollection": "m", "owner": "o",
+           "images": [{"p": str(slices[0]), "q": str(slices[1]), "pId": "t0", "qId": "t1",
+                       "pGroupId": "1.0", "qGroupId": "2.0", "output_name": "t0_t1"}]}
+    (pl,) = plan(write_cfg(tmp_path, cfg, name="shard_0.json", gz=True))
+    assert pl["output_type"] == "random_points"
+    assert pl["rois"] == {"bottom": [0, 20, 42, 10], "top": [0, 0, 42, 10]}
+    assert pl["output"] == f"{tmp_path}/t0_t1_0.50"
+
+
+def test_features_tristate(tmp_path, slices):
+    base = {"output_dir": str(tmp_path), "images": [{"p": str(slices[0]), "q": str(slices[1])}]}
+    assert plan(write_cfg(tmp_path, {**base, "features": 2}))[0]["features"] is True
+    cfg = {**base, "features": 2}
+    cfg["images"] = [{"p": str(slices[0]), "q": str(slices[1]), "features": False}]
+    assert plan(write_cfg(tmp_path, cfg))[0]["features"] is False
+
+
+def test_comments_allowed(tmp_path, slices):
+    text = ("{ /* block comment */\n \"output_dir\": \"%s\", // line comment\n"
+            " \"images\": [{\"p\": \"%s\", \"q\": \"%s\"}]\n}" % (tmp_path, slices[0], slices[1]))
+    assert len(plan(write_cfg(tmp_path, None, text=text))) == 1
+
+
+def test_malformed_json_is_reported(tmp_path, built):
+    p = write_cfg(tmp_path, None, text='{\n "a": 1\n "b": 2\n}')
+    r = run(p, check=False)
+    assert r.returncode == 2 and "line 3" in r.stderr
+
+
+@pytest.mark.skipif(not REF_EXAMPLE.exists(), reason="reference tree not mounted")
+def test_reference_example_json_defects_are_reported(built):
+    """docs/example.json is not valid JSON (missing commas after lines
+    72 and 81, trailing comma at 67); the reference silently ignores the parse error."""
+    r = run(REF_EXAMPLE, check=False)
+    assert r.returncode == 2 and "line" in r.stderr
+
+
+def test_unreadable_image_reported_and_skipped(tmp_path, slices):
+    cfg = {"output_dir": str(tmp_path),
+           "images": [{"p": str(tmp_path / "missing.png"), "q": str(slices[1])},
+                      {"p": str(slices[0]), "q": str(slices[1])}]}
+    r = run("--plan", write_cfg(tmp_path, cfg))
+    assert f"Error: {tmp_path / 'missing.png'}" in r.stdout
+    assert r.stdout.count(str(slices[0])) >= 1
+
+
+@pytest.mark.parametrize("fmt", ["png", "tif", "tif_lzw", "png16", "pgm"])
+def test_decode_formats(tmp_path, built, fmt):
+    rng = np.random.default_rng(7)
+    a = rng.integers(0, 256, (37, 53), dtype=np.uint8)
+    src = tmp_path / f"in.{fmt.split('_')[0].replace('16', '')}"
+    if fmt == "tif_lzw":
+        Image.fromarray(a).save(src, compression="tiff_lzw")
+    elif fmt == "png16":
+        Image.fromarray(a.astype(np.uint16) * 257).save(src)
+    elif fmt == "pgm":
+        src.write_bytes(b"P5\n53 37\n255\n" + a.tobytes())
+    else:
+        Image.fromarray(a).save(src)
+    out = tmp_path / "out.tif"
+    run("--decode", src, out)
+    assert np.array_equal(np.array(Image.open(out)), a)
+
+
+def test_prescale_half_is_2x2_mean(tmp_path, built):
+    """cv::resize at exactly 0.5 takes OpenCV's INTER_AREA fast path (2x2 mean)."""
+    rng = np.random.default_rng(8)
+    a = rng.integers(0, 256, (40, 64), dtype=np.uint8)
+    src = tmp_path / "a.png"
+    Image.fromarray(a).save(src)
+    out = tmp_path / "o.tif"
+    run("--decode", src, out, 0.5)
+    b = np.array(Image.open(out)).astype(int)
+    s = a.astype(int)
+    ref = (s[0::2, 0::2] + s[1::2, 0::2] + s[0::2, 1::2] + s[1::2, 1::2] + 2) >> 2
+    assert b.shape == (20, 32)
+    assert np.array_equal(b, ref)   # 32 columns = 4 full 8-wide vector blocks

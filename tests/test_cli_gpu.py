@@ -1,0 +1,132 @@
+"""End-to-end: the optflow CLI on the GPU vs the oracle (+ the reference's solve_wrapper
+post-ops).  Outputs must be bit-identical to oracle(ROI crops) + post-processing."""
+import ctypes as C
+import json
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from optflow_amd import capi, synth
+
+pytestmark = pytest.mark.gpu
+OPTFLOW = capi.PKG_ROOT / "bin" / "optflow"
+
+
+def run_cli(cfg, tmp_path, name="cfg.json"):
+    p = tmp_path / name
+    p.write_text(json.dumps(cfg))
+    r = subprocess.run([str(OPTFLOW), str(p)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r
+
+
+def oracle_post(I0, I1, params, mode):
+    u, v, _, _ = capi.oracle_calc(I0, I1, params, warp_iters=False)
+    lib = capi.load_oracle()
+    lib.orc_postprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                    C.c_int, C.c_int, C.c_int]
+    H, W = I0.shape
+    I1c = np.ascontiguousarray(I1)
+    lib.orc_postprocess(u.ctypes.data, v.ctypes.data, 4 * W, I1c.ctypes.data, W, W, H, mode)
+    return u, v
+
+
+@pytest.fixture
+def pair(tmp_path, built):
+    I0, I1 = synth.gen_pair(150, 110, seed=41)
+    I1[:, :6] = 0                       # exercise the I1 <= 1 output mask
+    Image.fromarray(I0).save(tmp_path / "p.png")
+    Image.fromarray(I1).save(tmp_path / "q.png")
+    return I0, I1
+
+
+def tif(path):
+    return np.array(Image.open(path)).astype(np.float32)
+
+
+def test_flow_output_top_bottom_rois(tmp_path, pair):
+    I0, I1 = pair
+    cfg = {"output_dir": str(tmp_path), "scale": 1, "output_type": "flow", "nscales": 4,
+           "warps": 4, "rois": {"top": 40, "bottom": 50},
+           "images": [{"p": str(tmp_path / "p.png"), "q": str(tmp_path / "q.png"),
+                       "output_name": "pq"}]}
+    r = run_cli(cfg, tmp_path)
+    assert f"{tmp_path / 'p.png'} {tmp_path / 'q.png'}" in r.stdout
+    params = capi.make_params(nscales=4, warps=4)
+    for suf, sl in (("_top", np.s_[0:40]), ("_bottom", np.s_[110 - 50:110])):
+        u, v = oracle_post(np.ascontiguousarray(I0[sl]), np.ascontiguousarray(I1[sl]), params, 0)
+        assert np.array_equal(tif(tmp_path / f"pq_1.00{suf}_x.tiff"), u)
+        assert np.array_equal(tif(tmp_path / f"pq_1.00{suf}_y.tiff"), v)
+
+
+def test_map_output_default_roi(tmp_path, pair):
+    """No ROI -> 'default' full frame; the reference would pre-align (features); this
+    build uses the identity transform, so map = flow + grid (then masked)."""
+    I0, I1 = pair
+    cfg = {"output_dir": str(tmp_path), "scale": 1, "nscales": 3, "warps": 3,
+           "images": [{"p": str(tmp_path / "p.png"), "q": str(tmp_path / "q.png"),
+                       "output_name": "m"}]}
+    run_cli(cfg, tmp_path)
+    u, v = oracle_post(I0, I1, capi.make_params(nscales=3, warps=3), 1)
+    assert np.array_equal(tif(tmp_path / "m_1.00_x.tiff"), u)
+    assert np.array_equal(tif(tmp_path / "m_1.00_y.tiff"), v)
+
+
+def test_prescale_half(tmp_path, pair):
+    I0, I1 = pair
+    cfg = {"output_dir": str(tmp_path), "output_type": "flow", "nscales": 3, "warps": 2,
+           "rois": {"custom": [0, 0, 75, 55]},
+           "images": [{"p": str(tmp_path / "p.png"), "q": str(tmp_path / "q.png"),
+                       "output_name": "h"}]}
+    run_cli(cfg, tmp_path)
+    dec = []
+    for n in ("p", "q"):
+        subprocess.run([str(OPTFLOW), "--decode", str(tmp_path / f"{n}.png"),
+                        str(tmp_path / f"{n}_s.tif"), "0.5"], check=True)
+        dec.append(np.array(Image.open(tmp_path / f"{n}_s.tif")))
+    u, v = oracle_post(dec[0], dec[1], capi.make_params(nscales=3, warps=2), 0)
+    assert np.array_equal(tif(tmp_path / "h_0.50_x.tiff"), u)
+
+
+def test_random_points_deterministic_with_debug(tmp_path, pair):
+    cfg = {"output_dir": str(tmp_path), "scale": 1, "output_type": "random_points",
+           "npoints": 10, "debug": True, "nscales": 3, "warps": 2, "rois": {"top": 30},
+           "images": [{"p": str(tmp_path / "p.png"), "q": str(tmp_path / "q.png"),
+                       "pId": "a", "qId": "b", "pGroupId": "1.0", "qGroupId": "2.0"}]}
+    run_cli(cfg, tmp_path)
+    first = (tmp_path / "point_matches_0.json").read_text()
+    run_cli(cfg, tmp_path)
+    assert (tmp_path / "point_matches_0.json").read_text() == first
+    (m,) = json.loads(first)
+    assert m["pId"] == "a" and m["qGroupId"] == "2.0"
+    pm = m["matches"]
+    assert len(pm["w"]) == 10 and len(pm["p"][0]) == 10 and len(pm["q"][1]) == 10
+    # q - p is the flow at p (no pre-scale, top ROI at the origin)
+    I0, I1 = pair
+    u, v = oracle_post(np.ascontiguousarray(I0[:30]), np.ascontiguousarray(I1[:30]),
+                       capi.make_params(nscales=3, warps=2), 0)
+    for k in range(10):
+        x, y = int(pm["p"][0][k]), int(pm["p"][1][k])
+        assert abs(pm["q"][0][k] - (x + float(u[y, x]))) < 1e-4
+        assert abs(pm["q"][1][k] - (y + float(v[y, x]))) < 1e-4
+
+
+def test_two_workers_match_one(tmp_path, built):
+    """Pairs sharded over two workers (here both on GPU 0) give byte-identical files."""
+    stack = synth.gen_stack(96, 64, 5, seed=77)
+    for z in range(5):
+        Image.fromarray(stack[z]).save(tmp_path / f"s{z}.png")
+    imgs = [{"p": str(tmp_path / f"s{z}.png"), "q": str(tmp_path / f"s{z+1}.png"),
+             "output_name": f"z{z}"} for z in range(4)]
+    outs = []
+    for tag, dev in (("one", [0]), ("two", [0, 0])):
+        d = tmp_path / tag
+        d.mkdir()
+        run_cli({"output_dir": str(d), "scale": 1, "output_type": "flow", "nscales": 3,
+                 "warps": 2, "devices": dev, "rois": {"custom": [0, 0, 96, 64]},
+                 "images": imgs}, tmp_path, name=f"{tag}.json")
+        outs.append({p.name: p.read_bytes() for p in sorted(d.glob("*.tiff"))})
+    assert len(outs[0]) == 8 and outs[0] == outs[1]

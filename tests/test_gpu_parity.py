@@ -94,3 +94,18 @@ def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
     ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
     np.testing.assert_array_equal(wi, wr)
     assert np.array_equal(u, ur) and np.array_equal(v, vr)
+
+
+GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
+
+
+@pytest.mark.parametrize("path", sorted(GOLDEN.glob("*.npz")), ids=lambda p: p.stem)
+def test_engine_reproduces_golden(engine, path):
+    import json
+    g = np.load(path, allow_pickle=False)
+    p = capi.make_params(**json.loads(str(g["params"])))
+    engine.set_params(p)
+    u, v, st, wi = engine.calc_host(g["I0"], g["I1"])
+    assert st["levels"] == int(g["levels"])
+    np.testing.assert_array_equal(wi, g["warp_iters"])
+    assert np.array_equal(u, g["u"]) and np.array_equal(v, g["v"])

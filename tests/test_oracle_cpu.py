@@ -1,0 +1,137 @@
+"""CPU tests of the oracle (CPU restatement of OpenCV 3.4.1 CUDA TV-L1, oracle/).
+
+PARITY UNPINNED: the reference ships no tests/fixtures and OpenCV is absent
+(SURVEY 8c).  The oracle is pinned here by known-answer tests and
+by the committed golden fixtures it generated (tests/golden/make_golden.py).
+"""
+import ctypes as C
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from optflow_amd import capi, synth
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+@pytest.fixture(scope="module")
+def oracle(built):
+    lib = capi.load_oracle()
+    lib.orc_pyramid_sizes.restype = C.c_int
+    lib.orc_pyramid_sizes.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double,
+                                      C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    return lib
+
+
+def pyramid(lib, w, h, n, step=0.8):
+    ws = (C.c_int * 32)()
+    hs = (C.c_int * 32)()
+    L = lib.orc_pyramid_sizes(w, h, n, step, ws, hs)
+    return [(ws[i], hs[i]) for i in range(L)]
+
+
+def test_pyramid_sizes_c2(oracle):
+    # the C2 pyramid, 62,405,817 px in total
+    lv = pyramid(oracle, 6144, 4096, 5)
+    assert lv == [(6144, 4096), (4915, 3277), (3932, 2622), (3146, 2098), (2517, 1678)]
+    assert sum(w * h for w, h in lv) == 62_405_817
+
+
+def test_pyramid_sizes_512_and_stop_rule(oracle):
+    lv = pyramid(oracle, 512, 512, 10)
+    assert [w for w, _ in lv] == [512, 410, 328, 262, 210, 168, 134, 107, 86, 69]
+    assert sum(w * h for w, h in lv) == 720_358
+    assert sum(w * h for w, h in pyramid(oracle, 512, 512, 5)) == 650_572
+    # a level with a side < 16 ends the pyramid (nscales_ = s) and is discarded
+    assert pyramid(oracle, 20, 20, 10) == [(20, 20), (16, 16)]
+    assert pyramid(oracle, 300, 19, 10) == [(300, 19)]
+    # production ROI strip (scale 0.5, 100-row strip of a 6144-wide slice): 9 levels
+    strip = pyramid(oracle, 3072, 100, 10)
+    assert len(strip) == 9 and sum(w * h for w, h in strip) == 837_872
+
+
+def test_identity_pair_is_exactly_zero(built):
+    I0, _ = synth.gen_pair(72, 50, seed=5)
+    u, v, st, wi = capi.oracle_calc(I0, I0, capi.make_params(nscales=4, warps=3))
+    assert np.all(u == 0) and np.all(v == 0)
+    assert np.all(wi == 2)      # n = 0 no check, n = 1 check -> error 0 -> stop
+
+
+def test_constant_images_zero_flow(built):
+    I0 = np.full((33, 47), 90, np.uint8)
+    I1 = np.full((33, 47), 130, np.uint8)
+    u, v, _, _ = capi.oracle_calc(I0, I1, capi.make_params(nscales=3, warps=2))
+    assert np.all(u == 0) and np.all(v == 0)
+
+
+@pytest.mark.parametrize("dx,dy", [(1.5, -0.75), (-2.0, 0.5), (0.25, 1.25)])
+def test_recovers_known_translation(built, dx, dy):
+    from scipy import ndimage
+    base = synth.base_texture(160, 128, seed=9)
+    ys, xs = np.mgrid[0:128, 0:160].astype(np.float32)
+    # I1(x + d) = I0(x)  =>  I1(x) = base(x - d)
+    I0 = np.clip(np.rint(base), 0, 255).astype(np.uint8)
+    I1 = np.clip(np.rint(ndimage.map_coordinates(base, [ys - dy, xs - dx], order=3,
+                                                 mode="nearest")), 0, 255).astype(np.uint8)
+    u, v, _, _ = capi.oracle_calc(I0, I1, capi.make_params(nscales=5, warps=5))
+    c = np.s_[16:-16, 16:-16]
+    assert abs(float(np.median(u[c])) - dx) < 0.05
+    assert abs(float(np.median(v[c])) - dy) < 0.05
+
+
+def test_fixed_work_mode_runs_exact_iteration_count(built):
+    I0, I1 = synth.gen_pair(64, 48, seed=2)
+    _, _, st, wi = capi.oracle_calc(I0, I1, capi.make_params(nscales=3, warps=2, epsilon=0.0,
+                                                             iterations=7))
+    assert np.all(wi == 7) and st["checks_total"] == 0
+
+
+def test_invalid_params_rejected(built):
+    lib = capi.load_oracle()
+    I0 = np.zeros((8, 8), np.uint8)
+    u = np.zeros((8, 8), np.float32)
+    p = capi.make_params(nscales=0)
+    rc = lib.orc_tvl1_calc(C.byref(p), capi._u8_ptr(I0), 8, capi._u8_ptr(I0), 8, 8, 8,
+                           capi._f32_ptr(u), capi._f32_ptr(u), 32, None)
+    assert rc == 1  # TVL1_EINVAL, like CV_Assert(nscales_ > 0)
+
+
+def test_thread_count_does_not_change_results(built):
+    I0, I1 = synth.gen_pair(96, 80, seed=12)
+    p = capi.make_params(nscales=4, warps=4)
+    a = capi.oracle_calc(I0, I1, p, threads=1)
+    b = capi.oracle_calc(I0, I1, p, threads=4)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert np.array_equal(a[3], b[3])
+
+
+@pytest.mark.parametrize("path", sorted(GOLDEN.glob("*.npz")), ids=lambda p: p.stem)
+def test_oracle_reproduces_golden(built, path):
+    g = np.load(path, allow_pickle=False)
+    params = capi.make_params(**json.loads(str(g["params"])))
+    u, v, st, wi = capi.oracle_calc(g["I0"], g["I1"], params)
+    assert st["levels"] == int(g["levels"])
+    np.testing.assert_array_equal(wi, g["warp_iters"])
+    assert np.array_equal(u, g["u"]) and np.array_equal(v, g["v"])
+
+
+def test_postprocess_semantics(built):
+    """solve_wrapper post-ops: map adds the pixel grid, mask zeroes where I1 <= 1."""
+    lib = capi.load_oracle()
+    lib.orc_postprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                    C.c_int, C.c_int, C.c_int]
+    H, W = 5, 7
+    u = np.full((H, W), 0.25, np.float32)
+    v = np.full((H, W), -0.5, np.float32)
+    I1 = np.full((H, W), 50, np.uint8)
+    I1[2, 3] = 1
+    I1[0, 0] = 0
+    lib.orc_postprocess(u.ctypes.data, v.ctypes.data, 4 * W, I1.ctypes.data, W, W, H, 1)
+    xs, ys = np.meshgrid(np.arange(W), np.arange(H))
+    exp_u = (0.25 + xs).astype(np.float32)
+    exp_v = (-0.5 + ys).astype(np.float32)
+    exp_u[I1 <= 1] = 0
+    exp_v[I1 <= 1] = 0
+    assert np.array_equal(u, exp_u) and np.array_equal(v, exp_v)
