@@ -173,8 +173,26 @@ bool ensure(DeviceCtx &dc, size_t img_bytes, size_t flow_bytes, bool &realloc, s
   return true;
 }
 
-// glibc rand() state is process-global, as in the reference (std::srand / rand).
+// The reference draws with glibc rand() after std::srand(time(0)) (or, with "debug",
+// from the unseeded default state = seed 1).  Other code in this process (the HIP
+// runtime) also consumes rand(), so use a PRIVATE generator with glibc's exact
+// rand() algorithm (random_r on a 128-byte TYPE_3 state, what rand()/srand() use).
 std::mutex g_rand_mutex;
+struct GlibcRand {
+  random_data rd{};
+  char state[128];
+  GlibcRand() { initstate_r(1, state, sizeof state, &rd); }
+  void seed(unsigned s) { srandom_r(s, &rd); }
+  int next() {
+    int32_t r;
+    random_r(&rd, &r);
+    return r;
+  }
+};
+GlibcRand &g_rand() {
+  static GlibcRand r;
+  return r;
+}
 
 // random_points (optflow.cpp:522-572) + the libstdc++ std::random_shuffle it uses.
 void random_points(const std::vector<float> &fx, const std::vector<float> &fy, int W, int H,
@@ -191,9 +209,9 @@ void random_points(const std::vector<float> &fx, const std::vector<float> &fy, i
   Value &pm = im["point_matches"];
   {
     std::lock_guard<std::mutex> lk(g_rand_mutex);
-    if (!debug) std::srand((unsigned)std::time(0));
+    if (!debug) g_rand().seed((unsigned)std::time(0));
     for (size_t i = 1; i < loc.size(); ++i) {  // std::random_shuffle (libstdc++)
-      const size_t j = (size_t)std::rand() % (i + 1);
+      const size_t j = (size_t)g_rand().next() % (i + 1);
       if (i != j) std::swap(loc[i], loc[j]);
     }
   }
