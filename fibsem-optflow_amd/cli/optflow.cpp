@@ -147,6 +147,8 @@ std::mutex g_io_mutex;
 
 bool ensure(DeviceCtx &dc, size_t img_bytes, size_t flow_bytes, bool &realloc, std::string &err) {
   realloc = false;
+  if ((img_bytes > dc.cap_img || flow_bytes > dc.cap_flow) && dc.stream)
+    (void)hipStreamSynchronize(dc.stream);  // buffers may still be in use by queued work
   if (img_bytes > dc.cap_img) {
     realloc = true;
     if (dc.d0) (void)hipFree(dc.d0);

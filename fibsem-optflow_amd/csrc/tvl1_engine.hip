@@ -56,15 +56,20 @@ struct tvl1_ctx {
   float4 *G = nullptr;
   float *U[2][3] = {};   // u1, u2, u3
   float *Pd[2][6] = {};  // p11, p12, p21, p22, p31, p32
-  float *C[3] = {};      // I1wx, I1wy, rho_c
+  float *C[2][3] = {};   // two sets of warp constants I1wx, I1wy, rho_c (speculation)
   uint8_t *in0 = nullptr, *in1 = nullptr;   // staging for tvl1_calc_host
   float *outu = nullptr, *outv = nullptr;
   double *partials = nullptr;
   int partials_cap = 0;
   double *red = nullptr;
   double *pinned = nullptr;  // host-pinned residual landing slot
+  hipEvent_t ev_check = nullptr;  // recorded after each residual copy
+  int speculate = 0;         // TVL1_SPECULATE=1 enables speculative enqueueing (measured slower)
   int iter_mode = 0;         // 0 = temporally blocked passes, 1 = one iteration per launch
-  int warp_mode = 0;         // 0 = LDS-staged gather (k_warp_lds), 1 = global gather (k_warp)
+  int warp_mode = 2;         // 2 = k_warp_lds (LDS-staged G window; fastest measured),
+                             // 0 = k_warp_img (gradient built in LDS from I1), 1 = k_warp (global)
+  int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
+  int warp_th = 16;          // k_warp_lds tile height (8, 16, 32)
   int tb_cfg = 0;            // k_iterate_tb shape: 0 = 64x32/512 thr, 1 = 64x32/256 thr, 2 = 64x64/1024 thr
 
   // optional per-kernel-class HIP-event timing (tvl1_set_profiling)
@@ -153,6 +158,10 @@ static int pyramid_sizes(int w, int h, int nscales, double step, int *ws, int *h
   return L;
 }
 
+// region height of k_iterate_tb for a tb_cfg (0: 64x32/512 threads 4 px each,
+// 1: 64x32/256 threads 2x4 px, 2: 64x64/1024 threads 4 px, 3: 64x32/1024 threads 2 px)
+static int tb_region_h(int cfg, int) { return cfg == 2 ? 64 : 32; }
+
 static int iterate_blocks(int W, int H) {
   const int segs = (W + kSegPx - 1) / kSegPx;
   const int strips = (H + kStripRows - 1) / kStripRows;
@@ -180,17 +189,19 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
   bytes += 4 * plane;                       // G (float4)
   bytes += 2 * 3 * plane;                   // U[2][3]
   bytes += 2 * 6 * plane;                   // Pd[2][6]
-  bytes += 3 * plane;                       // C
+  bytes += 2 * 3 * plane;                   // C[2]
   bytes += 2 * align_up(P0 * H, 256);       // in0, in1 (u8)
   bytes += 2 * plane;                       // outu, outv
-  const int tb_blocks = ((W + 55) / 56) * ((H + 23) / 24);   // RH 32 at 4 iterations
+  const int tb_blocks = ((W + 55) / 56) * ((H + 23) / 24);   // worst case: RH 32 at 4 iterations
   const int nblk = (iterate_blocks(W, H) > tb_blocks ? iterate_blocks(W, H) : tb_blocks) + 64;
   bytes += align_up((size_t)nblk * sizeof(double), 256) + 256;
   bytes += 4096;                            // alignment slack
 
   if (bytes > c->arena_bytes) {
     if (c->arena) {
-      (void)hipStreamSynchronize(c->own_stream);
+      // The old arena may still be in use by work on the caller's stream (tvl1_calc
+      // is asynchronous): drain the device before freeing it.
+      HIP_TRY(c, hipDeviceSynchronize());
       (void)hipFree(c->arena);
       c->arena = nullptr;
       c->arena_bytes = 0;
@@ -199,8 +210,11 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
     if (e != hipSuccess)
       return set_err(c, TVL1_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
     c->arena_bytes = bytes;
-    // Zero once: pitch padding then holds finite values forever.
-    HIP_TRY(c, hipMemset(c->arena, 0, bytes));
+    // Zero once so pitch padding starts finite.  NOT a plain hipMemset: that runs on
+    // the legacy null stream, which does not order against the ctx's non-blocking
+    // stream or the caller's stream, and could land after the solve's kernels.
+    HIP_TRY(c, hipMemsetAsync(c->arena, 0, bytes, c->own_stream));
+    HIP_TRY(c, hipStreamSynchronize(c->own_stream));
   }
   char *p = c->arena;
   auto take = [&](size_t n) {
@@ -219,7 +233,8 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
     for (int k = 0; k < 3; ++k) c->U[b][k] = (float *)take(plane);
   for (int b = 0; b < 2; ++b)
     for (int k = 0; k < 6; ++k) c->Pd[b][k] = (float *)take(plane);
-  for (int k = 0; k < 3; ++k) c->C[k] = (float *)take(plane);
+  for (int b = 0; b < 2; ++b)
+    for (int k = 0; k < 3; ++k) c->C[b][k] = (float *)take(plane);
   c->in0 = (uint8_t *)take(P0 * H);
   c->in1 = (uint8_t *)take(P0 * H);
   c->outu = (float *)take(plane);
@@ -231,6 +246,19 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
   c->geo_valid = true;
   return TVL1_OK;
 }
+
+// Diagnostics (TVL1_CHECK=1): after every launch, synchronise and report which
+// kernel at which level / warp / iteration failed.
+#define DIAG(ctx, st, what, lev, warp, it)                                                   \
+  do {                                                                                     \
+    if ((ctx)->check) {                                                                    \
+      hipError_t e_ = hipStreamSynchronize(st);                                            \
+      if (e_ == hipSuccess) e_ = hipGetLastError();                                        \
+      if (e_ != hipSuccess)                                                                \
+        return set_err((ctx), TVL1_EHIP, "%s failed at level %d warp %d n %d: %s", what,    \
+                       (int)(lev), (int)(warp), (int)(it), hipGetErrorString(e_));         \
+    }                                                                                      \
+  } while (0)
 
 static inline dim3 grid2(int w, int h, int z = 1) {
   return dim3((unsigned)((w + 63) / 64), (unsigned)((h + 3) / 4), (unsigned)z);
@@ -253,6 +281,23 @@ static double survey_bytes(const Geometry &g, int warps, const int64_t *iters) {
 
 // calcImpl + procOneScale on device inputs already in the arena
 // or caller memory.  Result left in caller's u, v.
+//
+// Host schedule.  procOneScale's inner loop
+//     for (n = 0; error > eps^2*W*H && n < iterations; ++n)
+//         calcError = eps > 0 && (n & 1) && prevError < eps^2*W*H
+// is known on the host for every iteration up to and including the next check,
+// so those iterations run as ONE temporally blocked pass (<= kTbMax iterations);
+// the residual of the check is then read exactly where OpenCV reads it.
+//
+// Speculation (default on, TVL1_SPECULATE=0 disables): right after a check pass,
+// before the host blocks on its residual, the work that follows if the warp has
+// converged is enqueued — the next warp's warpBackward (into the other constants
+// buffer), or at the end of a level the flow upsample + the next level's gradient
+// + its first warpBackward.  Converged (the common case): that work is simply used.
+// Not converged: it wrote only buffers the continuing warp does not read (the
+// spare constants buffer, the next ping-pong u set, the gradient of a level whose
+// gathers are done) and is redone at the next check.  Results are bit-identical
+// either way; the GPU just never idles while the host reads a residual.
 static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8_t *I1,
                          size_t pitch1, int W, int H, float *u, float *v, size_t fpitch,
                          tvl1_stats *stats, hipStream_t st) {
@@ -260,16 +305,16 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   const Geometry &g = c->geo;
   const int L = g.L;
   const bool gam = g.gamma;
-
+  const bool median = prm.median_filtering > 1;
   if (c->profiling) {
     c->ev_used = 0;
     c->marks.clear();
   }
+
+  // [A.1] convertTo + [A.2] pyramid, kernel step = float(1/scaleStep)
   size_t tk = prof_begin(c, st);
-  // [A.1] convertTo
   hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 2), kBlk2, 0, st, I0, pitch0, I1, pitch1,
                      c->I0s[0], c->I1s[0], W, H, g.ps[0]);
-  // [A.2] pyramid, kernel step = float(1/scaleStep)
   const float fdown = (float)(1.0 / prm.scale_step);
   for (int s = 1; s < L; ++s)
     hipLaunchKernelGGL(k_resize_down2, grid2(g.ws[s], g.hs[s], 2), kBlk2, 0, st, c->I0s[s - 1],
@@ -283,6 +328,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   HIP_TRY(c, hipGetLastError());
 
   int ui = 0, pi = 0;  // ping-pong indices of the u and p buffer sets
+  int cb = 0;          // constants buffer (I1wx, I1wy, rho) of the current warp
   {                    // u = 0 at the coarsest level (no initial flow)
     const int s = L - 1;
     const size_t n = (size_t)g.ps[s] * g.hs[s] * sizeof(float);
@@ -296,23 +342,79 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   const float theta_f = (float)prm.theta;
   const float gamma_f = (float)prm.gamma;
   const float upmul = (float)(1.0 / prm.scale_step);
+  const bool speculate = c->speculate && !median;
 
   int64_t level_iters[TVL1_MAX_LEVELS] = {};
-  int64_t checks = 0;
+  int64_t checks = 0, spec_miss = 0;
 
+  // ---- launch helpers
+  auto gradient = [&](int s) -> tvl1_status {  // interleaved G plane for warp modes 1, 2
+    if (c->warp_mode == 0) return TVL1_OK;     // k_warp_img derives it from I1 in LDS
+    const int lw = g.ws[s], lh = g.hs[s];
+    size_t t0 = prof_begin(c, st);
+    hipLaunchKernelGGL(k_gradient, grid2(lw, lh), kBlk2, 0, st, c->I1s[s], lw, lh, g.ps[s], c->G);
+    prof_end(c, st, t0, 2, (double)lw * lh * (4 + 16));
+    DIAG(c, st, "k_gradient", s, -1, -1);
+    return TVL1_OK;
+  };
+  auto gather = [&](int s, int uset, int cbuf, int wp) -> tvl1_status {  // K5 warpBackward
+    const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
+    size_t t0 = prof_begin(c, st);
+    if (c->warp_mode == 0) {
+      const int tx = (lw + kWarpTW - 1) / kWarpTW, ty = (lh + kWarpTH - 1) / kWarpTH;
+      hipLaunchKernelGGL(k_warp_img, dim3(tx * ty), dim3(256), 0, st, c->I0s[s], c->I1s[s],
+                         c->U[uset][0], c->U[uset][1], lw, lh, P, tx, c->C[cbuf][0],
+                         c->C[cbuf][1], c->C[cbuf][2]);
+    } else if (c->warp_mode == 1) {
+      hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[uset][0],
+                         c->U[uset][1], lw, lh, P, c->C[cbuf][0], c->C[cbuf][1], c->C[cbuf][2]);
+    } else {
+#define WARP_LDS(TH)                                                                            \
+  {                                                                                             \
+    const int tx = (lw + kWarpTW - 1) / kWarpTW, ty = (lh + TH - 1) / TH;                       \
+    hipLaunchKernelGGL(k_warp_lds<TH>, dim3(tx * ty), dim3(256), 0, st, c->I0s[s], c->G,        \
+                       c->U[uset][0], c->U[uset][1], lw, lh, P, tx, c->C[cbuf][0],              \
+                       c->C[cbuf][1], c->C[cbuf][2]);                                           \
+  }
+      if (c->warp_th == 8) WARP_LDS(8) else if (c->warp_th == 32) WARP_LDS(32) else WARP_LDS(16)
+#undef WARP_LDS
+    }
+    // algorithmic: 40 B/px per warp
+    prof_end(c, st, t0, 1, (double)lw * lh * 40.0,
+             (double)lw * lh * (c->warp_mode == 0 ? 28.0 : 40.0));
+    DIAG(c, st, "warp kernel", s, wp, -1);
+    return TVL1_OK;
+  };
+  auto upsample = [&](int s, int uset) -> tvl1_status {  // level s -> s-1 into U[uset^1]
+    const int lw = g.ws[s], lh = g.hs[s];
+    const int dw = g.ws[s - 1], dh = g.hs[s - 1];
+    const float fxu = (float)(1.0 / ((double)dw / lw));
+    const float fyu = (float)(1.0 / ((double)dh / lh));
+    size_t t0 = prof_begin(c, st);
+    hipLaunchKernelGGL(k_upsample, grid2(dw, dh, gam ? 3 : 2), kBlk2, 0, st, c->U[uset][0],
+                       c->U[uset][1], c->U[uset][2], lw, lh, g.ps[s], c->U[uset ^ 1][0],
+                       c->U[uset ^ 1][1], c->U[uset ^ 1][2], dw, dh, g.ps[s - 1], fxu, fyu, upmul);
+    prof_end(c, st, t0, 2, (double)lw * lh * 8.0 + (double)dw * dh * 8.0);
+    DIAG(c, st, "k_upsample", s, -1, -1);
+    return TVL1_OK;
+  };
+#define TRY(expr)                      \
+  do {                                 \
+    tvl1_status r_ = (expr);           \
+    if (r_ != TVL1_OK) return r_;      \
+  } while (0)
+
+  bool have_level = false;   // level s's gradient (+ u upsample) already enqueued speculatively
+  bool have_gather = false;  // the next warp's constants already enqueued speculatively
   for (int s = L - 1; s >= 0; --s) {
     const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
-    const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
     const double Nl = (double)lw * lh;
-    tk = prof_begin(c, st);
-    hipLaunchKernelGGL(k_gradient, grid2(lw, lh), kBlk2, 0, st, c->I1s[s], lw, lh, P, c->G);
-    prof_end(c, st, tk, 2, Nl * (4 + 16));
+    const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
+    if (!have_level) TRY(gradient(s));
+    have_level = false;
     bool p_zero = true;  // p = 0 at the start of every level (setTo(0) in procOneScale)
 
     IterArgs a{};
-    a.I1wx = c->C[0];
-    a.I1wy = c->C[1];
-    a.rho = c->C[2];
     a.W = lw;
     a.H = lh;
     a.P = P;
@@ -326,7 +428,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     const int nblk = iterate_blocks(lw, lh);
 
     for (int wp = 0; wp < prm.warps; ++wp) {
-      if (prm.median_filtering > 1) {
+      if (median) {
         hipLaunchKernelGGL(k_median, grid2(lw, lh, 2), kBlk2, 0, st, c->U[ui][0], c->U[ui][1],
                            lw, lh, P, prm.median_filtering, c->U[ui ^ 1][0], c->U[ui ^ 1][1]);
         if (gam) {
@@ -335,23 +437,11 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         }
         ui ^= 1;
       }
-      tk = prof_begin(c, st);
-      if (c->warp_mode == 1) {
-        hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[ui][0],
-                           c->U[ui][1], lw, lh, P, c->C[0], c->C[1], c->C[2]);
-      } else {
-        const int tx = (lw + kWarpTW - 1) / kWarpTW, ty = (lh + kWarpTH - 1) / kWarpTH;
-        hipLaunchKernelGGL(k_warp_lds, dim3(tx * ty), dim3(256), 0, st, c->I0s[s], c->G,
-                           c->U[ui][0], c->U[ui][1], lw, lh, P, tx, c->C[0], c->C[1], c->C[2]);
-      }
-      prof_end(c, st, tk, 1, Nl * 40.0);  // u1,u2,I0 + one 16-B tap neighbourhood + 3 outputs
-      // procOneScale's inner loop.  The stopping rule
-      //   for (n = 0; error > scaledEps && n < iterations; ++n)
-      //     calcError = eps > 0 && (n & 1) && prevError < scaledEps
-      // is known on the host for every iteration up to and including the next
-      // check, so those iterations run as ONE temporally blocked pass (<= kTbMax);
-      // the residual of the check iteration is then read exactly where OpenCV
-      // reads it (device -> host), and the schedule continues.
+      if (!have_gather) TRY(gather(s, ui, cb, wp));
+      have_gather = false;
+      a.I1wx = c->C[cb][0];
+      a.I1wy = c->C[cb][1];
+      a.rho = c->C[cb][2];
       double error = DBL_MAX;
       double prevError = 0.0;
       int n = 0;
@@ -379,50 +469,47 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         a.p_zero = p_zero ? 1 : 0;
         int blocks = nblk;
         tk = prof_begin(c, st);
+        double hbm;
+        const int nu = gam ? 3 : 2, np = gam ? 6 : 4;
+        const double ld_planes = 3 + nu + (p_zero ? 0 : np), st_planes = nu + np;
         if (c->iter_mode == 1) {
           if (gam)
             hipLaunchKernelGGL(k_iterate<true>, dim3(nblk), dim3(kBlock), 0, st, a);
           else
             hipLaunchKernelGGL(k_iterate<false>, dim3(nblk), dim3(kBlock), 0, st, a);
+          hbm = Nl * 4.0 * (ld_planes + st_planes) * k;
         } else {
           TBArgs t;
           t.it = a;
           t.niter = k;
           t.tiles_x = (lw + 55) / 56;
-          t.out_h = (c->tb_cfg == 2 ? 64 : 32) - 2 * k;
-          const int tiles_y = (lh + t.out_h - 1) / t.out_h;
-          blocks = t.tiles_x * tiles_y;
+          const int rh = tb_region_h(c->tb_cfg, k);
+          t.out_h = rh - 2 * k;
+          blocks = t.tiles_x * ((lh + t.out_h - 1) / t.out_h);
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
                            c->partials_cap);
+#define TB_LAUNCH(RH, NG, PX)                                                                  \
+  if (gam)                                                                                     \
+    hipLaunchKernelGGL((k_iterate_tb<true, RH, NG, PX>), dim3(blocks),                         \
+                       dim3((64 / PX) * RH / NG), 0, st, t);                                   \
+  else                                                                                         \
+    hipLaunchKernelGGL((k_iterate_tb<false, RH, NG, PX>), dim3(blocks),                        \
+                       dim3((64 / PX) * RH / NG), 0, st, t);
           switch (c->tb_cfg) {
-#define TB_LAUNCH(RH, NG)                                                                   \
-  if (gam)                                                                                  \
-    hipLaunchKernelGGL((k_iterate_tb<true, RH, NG>), dim3(blocks), dim3(16 * RH / NG), 0, st, t); \
-  else                                                                                      \
-    hipLaunchKernelGGL((k_iterate_tb<false, RH, NG>), dim3(blocks), dim3(16 * RH / NG), 0, st, t);
-            case 1: TB_LAUNCH(32, 2) break;
-            case 2: TB_LAUNCH(64, 1) break;
-            default: TB_LAUNCH(32, 1) break;
+            case 1: TB_LAUNCH(32, 2, 4) break;
+            case 2: TB_LAUNCH(64, 1, 4) break;
+            case 3: TB_LAUNCH(32, 1, 2) break;
+            default: TB_LAUNCH(32, 1, 4) break;
+          }
 #undef TB_LAUNCH
-          }
-        }
-        {
-          // algorithmic: 64 B/px per executed iteration;
           // compulsory for this tiling: every staged region cell loads I1wx, I1wy, rho,
-          // u (+p unless p == 0), every px stores u and p once per pass.
-          const int nu = gam ? 3 : 2, np = gam ? 6 : 4;
-          const double ld_planes = 3 + nu + (p_zero ? 0 : np), st_planes = nu + np;
-          double hbm;
-          if (c->iter_mode == 1) {
-            hbm = Nl * 4.0 * (ld_planes + st_planes);
-          } else {
-            const int rh = c->tb_cfg == 2 ? 64 : 32;
-            const double cells = (double)blocks * 64.0 * rh;
-            hbm = cells * 4.0 * ld_planes + Nl * 4.0 * st_planes;
-          }
-          prof_end(c, st, tk, 0, Nl * 64.0 * k, hbm);
+          // u (+p unless p == 0), every px stores u and p once per pass
+          hbm = (double)blocks * 64.0 * rh * 4.0 * ld_planes + Nl * 4.0 * st_planes;
         }
+        // algorithmic: 64 B/px per executed iteration
+        prof_end(c, st, tk, 0, Nl * 64.0 * k, hbm);
+        DIAG(c, st, "iteration pass", s, wp, n);
         p_zero = false;
         ui ^= 1;
         pi ^= 1;
@@ -430,10 +517,30 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         if (calc_end) {
           hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, blocks, c->red);
           HIP_TRY(c, hipMemcpyAsync(c->pinned, c->red, sizeof(double), hipMemcpyDeviceToHost, st));
-          HIP_TRY(c, hipStreamSynchronize(st));  // the cuda::sum -> host read of procOneScale
+          HIP_TRY(c, hipEventRecord(c->ev_check, st));
+          // enqueue what follows if this check ends the warp (see the comment above)
+          int spec = 0;  // 1 = next warp's gather, 2 = next level's upsample/gradient/gather
+          // only where a check nearly always ends the warp: the first check of a warp
+          // that is not the level's first (those run 2 iterations almost always)
+          if (speculate && n < prm.iterations && wp > 0 && n == k) {
+            if (wp + 1 < prm.warps) {
+              TRY(gather(s, ui, cb ^ 1, wp + 1));
+              spec = 1;
+            } else if (s > 0) {
+              TRY(upsample(s, ui));
+              TRY(gradient(s - 1));
+              TRY(gather(s - 1, ui ^ 1, cb ^ 1, 0));
+              spec = 2;
+            }
+          }
+          HIP_TRY(c, hipEventSynchronize(c->ev_check));  // the cuda::sum -> host read
           error = *c->pinned;
           prevError = error;
           ++checks;
+          const bool ends = !(error > scaledEps && n < prm.iterations);
+          if (spec && !ends) ++spec_miss;
+          if (spec == 1 && ends) have_gather = true;
+          if (spec == 2 && ends) have_level = have_gather = true;
         } else {
           error = DBL_MAX;
           prevError = prev_sim;
@@ -442,20 +549,14 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       level_iters[s] += n;
       if (stats && stats->warp_iterations && s * prm.warps + wp < stats->warp_iterations_capacity)
         stats->warp_iterations[s * prm.warps + wp] = n;
+      cb ^= 1;  // every warp gets the other constants buffer
     }
     HIP_TRY(c, hipGetLastError());
     if (s == 0) break;
-    // zoom the flow to the next finer level, then scale by 1/scaleStep
-    const int dw = g.ws[s - 1], dh = g.hs[s - 1];
-    const float fxu = (float)(1.0 / ((double)dw / lw));
-    const float fyu = (float)(1.0 / ((double)dh / lh));
-    tk = prof_begin(c, st);
-    hipLaunchKernelGGL(k_upsample, grid2(dw, dh, gam ? 3 : 2), kBlk2, 0, st, c->U[ui][0],
-                       c->U[ui][1], c->U[ui][2], lw, lh, P, c->U[ui ^ 1][0], c->U[ui ^ 1][1],
-                       c->U[ui ^ 1][2], dw, dh, g.ps[s - 1], fxu, fyu, upmul);
-    prof_end(c, st, tk, 2, Nl * 8.0 + (double)dw * dh * 8.0);
+    if (!have_level) TRY(upsample(s, ui));  // zoom the flow to level s-1, scale by 1/scaleStep
     ui ^= 1;
   }
+#undef TRY
   tk = prof_begin(c, st);
   hipLaunchKernelGGL(k_output, grid2(W, H), kBlk2, 0, st, c->U[ui][0], c->U[ui][1], W, H,
                      g.ps[0], u, v, fpitch);
@@ -495,6 +596,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     }
     stats->iterations_total = tot;
     stats->checks_total = checks;
+    stats->speculation_misses = (int32_t)spec_miss;
     stats->algorithmic_bytes = survey_bytes(g, prm.warps, level_iters);
   }
   return TVL1_OK;
@@ -548,10 +650,14 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   c->prm = *params;
   if (const char *m = getenv("TVL1_ITER_MODE")) c->iter_mode = atoi(m) == 1 ? 1 : 0;
   if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = atoi(m);
-  if (const char *m = getenv("TVL1_WARP_MODE")) c->warp_mode = atoi(m) == 1 ? 1 : 0;
+  if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
+  if (const char *m = getenv("TVL1_WARP_TH")) c->warp_th = atoi(m);
+  if (const char *m = getenv("TVL1_SPECULATE")) c->speculate = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_WARP_MODE")) c->warp_mode = atoi(m);
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void **)&c->pinned, sizeof(double) * 8, hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void **)&c->pinned, sizeof(double) * 8, hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_check, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return set_err(nullptr, TVL1_EHIP, "HIP initialisation failed on device %d", device);
   }
@@ -643,6 +749,7 @@ void tvl1_destroy(tvl1_ctx *c) {
   if (c->arena) (void)hipFree(c->arena);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->ev_check) (void)hipEventDestroy(c->ev_check);
   delete c;
 }
 

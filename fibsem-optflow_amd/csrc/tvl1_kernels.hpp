@@ -190,6 +190,14 @@ __global__ void k_warp(const float *__restrict__ I0, const float4 *__restrict__ 
 constexpr int kWarpTW = 64, kWarpTH = 16, kWarpHalo = 6;
 constexpr int kWarpWW = kWarpTW + 2 * kWarpHalo, kWarpWH = kWarpTH + 2 * kWarpHalo;
 
+// floor() of a tap coordinate as an int with no overflow: coordinates are clamped to
+// +-2^24 first (every float beyond that is an integer and every tap of it clamps to
+// the image border anyway), so fx - 1 .. fx + 2 never overflow.  NaN maps to 0.
+__device__ __forceinline__ int tap_floor(float w) {
+  const float c = fminf(fmaxf(w, -16777216.0f), 16777216.0f);
+  return (int)floorf(c == c ? c : 0.0f);
+}
+
 // Keys kernel pieces: |t| <= 1 and 1 < |t| < 2 (OpenCV `cubic`).
 __device__ __forceinline__ float cubic_in(float x) {
   x = fabsf(x);
@@ -242,6 +250,7 @@ __device__ __forceinline__ void warp_gather(const float4 *__restrict__ src, int 
   }
 }
 
+template <int TH>
 __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
                                                   const float4 *__restrict__ G,
                                                   const float *__restrict__ u1,
@@ -249,14 +258,15 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
                                                   int P, int tiles_x, float *__restrict__ I1wx,
                                                   float *__restrict__ I1wy,
                                                   float *__restrict__ rho) {
-  __shared__ float4 win[kWarpWH * kWarpWW];
+  constexpr int WH = TH + 2 * kWarpHalo;
+  __shared__ float4 win[WH * kWarpWW];
   int bx, by;
   tile_of_block(blockIdx.x, gridDim.x, tiles_x, gridDim.x / tiles_x, bx, by);
-  const int x0 = bx * kWarpTW, y0 = by * kWarpTH;
+  const int x0 = bx * kWarpTW, y0 = by * TH;
   const int ox = x0 - kWarpHalo, oy = y0 - kWarpHalo;   // window origin (unclamped coords)
   // Issue this thread's own loads (u1, u2, I0 of its 4 rows) before the window fill so
   // their latency overlaps it.
-  constexpr int R = kWarpTH / 4;
+  constexpr int R = TH / 4;
   const int x = x0 + (threadIdx.x & 63);
   const int xc = imin(x, W - 1);
   float u1v[R], u2v[R], i0v[R];
@@ -268,7 +278,7 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
     u2v[j] = u2[i];
     i0v[j] = I0[i];
   }
-  for (int i = threadIdx.x; i < kWarpWH * kWarpWW; i += 256) {
+  for (int i = threadIdx.x; i < WH * kWarpWW; i += 256) {
     const int wy = i / kWarpWW, wx = i - wy * kWarpWW;
     const int cx = imin(imax(ox + wx, 0), W - 1);
     const int cy = imin(imax(oy + wy, 0), H - 1);
@@ -283,14 +293,131 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
     const size_t i = (size_t)y * P + x;
     const float wx = (float)x + u1v[j];
     const float wy = (float)y + u2v[j];
-    const int fx = (int)floorf(wx);
-    const int fy = (int)floorf(wy);
+    const int fx = tap_floor(wx);
+    const int fy = tap_floor(wy);
+    float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
+    const bool inwin = fx - 1 >= ox && fx + 2 < ox + kWarpWW && fy - 1 >= oy && fy + 2 < oy + WH;
+    if (inwin)
+      warp_gather<true>(win, kWarpWW, ox, oy, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+    else
+      warp_gather<false>(G, P, 0, 0, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+    const float coeff = 1.0f / wsum;
+    const float I1wv = sum * coeff;
+    const float I1wxv = sumx * coeff;
+    const float I1wyv = sumy * coeff;
+    I1wx[i] = I1wxv;
+    I1wy[i] = I1wyv;
+    rho[i] = I1wv - I1wxv * u1v[j] - I1wyv * u2v[j] - i0v[j];
+  }
+}
+
+// warpBackward straight from the level image (no precomputed gradient plane): the
+// tile stages I1 over its window + 1 px (clamped coordinates) in LDS, builds the
+// (I1, I1x, I1y) window from it with centeredGradient's exact formula
+//   I1x = 0.5f * (I1[y][min(x+1,W-1)] - I1[y][max(x-1,0)])   (likewise I1y)
+// evaluated at the CLAMPED tap coordinate (texture clamp of the gradient images), and
+// gathers as k_warp_lds.  Every image coordinate that formula needs for a window cell
+// lies in [ox-1, ox+WW] x [oy-1, oy+WH], so the extended I1 window covers it.  HBM per
+// px: u1, u2, I0, I1 (16 B) + 12 B of outputs, instead of 16 B of gradient plane.
+constexpr int kWarpEW = kWarpWW + 2, kWarpEH = kWarpWH + 2;
+
+__device__ __forceinline__ float4 grad_cell(const float *__restrict__ ext, int ox, int oy, int W,
+                                            int H, int cx, int cy) {
+  const int rx = imin(imax(cx, 0), W - 1), ry = imin(imax(cy, 0), H - 1);
+  auto E = [&](int x, int y) { return ext[(y - (oy - 1)) * kWarpEW + (x - (ox - 1))]; };
+  const float c = E(rx, ry);
+  const float gx = 0.5f * (E(imin(rx + 1, W - 1), ry) - E(imax(rx - 1, 0), ry));
+  const float gy = 0.5f * (E(rx, imin(ry + 1, H - 1)) - E(rx, imax(ry - 1, 0)));
+  return make_float4(c, gx, gy, 0.0f);
+}
+
+// Global-memory gather for pixels whose taps leave the window: the same taps, with the
+// gradient of each (clamped) tap computed from I1 in global memory.
+__device__ __forceinline__ void warp_gather_img_global(const float *__restrict__ I1, int P, int W,
+                                                       int H, float wx, float wy, int fx, int fy,
+                                                       float &sum, float &sumx, float &sumy,
+                                                       float &wsum) {
+  float kx[4], ky[4];
+  kx[0] = cubic_out(wx - (float)(fx - 1));
+  kx[1] = cubic_in(wx - (float)fx);
+  kx[2] = cubic_in(wx - (float)(fx + 1));
+  kx[3] = cubic_out(wx - (float)(fx + 2));
+  ky[0] = cubic_out(wy - (float)(fy - 1));
+  ky[1] = cubic_in(wy - (float)fy);
+  ky[2] = cubic_in(wy - (float)(fy + 1));
+  ky[3] = cubic_out(wy - (float)(fy + 2));
+  for (int j = 0; j < 4; ++j) {
+    const int ry = imin(imax(fy - 1 + j, 0), H - 1);
+    const float *row = I1 + (size_t)ry * P;
+    const float *up = I1 + (size_t)imax(ry - 1, 0) * P;
+    const float *dn = I1 + (size_t)imin(ry + 1, H - 1) * P;
+    for (int i = 0; i < 4; ++i) {
+      const int rx = imin(imax(fx - 1 + i, 0), W - 1);
+      const float w = kx[i] * ky[j];
+      const float c = row[rx];
+      const float gx = 0.5f * (row[imin(rx + 1, W - 1)] - row[imax(rx - 1, 0)]);
+      const float gy = 0.5f * (dn[rx] - up[rx]);
+      sum = sum + w * c;
+      sumx = sumx + w * gx;
+      sumy = sumy + w * gy;
+      wsum = wsum + w;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_warp_img(const float *__restrict__ I0,
+                                                  const float *__restrict__ I1,
+                                                  const float *__restrict__ u1,
+                                                  const float *__restrict__ u2, int W, int H,
+                                                  int P, int tiles_x, float *__restrict__ I1wx,
+                                                  float *__restrict__ I1wy,
+                                                  float *__restrict__ rho) {
+  __shared__ float4 win[kWarpWH * kWarpWW];
+  __shared__ float ext[kWarpEH * kWarpEW];
+  int bx, by;
+  tile_of_block(blockIdx.x, gridDim.x, tiles_x, gridDim.x / tiles_x, bx, by);
+  const int x0 = bx * kWarpTW, y0 = by * kWarpTH;
+  const int ox = x0 - kWarpHalo, oy = y0 - kWarpHalo;   // window origin (unclamped coords)
+  constexpr int R = kWarpTH / 4;
+  const int x = x0 + (threadIdx.x & 63);
+  const int xc = imin(x, W - 1);
+  float u1v[R], u2v[R], i0v[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int y = imin(y0 + (threadIdx.x >> 6) + 4 * j, H - 1);
+    const size_t i = (size_t)y * P + xc;
+    u1v[j] = u1[i];
+    u2v[j] = u2[i];
+    i0v[j] = I0[i];
+  }
+  for (int i = threadIdx.x; i < kWarpEH * kWarpEW; i += 256) {
+    const int ey = i / kWarpEW, ex = i - ey * kWarpEW;
+    const int cx = imin(imax(ox - 1 + ex, 0), W - 1);
+    const int cy = imin(imax(oy - 1 + ey, 0), H - 1);
+    ext[i] = I1[(size_t)cy * P + cx];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kWarpWH * kWarpWW; i += 256) {
+    const int wy = i / kWarpWW, wx = i - wy * kWarpWW;
+    win[i] = grad_cell(ext, ox, oy, W, H, ox + wx, oy + wy);
+  }
+  __syncthreads();
+  if (x >= W) return;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int y = y0 + (threadIdx.x >> 6) + 4 * j;
+    if (y >= H) break;
+    const size_t i = (size_t)y * P + x;
+    const float wx = (float)x + u1v[j];
+    const float wy = (float)y + u2v[j];
+    const int fx = tap_floor(wx);
+    const int fy = tap_floor(wy);
     float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
     const bool inwin = fx - 1 >= ox && fx + 2 < ox + kWarpWW && fy - 1 >= oy && fy + 2 < oy + kWarpWH;
     if (inwin)
       warp_gather<true>(win, kWarpWW, ox, oy, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
     else
-      warp_gather<false>(G, P, 0, 0, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+      warp_gather_img_global(I1, P, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
     const float coeff = 1.0f / wsum;
     const float I1wv = sum * coeff;
     const float I1wxv = sumx * coeff;
@@ -315,38 +442,60 @@ struct IterArgs {
   int calc_err, p_zero;
 };
 
-template <bool G>
+template <bool G, int PX = 4>
 struct Row {
-  float wx[4], wy[4], rh[4], u1[4], u2[4], p11[4], p12[4], p21[4], p22[4];
-  float u3[4], p31[4], p32[4];  // used only when G (dead otherwise)
+  float wx[PX], wy[PX], rh[PX], u1[PX], u2[PX], p11[PX], p12[PX], p21[PX], p22[PX];
+  float u3[PX], p31[PX], p32[PX];  // used only when G (dead otherwise)
 };
 
-__device__ __forceinline__ void ld4(float (&d)[4], const float *__restrict__ base, size_t off) {
-  const float4 t = *reinterpret_cast<const float4 *>(base + off);
+// PX consecutive floats <-> one 8- or 16-byte vector access
+template <int N> struct VecT;
+template <> struct VecT<4> { using type = float4; };
+template <> struct VecT<2> { using type = float2; };
+
+__device__ __forceinline__ void unpack(float (&d)[4], const float4 &t) {
   d[0] = t.x; d[1] = t.y; d[2] = t.z; d[3] = t.w;
 }
-__device__ __forceinline__ void st4(float *__restrict__ base, size_t off, const float (&s)[4]) {
-  *reinterpret_cast<float4 *>(base + off) = make_float4(s[0], s[1], s[2], s[3]);
+__device__ __forceinline__ void unpack(float (&d)[2], const float2 &t) {
+  d[0] = t.x; d[1] = t.y;
 }
-__device__ __forceinline__ void zero4(float (&d)[4]) { d[0] = d[1] = d[2] = d[3] = 0.0f; }
+__device__ __forceinline__ float4 pack(const float (&s)[4]) { return make_float4(s[0], s[1], s[2], s[3]); }
+__device__ __forceinline__ float2 pack(const float (&s)[2]) { return make_float2(s[0], s[1]); }
 
-template <bool G>
-__device__ __forceinline__ void load_row(Row<G> &r, const IterArgs &a, size_t off) {
-  ld4(r.wx, a.I1wx, off);
-  ld4(r.wy, a.I1wy, off);
-  ld4(r.rh, a.rho, off);
-  ld4(r.u1, a.u1s, off);
-  ld4(r.u2, a.u2s, off);
-  if (G) ld4(r.u3, a.u3s, off);
+template <int N>
+__device__ __forceinline__ void ldv(float (&d)[N], const float *__restrict__ base, size_t off) {
+  unpack(d, *reinterpret_cast<const typename VecT<N>::type *>(base + off));
+}
+template <int N>
+__device__ __forceinline__ void stv(float *__restrict__ base, size_t off, const float (&s)[N]) {
+  *reinterpret_cast<typename VecT<N>::type *>(base + off) = pack(s);
+}
+template <int N>
+__device__ __forceinline__ void zerov(float (&d)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i] = 0.0f;
+}
+__device__ __forceinline__ void ld4(float (&d)[4], const float *__restrict__ base, size_t off) { ldv<4>(d, base, off); }
+__device__ __forceinline__ void st4(float *__restrict__ base, size_t off, const float (&s)[4]) { stv<4>(base, off, s); }
+__device__ __forceinline__ void zero4(float (&d)[4]) { zerov<4>(d); }
+
+template <bool G, int PX = 4>
+__device__ __forceinline__ void load_row(Row<G, PX> &r, const IterArgs &a, size_t off) {
+  ldv<PX>(r.wx, a.I1wx, off);
+  ldv<PX>(r.wy, a.I1wy, off);
+  ldv<PX>(r.rh, a.rho, off);
+  ldv<PX>(r.u1, a.u1s, off);
+  ldv<PX>(r.u2, a.u2s, off);
+  if (G) ldv<PX>(r.u3, a.u3s, off);
   if (a.p_zero) {
-    zero4(r.p11); zero4(r.p12); zero4(r.p21); zero4(r.p22);
-    if (G) { zero4(r.p31); zero4(r.p32); }
+    zerov<PX>(r.p11); zerov<PX>(r.p12); zerov<PX>(r.p21); zerov<PX>(r.p22);
+    if (G) { zerov<PX>(r.p31); zerov<PX>(r.p32); }
   } else {
-    ld4(r.p11, a.p11s, off);
-    ld4(r.p12, a.p12s, off);
-    ld4(r.p21, a.p21s, off);
-    ld4(r.p22, a.p22s, off);
-    if (G) { ld4(r.p31, a.p31s, off); ld4(r.p32, a.p32s, off); }
+    ldv<PX>(r.p11, a.p11s, off);
+    ldv<PX>(r.p12, a.p12s, off);
+    ldv<PX>(r.p21, a.p21s, off);
+    ldv<PX>(r.p22, a.p22s, off);
+    if (G) { ldv<PX>(r.p31, a.p31s, off); ldv<PX>(r.p32, a.p32s, off); }
   }
 }
 
@@ -364,24 +513,24 @@ __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float
   return y > 0 ? yhi : ylo;
 }
 
-// estimateU for the 4 px of this lane on row y.  up* = p12/p22/p32 of row y-1.
-template <bool G>
-__device__ __forceinline__ void estimate_u(const Row<G> &r, const float (&up12)[4],
-                                           const float (&up22)[4], const float (&up32)[4],
-                                           int X0, int y, const IterArgs &a, float (&n1)[4],
-                                           float (&n2)[4], float (&n3)[4]) {
-  float l11[4], l21[4], l31[4];
-  l11[0] = __shfl_up(r.p11[3], 1);
-  l21[0] = __shfl_up(r.p21[3], 1);
-  if (G) l31[0] = __shfl_up(r.p31[3], 1);
+// estimateU for the PX px of this lane on row y.  up* = p12/p22/p32 of row y-1.
+template <bool G, int PX = 4>
+__device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up12)[PX],
+                                           const float (&up22)[PX], const float (&up32)[PX],
+                                           int X0, int y, const IterArgs &a, float (&n1)[PX],
+                                           float (&n2)[PX], float (&n3)[PX]) {
+  float l11[PX], l21[PX], l31[PX];
+  l11[0] = __shfl_up(r.p11[PX - 1], 1);
+  l21[0] = __shfl_up(r.p21[PX - 1], 1);
+  if (G) l31[0] = __shfl_up(r.p31[PX - 1], 1);
 #pragma unroll
-  for (int k = 1; k < 4; ++k) {
+  for (int k = 1; k < PX; ++k) {
     l11[k] = r.p11[k - 1];
     l21[k] = r.p21[k - 1];
     if (G) l31[k] = r.p31[k - 1];
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < PX; ++k) {
     const int x = X0 + k;
     const float I1wxv = r.wx[k];
     const float I1wyv = r.wy[k];
@@ -424,16 +573,17 @@ __device__ __forceinline__ void estimate_u(const Row<G> &r, const float (&up12)[
 __device__ __forceinline__ float hypot_f(float a, float b) { return sqrtf(a * a + b * b); }
 
 // One projection component: p' = (p + taut * du) / ng, du from u at (x+1) and (y+1).
-__device__ __forceinline__ void dual_component(const float (&uc)[4], const float (&un)[4],
+template <int PX>
+__device__ __forceinline__ void dual_component(const float (&uc)[PX], const float (&un)[PX],
                                                bool has_down, int X0, int W, float taut,
-                                               const float (&pa)[4], const float (&pb)[4],
-                                               float (&oa)[4], float (&ob)[4]) {
-  float ur[4];
-  ur[3] = __shfl_down(uc[0], 1);
+                                               const float (&pa)[PX], const float (&pb)[PX],
+                                               float (&oa)[PX], float (&ob)[PX]) {
+  float ur[PX];
+  ur[PX - 1] = __shfl_down(uc[0], 1);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) ur[k] = uc[k + 1];
+  for (int k = 0; k < PX - 1; ++k) ur[k] = uc[k + 1];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < PX; ++k) {
     const int x = X0 + k;
     const float right = (x + 1 < W) ? ur[k] : uc[k];
     const float down = has_down ? un[k] : uc[k];
@@ -538,8 +688,8 @@ __global__ __launch_bounds__(kBlock) void k_iterate(IterArgs a) {
 // ---------------------------------------------------------------- K6+K8 temporally blocked
 // k_iterate_tb: runs `niter` (1..4) consecutive primal-dual iterations in ONE HBM pass.
 //
-// A workgroup owns a region of 64 x RH px (16 float4 columns x RH rows; every thread
-// owns NG float4 groups, rows rr, rr + RH/NG, ...).  It loads u, p and the warp
+// A workgroup owns a region of 64 x RH px (64/PX lanes per row, PX = 4 or 2 px per
+// lane; every thread owns NG groups, rows rr, rr + RH/NG, ...).  It loads u, p and the warp
 // constants once, iterates in registers, and stores only the interior that is still
 // exact after niter iterations: each iteration invalidates one px at every internal
 // region edge (u needs p at x-1, y-1; p needs u at x+1, y+1), so the region keeps a
@@ -556,43 +706,41 @@ struct TBArgs {
   int out_h;        // output rows per region = RH - 2*niter
 };
 
-template <bool G, int RH, int NG>
-__global__ __launch_bounds__(16 * RH / NG) void k_iterate_tb(TBArgs t) {
-  constexpr int NT = 16 * RH / NG;   // threads; each owns NG float4 groups
+// Pass body of the blocked kernel: stage the vertically read planes, run the pass's
+// iterations on register-resident state, store the exact interior and the residual
+// partial of the last iteration.  lds = NPL planes of RH x LPR vectors of PX floats.
+template <bool G, int RH, int NG, int PX>
+__device__ __forceinline__ void tb_iterate_store(const TBArgs &t,
+                                                 typename VecT<PX>::type *__restrict__ lds,
+                                                 Row<G, PX> (&r)[NG], const int (&Y)[NG], int X,
+                                                 int c4, int rr) {
+  constexpr int LPR = 64 / PX;                   // lanes per region row
+  constexpr int NT = LPR * RH / NG;
   constexpr int HALF = RH / NG;
-  constexpr int NPL = G ? 6 : 4;                 // LDS planes
-  __shared__ float4 lds[NPL][RH][16];
+  constexpr int PL = RH * LPR;                   // vectors per LDS plane
+  constexpr int HALO = 4 / PX;                   // lanes of the 4-px x halo
+  using V = typename VecT<PX>::type;
   const IterArgs &a = t.it;
-  const int tid = threadIdx.x;
-  const int c4 = tid & 15;
-  const int rr = tid >> 4;
-  int bx, by;
-  tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
   const int K = t.niter;
-  const int xr0 = bx * 56 - 4;                   // region origin (16-B aligned)
-  const int yr0 = by * t.out_h - K;
-  const int X = xr0 + 4 * c4;                    // first image column of this thread
-  const int xa = imin(imax(X, 0), a.P - 4);
-
-  Row<G> r[NG];
-  int Y[NG];
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    Y[g] = yr0 + rr + g * HALF;
-    const int ya = imin(imax(Y[g], 0), a.H - 1);
-    load_row<G>(r[g], a, (size_t)ya * a.P + xa);
-  }
-  // stage the vertically read planes of the initial state
+  auto L = [&](int plane, int row) -> V & { return lds[plane * PL + row * LPR + c4]; };
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int row = rr + g * HALF;
-    lds[0][row][c4] = make_float4(r[g].p12[0], r[g].p12[1], r[g].p12[2], r[g].p12[3]);
-    lds[1][row][c4] = make_float4(r[g].p22[0], r[g].p22[1], r[g].p22[2], r[g].p22[3]);
-    if (G) lds[4][row][c4] = make_float4(r[g].p32[0], r[g].p32[1], r[g].p32[2], r[g].p32[3]);
+    L(0, row) = pack(r[g].p12);
+    L(1, row) = pack(r[g].p22);
+    if (G) L(4, row) = pack(r[g].p32);
   }
   __syncthreads();
 
-  float e1[NG][4], e2[NG][4];   // u before the last iteration (residual)
+  // this thread's cells that the pass stores (region interior, inside the image)
+  bool out_ok[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int row = rr + g * HALF;
+    out_ok[g] = c4 >= HALO && c4 < LPR - HALO && row >= K && row < RH - K && Y[g] >= 0 && Y[g] < a.H &&
+                X < a.W;
+  }
+  double acc = 0.0;   // residual of the last iteration over the stored cells
   for (int it = 0; it < K; ++it) {
     const bool last = it == K - 1;
     // ---- estimateU, one group at a time (keeps the live register set small)
@@ -600,55 +748,52 @@ __global__ __launch_bounds__(16 * RH / NG) void k_iterate_tb(TBArgs t) {
     for (int g = 0; g < NG; ++g) {
       const int row = rr + g * HALF;
       const int rowu = row > 0 ? row - 1 : 0;
-      float up12[4], up22[4], up32[4];
-      const float4 a12 = lds[0][rowu][c4];
-      const float4 a22 = lds[1][rowu][c4];
-      up12[0] = a12.x; up12[1] = a12.y; up12[2] = a12.z; up12[3] = a12.w;
-      up22[0] = a22.x; up22[1] = a22.y; up22[2] = a22.z; up22[3] = a22.w;
-      if (G) {
-        const float4 a32 = lds[4][rowu][c4];
-        up32[0] = a32.x; up32[1] = a32.y; up32[2] = a32.z; up32[3] = a32.w;
-      } else {
-        zero4(up32);
-      }
-      float n1[4], n2[4], n3[4];
-      estimate_u<G>(r[g], up12, up22, up32, X, Y[g], a, n1, n2, n3);
-      if (last) {
+      float up12[PX], up22[PX], up32[PX];
+      unpack(up12, L(0, rowu));
+      unpack(up22, L(1, rowu));
+      if (G) unpack(up32, L(4, rowu));
+      else zerov<PX>(up32);
+      float n1[PX], n2[PX], n3[PX];
+      estimate_u<G, PX>(r[g], up12, up22, up32, X, Y[g], a, n1, n2, n3);
+      if (last && a.calc_err && out_ok[g]) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { e1[g][k] = r[g].u1[k]; e2[g][k] = r[g].u2[k]; }
+        for (int k = 0; k < PX; ++k) {
+          if (X + k < a.W) {
+            const float f1 = (r[g].u1[k] - n1[k]) * (r[g].u1[k] - n1[k]);
+            const float f2 = (r[g].u2[k] - n2[k]) * (r[g].u2[k] - n2[k]);
+            acc += (double)(f1 + f2);
+          }
+        }
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < PX; ++k) {
         r[g].u1[k] = n1[k];
         r[g].u2[k] = n2[k];
         if (G) r[g].u3[k] = n3[k];
       }
-      lds[2][row][c4] = make_float4(n1[0], n1[1], n1[2], n1[3]);
-      lds[3][row][c4] = make_float4(n2[0], n2[1], n2[2], n2[3]);
-      if (G) lds[5][row][c4] = make_float4(n3[0], n3[1], n3[2], n3[3]);
+      L(2, row) = pack(n1);
+      L(3, row) = pack(n2);
+      if (G) L(5, row) = pack(n3);
     }
     __syncthreads();
-    // ---- estimateDualVariables on both groups
+    // ---- estimateDualVariables
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int row = rr + g * HALF;
       const int rowd = row < RH - 1 ? row + 1 : RH - 1;
       const bool has_down = Y[g] + 1 < a.H;
-      float d1[4], d2[4], d3[4];
-      const float4 b1 = lds[2][rowd][c4];
-      const float4 b2 = lds[3][rowd][c4];
-      d1[0] = b1.x; d1[1] = b1.y; d1[2] = b1.z; d1[3] = b1.w;
-      d2[0] = b2.x; d2[1] = b2.y; d2[2] = b2.z; d2[3] = b2.w;
-      float q11[4], q12[4], q21[4], q22[4], q31[4], q32[4];
+      float d1[PX], d2[PX], d3[PX];
+      unpack(d1, L(2, rowd));
+      unpack(d2, L(3, rowd));
+      float q11[PX], q12[PX], q21[PX], q22[PX], q31[PX], q32[PX];
       dual_component(r[g].u1, d1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12);
       dual_component(r[g].u2, d2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22);
       if (G) {
-        const float4 b3 = lds[5][rowd][c4];
-        d3[0] = b3.x; d3[1] = b3.y; d3[2] = b3.z; d3[3] = b3.w;
+        unpack(d3, L(5, rowd));
         dual_component(r[g].u3, d3, has_down, X, a.W, a.taut, r[g].p31, r[g].p32, q31, q32);
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < PX; ++k) {
         r[g].p11[k] = q11[k]; r[g].p12[k] = q12[k];
         r[g].p21[k] = q21[k]; r[g].p22[k] = q22[k];
         if (G) { r[g].p31[k] = q31[k]; r[g].p32[k] = q32[k]; }
@@ -661,43 +806,29 @@ __global__ __launch_bounds__(16 * RH / NG) void k_iterate_tb(TBArgs t) {
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
         const int row = rr + g * HALF;
-        lds[0][row][c4] = make_float4(r[g].p12[0], r[g].p12[1], r[g].p12[2], r[g].p12[3]);
-        lds[1][row][c4] = make_float4(r[g].p22[0], r[g].p22[1], r[g].p22[2], r[g].p22[3]);
-        if (G) lds[4][row][c4] = make_float4(r[g].p32[0], r[g].p32[1], r[g].p32[2], r[g].p32[3]);
+        L(0, row) = pack(r[g].p12);
+        L(1, row) = pack(r[g].p22);
+        if (G) L(4, row) = pack(r[g].p32);
       }
       __syncthreads();
     }
   }
 
   // ---- store the exact interior: region cols 4..59, rows K..RH-K-1, inside the image
-  double acc = 0.0;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    const int row = rr + g * HALF;
-    const bool ok = c4 >= 1 && c4 <= 14 && row >= K && row < RH - K && Y[g] >= 0 &&
-                    Y[g] < a.H && X < a.W;
-    if (ok) {
+    if (out_ok[g]) {
       const size_t off = (size_t)Y[g] * a.P + X;
-      st4(a.u1d, off, r[g].u1);
-      st4(a.u2d, off, r[g].u2);
-      st4(a.p11d, off, r[g].p11);
-      st4(a.p12d, off, r[g].p12);
-      st4(a.p21d, off, r[g].p21);
-      st4(a.p22d, off, r[g].p22);
+      stv<PX>(a.u1d, off, r[g].u1);
+      stv<PX>(a.u2d, off, r[g].u2);
+      stv<PX>(a.p11d, off, r[g].p11);
+      stv<PX>(a.p12d, off, r[g].p12);
+      stv<PX>(a.p21d, off, r[g].p21);
+      stv<PX>(a.p22d, off, r[g].p22);
       if (G) {
-        st4(a.u3d, off, r[g].u3);
-        st4(a.p31d, off, r[g].p31);
-        st4(a.p32d, off, r[g].p32);
-      }
-      if (a.calc_err) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (X + k < a.W) {
-            const float f1 = (e1[g][k] - r[g].u1[k]) * (e1[g][k] - r[g].u1[k]);
-            const float f2 = (e2[g][k] - r[g].u2[k]) * (e2[g][k] - r[g].u2[k]);
-            acc += (double)(f1 + f2);
-          }
-        }
+        stv<PX>(a.u3d, off, r[g].u3);
+        stv<PX>(a.p31d, off, r[g].p31);
+        stv<PX>(a.p32d, off, r[g].p32);
       }
     }
   }
@@ -705,14 +836,42 @@ __global__ __launch_bounds__(16 * RH / NG) void k_iterate_tb(TBArgs t) {
     __shared__ double red[NT / kWave];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-    if ((tid & 63) == 0) red[tid >> 6] = acc;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (tid == 0) {
-      double s = 0.0;
-      for (int i = 0; i < NT / kWave; ++i) s += red[i];
-      a.partials[blockIdx.x] = s;
+    if (threadIdx.x == 0) {
+      double sum = 0.0;
+      for (int i = 0; i < NT / kWave; ++i) sum += red[i];
+      a.partials[blockIdx.x] = sum;
     }
   }
+}
+
+template <bool G, int RH, int NG, int PX = 4>
+__global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterate_tb(TBArgs t) {
+  constexpr int LPR = 64 / PX;
+  constexpr int HALF = RH / NG;
+  constexpr int NPL = G ? 6 : 4;                 // LDS planes
+  __shared__ typename VecT<PX>::type lds[NPL * RH * LPR];
+  const IterArgs &a = t.it;
+  const int tid = threadIdx.x;
+  const int c4 = tid % LPR;
+  const int rr = tid / LPR;
+  int bx, by;
+  tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
+  const int K = t.niter;
+  const int xr0 = bx * 56 - 4;                   // region origin (16-B aligned)
+  const int yr0 = by * t.out_h - K;
+  const int X = xr0 + PX * c4;                   // first image column of this thread
+  const int xa = imin(imax(X, 0), a.P - PX);
+  Row<G, PX> r[NG];
+  int Y[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    Y[g] = yr0 + rr + g * HALF;
+    const int ya = imin(imax(Y[g], 0), a.H - 1);
+    load_row<G, PX>(r[g], a, (size_t)ya * a.P + xa);
+  }
+  tb_iterate_store<G, RH, NG, PX>(t, lds, r, Y, X, c4, rr);
 }
 
 // K7: fixed-order sum of the per-block partials (one block).

@@ -50,7 +50,7 @@ class TVL1Stats(C.Structure):
         ("algorithmic_bytes", C.c_double),
         ("warp_iterations", C.POINTER(C.c_int32)),
         ("warp_iterations_capacity", C.c_int32),
-        ("reserved", C.c_int32),
+        ("speculation_misses", C.c_int32),
         ("kernel_ms", C.c_double * 4),
         ("kernel_launches", C.c_int64 * 4),
         ("kernel_bytes", C.c_double * 4),
@@ -93,6 +93,7 @@ def stats_dict(st: TVL1Stats, warps: int | None = None) -> dict:
         "level_iterations": [int(st.level_iterations[i]) for i in range(L)],
         "iterations_total": int(st.iterations_total),
         "checks_total": int(st.checks_total),
+        "speculation_misses": int(st.speculation_misses),
         "algorithmic_bytes": float(st.algorithmic_bytes),
         "kernel_ms": [float(st.kernel_ms[i]) for i in range(4)],
         "kernel_launches": [int(st.kernel_launches[i]) for i in range(4)],

@@ -67,11 +67,13 @@ def test_constant_images_give_zero_flow(engine):
     assert np.all(u == 0) and np.all(v == 0)
 
 
-# Every iteration-kernel configuration must give the same bits (selected by env at
+# Every kernel / schedule configuration must give the same bits (selected by env at
 # tvl1_create): TVL1_ITER_MODE=1 -> one iteration per launch (rolling-strip kernel),
-# TVL1_TB_CFG = 0/1/2 -> temporally blocked regions 64x32/512thr, 64x32/256thr, 64x64/1024thr.
+# TVL1_TB_CFG = 0/1/2 -> temporally blocked regions 64x32/512thr, 64x32/256thr,
+# 64x64/1024thr; TVL1_WARP_MODE=1 -> global-memory gather; TVL1_SPECULATE=0 -> no
+# speculative enqueueing at check iterations.
 MODES = [("TVL1_ITER_MODE", "1"), ("TVL1_TB_CFG", "0"), ("TVL1_TB_CFG", "1"),
-         ("TVL1_TB_CFG", "2"), ("TVL1_WARP_MODE", "1")]
+         ("TVL1_TB_CFG", "2"), ("TVL1_TB_CFG", "3"), ("TVL1_WARP_TH", "8"), ("TVL1_WARP_TH", "32"), ("TVL1_WARP_MODE", "1"), ("TVL1_WARP_MODE", "0"), ("TVL1_SPECULATE", "1")]
 
 
 @pytest.mark.parametrize("env", MODES, ids=[f"{k}={v}" for k, v in MODES])
@@ -79,12 +81,14 @@ MODES = [("TVL1_ITER_MODE", "1"), ("TVL1_TB_CFG", "0"), ("TVL1_TB_CFG", "1"),
     (250, 131, 21, dict(nscales=5, warps=5)),
     (97, 201, 22, dict(nscales=4, warps=3, gamma=0.1)),
     (400, 300, 23, dict(nscales=3, warps=4, epsilon=0.0, iterations=9)),
-    (300, 200, 24, dict(nscales=1, warps=2)),   # level 0 only: large flow leaves LDS windows
+    (300, 200, 24, dict(nscales=1, warps=2)),
 ])
 def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
     monkeypatch.delenv("TVL1_ITER_MODE", raising=False)
     monkeypatch.delenv("TVL1_TB_CFG", raising=False)
     monkeypatch.delenv("TVL1_WARP_MODE", raising=False)
+    monkeypatch.delenv("TVL1_SPECULATE", raising=False)
+    monkeypatch.delenv("TVL1_WARP_TH", raising=False)
     monkeypatch.setenv(*env)
     p = capi.make_params(**kw)
     eng = capi.Engine(p)
@@ -109,3 +113,21 @@ def test_engine_reproduces_golden(engine, path):
     assert st["levels"] == int(g["levels"])
     np.testing.assert_array_equal(wi, g["warp_iters"])
     assert np.array_equal(u, g["u"]) and np.array_equal(v, g["v"])
+
+
+def test_large_flow_uses_global_gather_fallback(engine):
+    """A ~7 px shift puts taps outside the warp kernel's LDS window (margin 4 px):
+    the global-memory fallback must give the same bits."""
+    from scipy import ndimage
+    base = synth.base_texture(192, 160, seed=31)
+    ys, xs = np.mgrid[0:160, 0:192].astype(np.float32)
+    I0 = np.clip(np.rint(base), 0, 255).astype(np.uint8)
+    I1 = np.clip(np.rint(ndimage.map_coordinates(base, [ys + 6.75, xs - 7.5], order=3,
+                                                 mode="nearest")), 0, 255).astype(np.uint8)
+    p = capi.make_params(nscales=4, warps=6)
+    engine.set_params(p)
+    u, v, st, wi = engine.calc_host(I0, I1)
+    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    assert float(np.abs(ur).max()) > 5.0   # the case really leaves the window
+    np.testing.assert_array_equal(wi, wr)
+    assert np.array_equal(u, ur) and np.array_equal(v, vr)
