@@ -35,6 +35,20 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "fibsem-optflow_amd"))
 
 HBM_PEAK_GBS = 8000.0
+
+
+def _traffic():
+    """HBM bytes per k_iterate_tb launch measured with rocprofv3 PMC counters
+    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile.sh +
+    tools/pmc_summary.py), committed under profiles/.  None if not measured."""
+    p = ROOT / "profiles" / "traffic.json"
+    try:
+        return json.loads(p.read_text())["k_iterate_tb_hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+TRAFFIC = _traffic()
 METRIC = "slice-pairs/sec (6k×4k, 5 scales, 30 warps) at 1/2/4/8 GPUs; % HBM roofline"
 
 
@@ -51,7 +65,7 @@ def parse():
     ap.add_argument("--epsilon", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="3072x2048")
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="slice pairs solved concurrently per GPU (one ctx + stream + host "
                          "thread each); a step = one batch of this many pairs")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -117,7 +131,8 @@ def main():
         I0h, I1h = synth.gen_pair(W, H, seed=0x5EED, z=1 + rank * F + j)
         eng = capi.Engine(params, device=local_rank)
         eng.set_profiling(not args.no_kernel_timing)
-        st = torch.cuda.Stream(dev) if F > 1 else torch.cuda.current_stream(dev)
+        # F == 1: torch's current stream; F > 1: each ctx on its own non-blocking stream
+        st = eng.stream if F > 1 else torch.cuda.current_stream(dev).cuda_stream
         slots.append(dict(I0h=I0h, I1h=I1h, eng=eng, stream=st,
                           I0=torch.from_numpy(I0h).to(dev), I1=torch.from_numpy(I1h).to(dev),
                           u=torch.empty((H, W), dtype=torch.float32, device=dev),
@@ -127,7 +142,7 @@ def main():
     def solve(sl):
         return sl["eng"].calc_device(sl["I0"].data_ptr(), W, sl["I1"].data_ptr(), W, W, H,
                                      sl["u"].data_ptr(), sl["v"].data_ptr(), 4 * W,
-                                     stream=sl["stream"].cuda_stream)
+                                     stream=sl["stream"])
 
     pool = None
     if F > 1:
@@ -159,6 +174,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     I0h, I1h = slots[0]["I0h"], slots[0]["I1h"]
+    # one extra solve alone on the GPU (not timed): clean per-kernel durations, no
+    # interleaving with the other in-flight pair
+    t_iso = time.perf_counter()
+    iso = solve(slots[0])
+    torch.cuda.synchronize(dev)
+    single_pair_ms = 1e3 * (time.perf_counter() - t_iso)
+    if F == 1 or args.no_kernel_timing:
+        iso = None
 
     # aggregate per-kernel timing of this rank (rank 0 reports its own kernel roofline)
     k_ms = sum(s["kernel_ms"][0] for s in stats)
@@ -176,21 +199,34 @@ def main():
 
     value = world * args.steps * F / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
-    roof = None
-    if k_ms > 0:
+    def roofline(k_bytes, k_hbm, k_ms, k_launch, wall_ms):
         achieved = k_bytes / (k_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_iterate (fused estimateU + estimateDualVariables + residual partials)",
+        return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": TRAFFIC,
+                "kernel": "k_iterate_tb (temporally blocked estimateU + estimateDualVariables "
+                          "+ residual partials, <= 4 iterations per HBM pass)",
                 "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
                 "algorithmic_bytes_per_launch": round(k_bytes / k_launch),
                 "algorithmic_model": "SURVEY 8(d): 64 B/px per executed iteration",
                 # what this kernel must move with its temporal blocking (tile loads incl.
-                # halos + interior stores), the honest bandwidth-efficiency figure:
+                # halos + interior stores): the bandwidth-efficiency figure
                 "compulsory_bytes_per_launch": round(k_hbm / k_launch),
                 "compulsory_GBs": round(k_hbm / (k_ms * 1e-3) / 1e9, 1),
                 "compulsory_frac": round(k_hbm / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "kernel_busy_share": round(k_ms / (1e3 * elapsed), 4)}
+                "kernel_busy_share": round(k_ms / wall_ms, 4)}
+
+    roof = None
+    if k_ms > 0:
+        roof = roofline(k_bytes, k_hbm, k_ms, k_launch, 1e3 * elapsed)
+        if F > 1:
+            roof["note"] = (f"{F} pairs in flight: launch durations include interleaving "
+                            f"with the other stream; see roofline_single_stream")
+    roof_iso = None
+    if iso is not None and iso["kernel_ms"][0] > 0:
+        roof_iso = roofline(iso["kernel_bytes"][0], iso["kernel_hbm_bytes"][0],
+                            iso["kernel_ms"][0], iso["kernel_launches"][0],
+                            sum(iso["kernel_ms"][:3]))
+        roof_iso.pop("kernel_busy_share")
     out = {
         "metric": METRIC,
         "value": round(value, 4),
@@ -199,6 +235,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
+        "single_pair_ms": round(single_pair_ms, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -211,6 +248,7 @@ def main():
             "pair": f"{W}x{H}",
             "parallelism": f"pairs sharded over {world} GPU(s), no data-path collective",
             "pairs_in_flight_per_gpu": F,
+            "step": f"one batch of {F} pair(s) solved concurrently per GPU (one ctx + stream each)",
             "iterations_per_pair": iters[0],
             "checks_per_pair": stats[0]["checks_total"],
             "speculation_misses": stats[0]["speculation_misses"],
@@ -219,10 +257,17 @@ def main():
             "pair_roofline_frac": round(pair_bytes * args.steps * F / elapsed / 1e9 / HBM_PEAK_GBS, 4),
         },
         "roofline": roof,
-        "step_breakdown_ms": None if k_ms <= 0 else {
-            "iterate": round(cls_ms[0], 2), "warp": round(cls_ms[1], 2),
-            "other_kernels": round(cls_ms[2], 2),
-            "host_sync_and_gaps": round(ms_per_step - sum(cls_ms), 2)},
+        "roofline_single_stream": roof_iso,
+        # per-pair breakdown of one solve alone on the GPU (F > 1: the isolated solve;
+        # F == 1: the timed steps)
+        "pair_breakdown_ms": None if k_ms <= 0 else (
+            {"iterate": round(iso["kernel_ms"][0], 2), "warp": round(iso["kernel_ms"][1], 2),
+             "other_kernels": round(iso["kernel_ms"][2], 2),
+             "host_sync_and_gaps": round(single_pair_ms - sum(iso["kernel_ms"][:3]), 2)}
+            if iso is not None else
+            {"iterate": round(cls_ms[0], 2), "warp": round(cls_ms[1], 2),
+             "other_kernels": round(cls_ms[2], 2),
+             "host_sync_and_gaps": round(ms_per_step - sum(cls_ms), 2)}),
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -25,7 +25,8 @@
 //     they are silently ignored there);
 //   * a malformed JSON file is an error (the reference ignores parse failure);
 //   * build-only keys: "devices" (list of GPU ordinals, pairs sharded over them),
-//     "medianFiltering", "matches_file", "stats_json", "skip_existing".
+//     "inflight" (pairs in flight per GPU, default 2), "medianFiltering",
+//     "matches_file", "stats_json", "skip_existing".
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -586,11 +587,15 @@ static int from_file(Value &args, bool plan_only) {
       if (ptr) (void)hipFree(ptr);
   };
 
-  if (devices.size() == 1 || plan_only) {
+  // build-only "inflight": pairs solved concurrently per GPU (one worker thread, ctx and
+  // stream each) so one pair's residual read-backs overlap another pair's kernels
+  const int inflight = std::max(1, args.get("inflight", 2).asInt());
+  if (plan_only || (devices.size() == 1 && inflight == 1)) {
     worker(devices[0]);
   } else {
     std::vector<std::thread> th;
-    for (int d : devices) th.emplace_back(worker, d);
+    for (int f = 0; f < inflight; ++f)
+      for (int d : devices) th.emplace_back(worker, d);
     for (auto &t : th) t.join();
   }
   if (hard_error) return 1;

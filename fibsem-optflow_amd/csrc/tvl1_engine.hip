@@ -735,6 +735,8 @@ tvl1_status tvl1_postprocess(tvl1_ctx *c, float *u, float *v, size_t fpitch, con
   return TVL1_OK;
 }
 
+void *tvl1_stream(tvl1_ctx *c) { return c ? (void *)c->own_stream : nullptr; }
+
 tvl1_status tvl1_set_profiling(tvl1_ctx *c, int32_t enable) {
   if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
   c->profiling = enable != 0;

@@ -158,6 +158,8 @@ def load_engine() -> C.CDLL:
                                      C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, C.c_int32,
                                      C.c_void_p]
     lib.tvl1_postprocess.restype = C.c_int
+    lib.tvl1_stream.argtypes = [C.c_void_p]
+    lib.tvl1_stream.restype = C.c_void_p
     lib.tvl1_set_profiling.argtypes = [C.c_void_p, C.c_int32]
     lib.tvl1_set_profiling.restype = C.c_int
     lib.tvl1_destroy.argtypes = [C.c_void_p]
@@ -217,6 +219,11 @@ class Engine:
     def set_params(self, params: TVL1Params):
         self.params = params
         self._check(self.lib.tvl1_set_params(self.ctx, C.byref(params)), "tvl1_set_params")
+
+    @property
+    def stream(self) -> int:
+        """The ctx's own non-blocking hipStream_t (as an int handle)."""
+        return int(self.lib.tvl1_stream(self.ctx) or 0)
 
     def set_profiling(self, on: bool):
         self._check(self.lib.tvl1_set_profiling(self.ctx, 1 if on else 0), "tvl1_set_profiling")

@@ -143,6 +143,10 @@ tvl1_status tvl1_postprocess(tvl1_ctx *ctx, float *u, float *v, size_t flow_pitc
                              const uint8_t *I1, size_t pitch1,
                              int32_t width, int32_t height, int32_t mode, void *stream);
 
+/* The ctx's own non-blocking HIP stream (hipStream_t as void*): callers that keep
+ * several pairs in flight on one device give each ctx its own stream this way. */
+void *tvl1_stream(tvl1_ctx *ctx);
+
 /* Enable (1) / disable (0) per-kernel-class HIP-event timing into tvl1_stats. */
 tvl1_status tvl1_set_profiling(tvl1_ctx *ctx, int32_t enable);
 

@@ -19,7 +19,8 @@ def short(name):
 
 def main():
     d = sys.argv[1]
-    want = sys.argv[2:] or ["k_iterate", "k_warp"]
+    args = [a for a in sys.argv[2:] if not a.startswith("--") and not a.endswith(".json")]
+    want = args or ["k_iterate", "k_warp"]
     rows = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv"))))
     dur = defaultdict(list)
     for r in rows:
@@ -62,6 +63,16 @@ def main():
             res["valu_active_frac"] = round(c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"], 3)
         out[k] = res
     print(json.dumps(out, indent=1))
+    # profiles/traffic.json for bench.py's roofline.traffic
+    tb = [k for k in out if k.startswith("k_iterate_tb") and "hbm_bytes_per_dispatch" in out[k]]
+    if "--emit-traffic" in sys.argv and tb:
+        k = max(tb, key=lambda k: out[k]["dispatches"])
+        path = sys.argv[sys.argv.index("--emit-traffic") + 1]
+        json.dump({"k_iterate_tb_hbm_bytes_per_launch": out[k]["hbm_bytes_per_dispatch"],
+                   "kernel": k, "dispatches": out[k]["dispatches"],
+                   "source": d, "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
+                   "separate passes, average over every dispatch of the bench run"},
+                  open(path, "w"), indent=1)
 
 
 if __name__ == "__main__":
