@@ -28,6 +28,7 @@ thread_local std::string g_create_error;
 
 constexpr int kStripRows = 32;   // rows per wave strip in k_iterate
 constexpr int kTbMax = 4;        // max iterations fused per pass in k_iterate_tb
+constexpr int kRollMinSeg = 8;   // smallest k_iterate_roll segment (rows)
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -65,7 +66,12 @@ struct tvl1_ctx {
   double *pinned = nullptr;  // host-pinned residual landing slot
   hipEvent_t ev_check = nullptr;  // recorded after each residual copy
   int speculate = 0;         // TVL1_SPECULATE=1 enables speculative enqueueing (measured slower)
-  int iter_mode = 0;         // 0 = temporally blocked passes, 1 = one iteration per launch
+  int iter_mode = 3;         // 0 = temporally blocked passes, 1 = one iteration per launch,
+                             // 2 = wavefront-pipelined passes (k_iterate_roll),
+                             // 3 = hybrid: roll for passes of >= 3 iterations on large levels
+  int roll_seg = 0;          // k_iterate_roll rows per segment (0 = auto, see roll_segment)
+  int roll_slots[kRollMax + 1][2] = {};   // resident k_iterate_roll<G, K> wavefronts per device
+  int roll_lds = 0;          // experiment: dummy dynamic LDS per k_iterate_roll block (bytes)
   int warp_mode = 2;         // 2 = k_warp_lds (LDS-staged G window; fastest measured),
                              // 0 = k_warp_img (gradient built in LDS from I1), 1 = k_warp (global)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
@@ -162,6 +168,28 @@ static int pyramid_sizes(int w, int h, int nscales, double step, int *ws, int *h
 // 1: 64x32/256 threads 2x4 px, 2: 64x64/1024 threads 4 px, 3: 64x32/1024 threads 2 px)
 static int tb_region_h(int cfg, int) { return cfg == 2 ? 64 : 32; }
 
+// Rows per k_iterate_roll segment.  Every wavefront runs (rows + 2K) steps, so the pass
+// takes about rounds x (rows + 2K) step times, rounds = ceil(wavefronts / resident slots):
+// pick the split into segments that minimises that (a partial last round idles most of
+// the device; short segments repeat the 2K-row halo).
+static int roll_segment(int bands, int lh, int k, int slots) {
+  if (slots <= 0) slots = 4096;
+  int best = lh;
+  long best_cost = -1;
+  for (int R = 1; R <= 4; ++R) {
+    const int segs = std::max(1, R * slots / bands);
+    const int seg = std::max(kRollMinSeg, (lh + segs - 1) / segs);
+    const long waves = (long)bands * ((lh + seg - 1) / seg);
+    const long rounds = (waves + slots - 1) / slots;
+    const long cost = rounds * (seg + 2 * k);
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best = seg;
+    }
+  }
+  return best;
+}
+
 static int iterate_blocks(int W, int H) {
   const int segs = (W + kSegPx - 1) / kSegPx;
   const int strips = (H + kStripRows - 1) / kStripRows;
@@ -192,8 +220,11 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
   bytes += 2 * 3 * plane;                   // C[2]
   bytes += 2 * align_up(P0 * H, 256);       // in0, in1 (u8)
   bytes += 2 * plane;                       // outu, outv
-  const int tb_blocks = ((W + 55) / 56) * ((H + 23) / 24);   // worst case: RH 32 at 4 iterations
-  const int nblk = (iterate_blocks(W, H) > tb_blocks ? iterate_blocks(W, H) : tb_blocks) + 64;
+  // residual partials: k_iterate_tb worst case (RH 32 at 4 iterations: 56 x 24 px per
+  // block), k_iterate_roll worst case (56-px bands, segments of kRollMinSeg rows)
+  const int tb_blocks = ((W + 55) / 56) * ((H + 23) / 24);
+  const int roll_waves = ((W + 55) / 56) * ((H + kRollMinSeg - 1) / kRollMinSeg);
+  const int nblk = std::max(std::max(iterate_blocks(W, H), tb_blocks), roll_waves) + 64;
   bytes += align_up((size_t)nblk * sizeof(double), 256) + 256;
   bytes += 4096;                            // alignment slack
 
@@ -426,6 +457,14 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     a.taut = taut;
     a.partials = c->partials;
     const int nblk = iterate_blocks(lw, lh);
+    // k_iterate_roll addresses a plane with 32-bit buffer offsets (< 2 GiB per plane).
+    // Passes of >= 3 iterations are VALU-bound, where its smaller halo (x only) wins, as
+    // long as the level has enough rows for one round of >= 32-row segments; 2-iteration
+    // passes are HBM-bound, where k_iterate_tb's float4 streaming is faster (hybrid 3).
+    const bool roll_ok = (size_t)P * lh * sizeof(float) < ((size_t)1 << 31) - 4096;
+    const bool roll_all = roll_ok && c->iter_mode == 2;
+    const bool roll_long = roll_ok && c->iter_mode == 3 &&
+                           (long)((lw + 55) / 56) * ((lh + 31) / 32) >= c->roll_slots[4][gam];
 
     for (int wp = 0; wp < prm.warps; ++wp) {
       if (median) {
@@ -449,7 +488,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         int k = 0;
         bool calc_end = false;
         double prev_sim = prevError;
-        const int kmax = c->iter_mode == 1 ? 1 : kTbMax;
+        const int kmax = c->iter_mode == 1 ? 1 : (roll_all || roll_long) ? kRollMax : kTbMax;
         while (k < kmax && n + k < prm.iterations) {
           const bool calcError = (prm.epsilon > 0) && ((n + k) & 1) && (prev_sim < scaledEps);
           ++k;
@@ -478,6 +517,41 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           else
             hipLaunchKernelGGL(k_iterate<false>, dim3(nblk), dim3(kBlock), 0, st, a);
           hbm = Nl * 4.0 * (ld_planes + st_planes) * k;
+        } else if (roll_all || (roll_long && k >= 3)) {
+          RollArgs ra;
+          ra.it = a;
+          const int out_w = 64 - 2 * k;
+          ra.bands = (lw + out_w - 1) / out_w;
+          const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
+                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam]);
+          ra.seg_rows = seg;
+          const int segs = (lh + seg - 1) / seg;
+          ra.waves = ra.bands * segs;
+          blocks = ra.waves;  // one residual partial per wavefront
+          if (blocks > c->partials_cap)
+            return set_err(c, TVL1_EHIP, "internal: %d wavefronts > partials capacity %d", blocks,
+                           c->partials_cap);
+#define ROLL_LAUNCH(K)                                                                         \
+  if (gam)                                                                                     \
+    hipLaunchKernelGGL((k_iterate_roll<true, K>), dim3((ra.waves + 3) / 4), dim3(256),         \
+                       c->roll_lds, st, ra);                                                   \
+  else                                                                                         \
+    hipLaunchKernelGGL((k_iterate_roll<false, K>), dim3((ra.waves + 3) / 4), dim3(256),        \
+                       c->roll_lds, st, ra);
+          switch (k) {
+            case 1: ROLL_LAUNCH(1) break;
+            case 2: ROLL_LAUNCH(2) break;
+            case 3: ROLL_LAUNCH(3) break;
+            default: ROLL_LAUNCH(4) break;
+          }
+#undef ROLL_LAUNCH
+          // compulsory: every band lane loads its column over the segment's rows + halo
+          double rows = 0.0;
+          for (int sg = 0; sg < segs; ++sg) {
+            const int ys = sg * seg, ye = std::min(ys + seg, lh);
+            rows += std::min(ye - 1 + k, lh - 1) - std::max(ys - k, 0) + 1;
+          }
+          hbm = (double)ra.bands * 64.0 * rows * 4.0 * ld_planes + Nl * 4.0 * st_planes;
         } else {
           TBArgs t;
           t.it = a;
@@ -648,7 +722,12 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (!c) return set_err(nullptr, TVL1_ENOMEM, "out of host memory");
   c->device = device;
   c->prm = *params;
-  if (const char *m = getenv("TVL1_ITER_MODE")) c->iter_mode = atoi(m) == 1 ? 1 : 0;
+  if (const char *m = getenv("TVL1_ITER_MODE")) {
+    const int v = atoi(m);
+    c->iter_mode = v >= 0 && v <= 3 ? v : 3;
+  }
+  if (const char *m = getenv("TVL1_ROLL_SEG")) c->roll_seg = atoi(m);
+  if (const char *m = getenv("TVL1_ROLL_LDS")) c->roll_lds = std::max(0, atoi(m));
   if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = atoi(m);
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
   if (const char *m = getenv("TVL1_WARP_TH")) c->warp_th = atoi(m);
@@ -660,6 +739,24 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
       hipEventCreateWithFlags(&c->ev_check, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return set_err(nullptr, TVL1_EHIP, "HIP initialisation failed on device %d", device);
+  }
+  // resident wavefronts of each k_iterate_roll instance (4 per 256-thread block)
+  {
+    auto slots = [&](const void *fn) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, c->roll_lds) != hipSuccess)
+        nb = 0;
+      return nb * 4 * prop.multiProcessorCount;
+    };
+    c->roll_slots[1][0] = slots((const void *)k_iterate_roll<false, 1>);
+    c->roll_slots[2][0] = slots((const void *)k_iterate_roll<false, 2>);
+    c->roll_slots[3][0] = slots((const void *)k_iterate_roll<false, 3>);
+    c->roll_slots[4][0] = slots((const void *)k_iterate_roll<false, 4>);
+    c->roll_slots[1][1] = slots((const void *)k_iterate_roll<true, 1>);
+    c->roll_slots[2][1] = slots((const void *)k_iterate_roll<true, 2>);
+    c->roll_slots[3][1] = slots((const void *)k_iterate_roll<true, 3>);
+    c->roll_slots[4][1] = slots((const void *)k_iterate_roll<true, 4>);
+    (void)hipGetLastError();
   }
   *out = c;
   return TVL1_OK;

@@ -513,6 +513,49 @@ __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float
   return y > 0 ? yhi : ylo;
 }
 
+// estimateU at one px (x, y): the TH step from the warp constants and u^{n-1}, then
+// u^n = v + theta * div(p^{n-1}).  pl = p*1 at x-1, pu = p*2 at y-1.  Shared by every
+// iteration kernel, so they all run exactly this sequence of IEEE float operations.
+template <bool G>
+__device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rhoc, float u1o,
+                                              float u2o, float u3o, float p11, float p11l,
+                                              float p12, float p12u, float p21, float p21l,
+                                              float p22, float p22u, float p31, float p31l,
+                                              float p32, float p32u, int x, int y,
+                                              const IterArgs &a, float &n1, float &n2,
+                                              float &n3) {
+  const float Ix2 = I1wxv * I1wxv;
+  const float Iy2 = I1wyv * I1wyv;
+  const float gradv = Ix2 + Iy2;
+  const float rho = rhoc + (I1wxv * u1o + I1wyv * u2o) + a.gamma * (G ? u3o : 0.0f);
+  // TH operator, branch-free: the three candidate steps are computed with the
+  // reference's exact expressions and the applicable one selected.
+  const bool lo = rho < -a.l_t * gradv;
+  const bool hi = rho > a.l_t * gradv;
+  const bool mid = gradv > kFltEps;
+  const float fi = -rho / gradv;     // only selected when gradv > FLT_EPSILON
+  float d1 = mid ? fi * I1wxv : 0.0f;
+  float d2 = mid ? fi * I1wyv : 0.0f;
+  float d3 = mid ? fi * a.gamma : 0.0f;
+  d1 = hi ? -a.l_t * I1wxv : d1;
+  d2 = hi ? -a.l_t * I1wyv : d2;
+  d3 = hi ? -a.theta * a.gamma : d3;
+  d1 = lo ? a.l_t * I1wxv : d1;
+  d2 = lo ? a.l_t * I1wyv : d2;
+  d3 = lo ? a.theta * a.gamma : d3;
+  const float v1 = u1o + d1;
+  const float v2 = u2o + d2;
+  const float div1 = divergence(p11, p11l, p12, p12u, x, y);
+  const float div2 = divergence(p21, p21l, p22, p22u, x, y);
+  n1 = v1 + a.theta * div1;
+  n2 = v2 + a.theta * div2;
+  if (G) {
+    const float v3 = u3o + d3;
+    const float div3 = divergence(p31, p31l, p32, p32u, x, y);
+    n3 = v3 + a.theta * div3;
+  }
+}
+
 // estimateU for the PX px of this lane on row y.  up* = p12/p22/p32 of row y-1.
 template <bool G, int PX = 4>
 __device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up12)[PX],
@@ -531,48 +574,33 @@ __device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up
   }
 #pragma unroll
   for (int k = 0; k < PX; ++k) {
-    const int x = X0 + k;
-    const float I1wxv = r.wx[k];
-    const float I1wyv = r.wy[k];
-    const float Ix2 = I1wxv * I1wxv;
-    const float Iy2 = I1wyv * I1wyv;
-    const float gradv = Ix2 + Iy2;
-    const float u1o = r.u1[k];
-    const float u2o = r.u2[k];
     const float u3o = G ? r.u3[k] : 0.0f;
-    const float rho = r.rh[k] + (I1wxv * u1o + I1wyv * u2o) + a.gamma * u3o;
-    // TH operator, branch-free: the three candidate steps are computed with the
-    // reference's exact expressions and the applicable one selected.
-    const bool lo = rho < -a.l_t * gradv;
-    const bool hi = rho > a.l_t * gradv;
-    const bool mid = gradv > kFltEps;
-    const float fi = -rho / gradv;     // only selected when gradv > FLT_EPSILON
-    float d1 = mid ? fi * I1wxv : 0.0f;
-    float d2 = mid ? fi * I1wyv : 0.0f;
-    float d3 = mid ? fi * a.gamma : 0.0f;
-    d1 = hi ? -a.l_t * I1wxv : d1;
-    d2 = hi ? -a.l_t * I1wyv : d2;
-    d3 = hi ? -a.theta * a.gamma : d3;
-    d1 = lo ? a.l_t * I1wxv : d1;
-    d2 = lo ? a.l_t * I1wyv : d2;
-    d3 = lo ? a.theta * a.gamma : d3;
-    const float v1 = u1o + d1;
-    const float v2 = u2o + d2;
-    const float div1 = divergence(r.p11[k], l11[k], r.p12[k], up12[k], x, y);
-    const float div2 = divergence(r.p21[k], l21[k], r.p22[k], up22[k], x, y);
-    n1[k] = v1 + a.theta * div1;
-    n2[k] = v2 + a.theta * div2;
-    if (G) {
-      const float v3 = u3o + d3;
-      const float div3 = divergence(r.p31[k], l31[k], r.p32[k], up32[k], x, y);
-      n3[k] = v3 + a.theta * div3;
-    }
+    const float p31 = G ? r.p31[k] : 0.0f, p31l = G ? l31[k] : 0.0f;
+    const float p32 = G ? r.p32[k] : 0.0f;
+    estimate_u_px<G>(r.wx[k], r.wy[k], r.rh[k], r.u1[k], r.u2[k], u3o, r.p11[k], l11[k],
+                     r.p12[k], up12[k], r.p21[k], l21[k], r.p22[k], up22[k], p31, p31l, p32,
+                     up32[k], X0 + k, y, a, n1[k], n2[k], n3[k]);
   }
 }
 
 __device__ __forceinline__ float hypot_f(float a, float b) { return sqrtf(a * a + b * b); }
 
-// One projection component: p' = (p + taut * du) / ng, du from u at (x+1) and (y+1).
+// estimateDualVariables for one (u, p*1, p*2) component at one px:
+// p' = (p + taut * du) / ng, du from u at (x+1) and (y+1) (clamped at the image edge).
+__device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_right,
+                                        bool has_down, float taut, float pa, float pb, float &oa,
+                                        float &ob) {
+  const float right = has_right ? ur : uc;
+  const float down = has_down ? ud : uc;
+  const float ux = right - uc;
+  const float uy = down - uc;
+  const float g = hypot_f(ux, uy);
+  const float ng = 1.0f + taut * g;
+  oa = (pa + taut * ux) / ng;
+  ob = (pb + taut * uy) / ng;
+}
+
+// One projection component for the PX px of this lane.
 template <int PX>
 __device__ __forceinline__ void dual_component(const float (&uc)[PX], const float (&un)[PX],
                                                bool has_down, int X0, int W, float taut,
@@ -583,17 +611,8 @@ __device__ __forceinline__ void dual_component(const float (&uc)[PX], const floa
 #pragma unroll
   for (int k = 0; k < PX - 1; ++k) ur[k] = uc[k + 1];
 #pragma unroll
-  for (int k = 0; k < PX; ++k) {
-    const int x = X0 + k;
-    const float right = (x + 1 < W) ? ur[k] : uc[k];
-    const float down = has_down ? un[k] : uc[k];
-    const float ux = right - uc[k];
-    const float uy = down - uc[k];
-    const float g = hypot_f(ux, uy);
-    const float ng = 1.0f + taut * g;
-    oa[k] = (pa[k] + taut * ux) / ng;
-    ob[k] = (pb[k] + taut * uy) / ng;
-  }
+  for (int k = 0; k < PX; ++k)
+    dual_px(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k], oa[k], ob[k]);
 }
 
 template <bool G>
@@ -872,6 +891,257 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
     load_row<G, PX>(r[g], a, (size_t)ya * a.P + xa);
   }
   tb_iterate_store<G, RH, NG, PX>(t, lds, r, Y, X, c4, rr);
+}
+
+// ---------------------------------------------------------------- K6+K8 wavefront pipeline
+// k_iterate_roll<G, K>: K consecutive primal-dual iterations in ONE streaming pass.  One
+// wavefront owns a 64-px column band of one row segment and walks down it, one row per
+// step; no LDS, no barriers.
+//
+// Dependencies of iteration n of a pass (Jacobi: reads n-1, writes n):
+//   u^n(y) <- u^{n-1}(y), p^{n-1}(y), p^{n-1}(x-1, y), p^{n-1}(y-1)      (estimateU)
+//   p^n(y) <- p^{n-1}(y), u^n(y), u^n(x+1, y), u^n(y+1)                    (estimateDual)
+// so once input row r is loaded, stage n computes u^n at row r-n+1 and p^n at row r-n.
+// Per stage the wave keeps the two newest u rows and p rows in registers (one px per
+// lane), plus the warp constants of the K newest input rows, and it stores u^K and p^K.
+// x neighbours are DPP wavefront shifts.  Every iteration invalidates one lane at each
+// band edge, so a band carries a K-px halo on both sides and stores its 64 - 2K interior
+// lanes; a segment starts K rows above its output rows (their p^{n-1}(y-1) is missing)
+// and reads K rows below them.  At the image border OpenCV's clamp / special divergence
+// forms apply and nothing is invalidated.  HBM per px and pass: 36 B x 64/(64-2K) x
+// (rows + 2K)/rows loaded, 24 B stored -- for any K.  Arithmetic is estimate_u_px /
+// dual_px, the same as the other iteration kernels (bit-identical results).
+constexpr int kRollMax = 4;
+constexpr int kRollAhead = 2;   // input rows loaded ahead of the row entering the pipeline
+
+struct RollArgs {
+  IterArgs it;
+  int bands;      // column bands per row: ceil(W / (64 - 2K))
+  int seg_rows;   // output rows per segment
+  int waves;      // bands * segments
+};
+
+// lane i <- lane i-1 (DPP wave_shr:1; lane 0 gets 0)
+__device__ __forceinline__ float from_left(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+// lane i <- lane i+1 (DPP wave_shl:1; lane 63 gets 0)
+__device__ __forceinline__ float from_right(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+// XCD-contiguous block order: the blocks the hardware sends to one XCD (b % 8) get one
+// contiguous run of logical indices, so neighbouring bands share that XCD's L2.
+__device__ __forceinline__ int xcd_chunk(int b, int n) {
+  const int q = n / kXcds, rem = n % kXcds;
+  const int x = b % kXcds, i = b / kXcds;
+  return x * q + imin(x, rem) + i;
+}
+
+template <bool G>
+struct RollIn {   // one input row at this lane
+  float wx, wy, rh, u1, u2, u3, p11, p12, p21, p22, p31, p32;
+};
+
+// Buffer access to a plane: scalar descriptor (base, size in bytes), the row in the
+// scalar offset, the lane's column as one 32-bit VGPR byte offset.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bload(const float *p, unsigned bytes, unsigned voff, unsigned soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(plane_rsrc(p, bytes), (int)voff, (int)soff, 0));
+}
+constexpr unsigned kOOB = 0x7ffffff0u;   // byte offset beyond every plane: store dropped
+__device__ __forceinline__ void bstore(float *p, unsigned bytes, unsigned voff, unsigned soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
+}
+
+// p is loaded unconditionally and zeroed by a select when p == 0 (first pass of a level):
+// a branch here would make the compiler's wait counts conservative for every row.
+template <bool G>
+__device__ __forceinline__ void roll_load(RollIn<G> &v, const IterArgs &a, unsigned nb,
+                                          unsigned soff, unsigned voff) {
+  v.wx = bload(a.I1wx, nb, voff, soff);
+  v.wy = bload(a.I1wy, nb, voff, soff);
+  v.rh = bload(a.rho, nb, voff, soff);
+  v.u1 = bload(a.u1s, nb, voff, soff);
+  v.u2 = bload(a.u2s, nb, voff, soff);
+  v.u3 = G ? bload(a.u3s, nb, voff, soff) : 0.0f;
+  v.p11 = bload(a.p11s, nb, voff, soff);
+  v.p12 = bload(a.p12s, nb, voff, soff);
+  v.p21 = bload(a.p21s, nb, voff, soff);
+  v.p22 = bload(a.p22s, nb, voff, soff);
+  v.p31 = G ? bload(a.p31s, nb, voff, soff) : 0.0f;
+  v.p32 = G ? bload(a.p32s, nb, voff, soff) : 0.0f;
+}
+
+template <bool G>
+__device__ __forceinline__ void roll_pzero(RollIn<G> &v, bool z) {
+  v.p11 = z ? 0.0f : v.p11;
+  v.p12 = z ? 0.0f : v.p12;
+  v.p21 = z ? 0.0f : v.p21;
+  v.p22 = z ? 0.0f : v.p22;
+  v.p31 = z ? 0.0f : v.p31;
+  v.p32 = z ? 0.0f : v.p32;
+}
+
+// One step of the pipeline: input row r (in `in`) enters stage 0, every stage advances
+// one row, and input row r + kRollAhead is loaded into `ahead` (a ring of kRollAhead + 1
+// rows, so no register holding a load in flight is ever copied).  Every load and store is issued
+// unconditionally (rows clamped; masked stores use an out-of-range offset, which the
+// buffer unit drops), so the compiler can keep this step's stores and the next row's
+// loads in flight with counted waits.  Stages run every step: before a segment's first
+// rows reach them and past the image bottom they compute values that no stored cell
+// depends on (see the dependency list above; the border forms select, never combine).
+template <bool G, int K>
+struct RollPipe {
+  float U1c[K + 1], U2c[K + 1], U3c[K + 1], U1p[K + 1], U2p[K + 1], U3p[K + 1];
+  float P11c[K + 1], P12c[K + 1], P21c[K + 1], P22c[K + 1], P31c[K + 1], P32c[K + 1];
+  float P11p[K + 1], P12p[K + 1], P21p[K + 1], P22p[K + 1], P31p[K + 1], P32p[K + 1];
+  float CX[K], CY[K], CR[K];   // warp constants of input rows r, r-1, ...
+};
+
+template <bool G, int K>
+__device__ __forceinline__ void roll_step(RollPipe<G, K> &S, const RollIn<G> &in, RollIn<G> &ahead,
+                                          const IterArgs &a, int r, int X, unsigned Xc,
+                                          unsigned Xs, unsigned nb, unsigned rowb, bool out_col,
+                                          bool has_right, int ys, int ye, double &acc) {
+  roll_load<G>(ahead, a, nb, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, Xc);
+  // keep the loads of row r + kRollAhead ahead of this step's stores: waiting for them
+  // kRollAhead steps later then leaves the younger stores and loads in flight (vmcnt
+  // counts in issue order)
+  __builtin_amdgcn_sched_barrier(0);
+  // shift every stage one row down
+#pragma unroll
+  for (int n = K; n >= 1; --n) {
+    S.U1p[n] = S.U1c[n]; S.U2p[n] = S.U2c[n]; if (G) S.U3p[n] = S.U3c[n];
+  }
+#pragma unroll
+  for (int n = K - 1; n >= 0; --n) {
+    S.P11p[n] = S.P11c[n]; S.P12p[n] = S.P12c[n]; S.P21p[n] = S.P21c[n]; S.P22p[n] = S.P22c[n];
+    if (G) { S.P31p[n] = S.P31c[n]; S.P32p[n] = S.P32c[n]; }
+  }
+#pragma unroll
+  for (int n = K - 1; n >= 1; --n) { S.CX[n] = S.CX[n - 1]; S.CY[n] = S.CY[n - 1]; S.CR[n] = S.CR[n - 1]; }
+  RollIn<G> v = in;
+  roll_pzero<G>(v, a.p_zero);
+  S.CX[0] = v.wx; S.CY[0] = v.wy; S.CR[0] = v.rh;
+  S.U1p[0] = v.u1; S.U2p[0] = v.u2; S.U3p[0] = v.u3;
+  S.P11c[0] = v.p11; S.P12c[0] = v.p12; S.P21c[0] = v.p21; S.P22c[0] = v.p22;
+  S.P31c[0] = v.p31; S.P32c[0] = v.p32;
+
+#pragma unroll
+  for (int n = 1; n <= K; ++n) {
+    const int yU = r - n + 1;    // estimateU row of stage n
+    float n1, n2, n3 = 0.0f;
+    estimate_u_px<G>(S.CX[n - 1], S.CY[n - 1], S.CR[n - 1], S.U1p[n - 1], S.U2p[n - 1],
+                     S.U3p[n - 1], S.P11c[n - 1], from_left(S.P11c[n - 1]), S.P12c[n - 1],
+                     S.P12p[n - 1], S.P21c[n - 1], from_left(S.P21c[n - 1]), S.P22c[n - 1],
+                     S.P22p[n - 1], S.P31c[n - 1], G ? from_left(S.P31c[n - 1]) : 0.0f,
+                     S.P32c[n - 1], S.P32p[n - 1], X, yU, a, n1, n2, n3);
+    if (n == K) {
+      const bool st = out_col && yU >= ys && yU < ye;
+      if (a.calc_err) {
+        const float f1 = (S.U1p[n - 1] - n1) * (S.U1p[n - 1] - n1);
+        const float f2 = (S.U2p[n - 1] - n2) * (S.U2p[n - 1] - n2);
+        acc += st ? (double)(f1 + f2) : 0.0;
+      }
+      const unsigned vo = st ? (unsigned)yU * rowb + Xs : kOOB;
+      bstore(a.u1d, nb, vo, 0, n1);
+      bstore(a.u2d, nb, vo, 0, n2);
+      if (G) bstore(a.u3d, nb, vo, 0, n3);
+    }
+    S.U1c[n] = n1; S.U2c[n] = n2; if (G) S.U3c[n] = n3;
+
+    const int yD = r - n;        // estimateDualVariables row of stage n
+    const bool has_down = yD + 1 < a.H;
+    dual_px(S.U1p[n], from_right(S.U1p[n]), S.U1c[n], has_right, has_down, a.taut, S.P11p[n - 1],
+            S.P12p[n - 1], S.P11c[n], S.P12c[n]);
+    dual_px(S.U2p[n], from_right(S.U2p[n]), S.U2c[n], has_right, has_down, a.taut, S.P21p[n - 1],
+            S.P22p[n - 1], S.P21c[n], S.P22c[n]);
+    if (G)
+      dual_px(S.U3p[n], from_right(S.U3p[n]), S.U3c[n], has_right, has_down, a.taut,
+              S.P31p[n - 1], S.P32p[n - 1], S.P31c[n], S.P32c[n]);
+    if (n == K) {
+      const bool st = out_col && yD >= ys && yD < ye;
+      const unsigned vo = st ? (unsigned)yD * rowb + Xs : kOOB;
+      bstore(a.p11d, nb, vo, 0, S.P11c[n]);
+      bstore(a.p12d, nb, vo, 0, S.P12c[n]);
+      bstore(a.p21d, nb, vo, 0, S.P21c[n]);
+      bstore(a.p22d, nb, vo, 0, S.P22c[n]);
+      if (G) {
+        bstore(a.p31d, nb, vo, 0, S.P31c[n]);
+        bstore(a.p32d, nb, vo, 0, S.P32c[n]);
+      }
+    }
+  }
+}
+
+template <bool G, int K>
+__global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
+  const IterArgs &a = ra.it;
+  const int lane = threadIdx.x & 63;
+  // wave-uniform (scalar) band / segment
+  const int wid =
+      __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+  if (wid >= ra.waves) return;                       // whole wavefronts only
+  const int band = wid % ra.bands, seg = wid / ra.bands;
+  const int X = band * (64 - 2 * K) - K + lane;
+  const unsigned Xc = 4u * imin(imax(X, 0), a.W - 1);  // byte offset of the clamped load column
+  const unsigned Xs = 4u * imax(X, 0);                  // store column (out_col only)
+  const unsigned nb = 4u * (unsigned)a.P * (unsigned)a.H;   // plane bytes
+  const unsigned rowb = 4u * (unsigned)a.P;                 // row pitch in bytes
+  const bool out_col = lane >= K && lane < 64 - K && X < a.W;
+  const bool has_right = X + 1 < a.W;
+  const int ys = seg * ra.seg_rows, ye = imin(ys + ra.seg_rows, a.H);
+  const int r0 = imax(ys - K, 0);
+  // steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K (rows >= H drain the pipeline)
+  const int thirds = (ye + K - r0 + 2) / 3;
+
+  RollPipe<G, K> S;
+#pragma unroll
+  for (int n = 0; n <= K; ++n) {
+    S.U1c[n] = S.U2c[n] = S.U3c[n] = S.U1p[n] = S.U2p[n] = S.U3p[n] = 0.0f;
+    S.P11c[n] = S.P12c[n] = S.P21c[n] = S.P22c[n] = S.P31c[n] = S.P32c[n] = 0.0f;
+    S.P11p[n] = S.P12p[n] = S.P21p[n] = S.P22p[n] = S.P31p[n] = S.P32p[n] = 0.0f;
+  }
+#pragma unroll
+  for (int n = 0; n < K; ++n) S.CX[n] = S.CY[n] = S.CR[n] = 0.0f;
+
+  // Each prologue row load is followed by dropped (out-of-range) stores, as many as a
+  // step issues: the loop is then entered with the same memory operations in flight as
+  // its back edge carries, so the waits at the top of the loop are counted past the
+  // younger stores and loads on both paths.
+  auto dummy_stores = [&]() {
+    bstore(a.u1d, nb, kOOB, 0, 0.0f);
+    bstore(a.u2d, nb, kOOB, 0, 0.0f);
+    if (G) bstore(a.u3d, nb, kOOB, 0, 0.0f);
+    bstore(a.p11d, nb, kOOB, 0, 0.0f);
+    bstore(a.p12d, nb, kOOB, 0, 0.0f);
+    bstore(a.p21d, nb, kOOB, 0, 0.0f);
+    bstore(a.p22d, nb, kOOB, 0, 0.0f);
+    if (G) {
+      bstore(a.p31d, nb, kOOB, 0, 0.0f);
+      bstore(a.p32d, nb, kOOB, 0, 0.0f);
+    }
+  };
+  static_assert(kRollAhead == 2, "the step loop below is unrolled for a 3-row ring");
+  RollIn<G> A, B, C;
+  roll_load<G>(A, a, nb, (unsigned)r0 * rowb, Xc);
+  dummy_stores();
+  roll_load<G>(B, a, nb, (unsigned)imin(r0 + 1, a.H - 1) * rowb, Xc);
+  dummy_stores();
+  double acc = 0.0;
+  for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
+    roll_step<G, K>(S, A, C, a, r, X, Xc, Xs, nb, rowb, out_col, has_right, ys, ye, acc);
+    roll_step<G, K>(S, B, A, a, r + 1, X, Xc, Xs, nb, rowb, out_col, has_right, ys, ye, acc);
+    roll_step<G, K>(S, C, B, a, r + 2, X, Xc, Xs, nb, rowb, out_col, has_right, ys, ye, acc);
+  }
+  if (a.calc_err) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) a.partials[wid] = acc;
+  }
 }
 
 // K7: fixed-order sum of the per-block partials (one block).

@@ -14,6 +14,12 @@ pytestmark = pytest.mark.gpu
 EPE_TOL = 1e-3  # px, BASELINE.json north_star
 
 
+def bits_equal(a, b):
+    """Bitwise equality of float arrays (distinguishes -0.0 from +0.0, NaN payloads)."""
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 @pytest.fixture(scope="module")
 def engine(built):
     return capi.Engine(capi.make_params())
@@ -47,7 +53,7 @@ def test_engine_matches_oracle(engine, W, H, seed, kw):
     e = capi.epe(u, v, ur, vr)
     assert float(e.max()) <= EPE_TOL, f"max EPE {e.max()}"
     # bit-exactness is expected (same IEEE ops, no FMA); report if it ever drifts
-    assert np.array_equal(u, ur) and np.array_equal(v, vr), \
+    assert bits_equal(u, ur) and bits_equal(v, vr), \
         f"not bit-exact: max|du|={np.abs(u-ur).max()} max|dv|={np.abs(v-vr).max()}"
 
 
@@ -69,14 +75,20 @@ def test_constant_images_give_zero_flow(engine):
 
 # Every kernel / schedule configuration must give the same bits (selected by env at
 # tvl1_create): TVL1_ITER_MODE=1 -> one iteration per launch (rolling-strip kernel),
-# TVL1_TB_CFG = 0/1/2 -> temporally blocked regions 64x32/512thr, 64x32/256thr,
-# 64x64/1024thr; TVL1_WARP_MODE=1 -> global-memory gather; TVL1_SPECULATE=0 -> no
-# speculative enqueueing at check iterations.
-MODES = [("TVL1_ITER_MODE", "1"), ("TVL1_TB_CFG", "0"), ("TVL1_TB_CFG", "1"),
-         ("TVL1_TB_CFG", "2"), ("TVL1_TB_CFG", "3"), ("TVL1_WARP_TH", "8"), ("TVL1_WARP_TH", "32"), ("TVL1_WARP_MODE", "1"), ("TVL1_WARP_MODE", "0"), ("TVL1_SPECULATE", "1")]
+# TVL1_ITER_MODE=2 -> wavefront-pipelined passes (TVL1_ROLL_SEG rows per segment),
+# TVL1_TB_CFG = 0/1/2/3 -> temporally blocked regions 64x32/512thr, 64x32/256thr,
+# 64x64/1024thr, 2 px per lane; TVL1_WARP_MODE=1/0 -> global-memory gather / gradient
+# from I1 in LDS; TVL1_WARP_TH -> warp tile height; TVL1_SPECULATE=1 -> speculative
+# enqueueing at check iterations.
+MODES = ["TVL1_ITER_MODE=0", "TVL1_ITER_MODE=1", "TVL1_ITER_MODE=2", "TVL1_ITER_MODE=3", "TVL1_ITER_MODE=2,TVL1_ROLL_SEG=8",
+         "TVL1_ITER_MODE=2,TVL1_ROLL_SEG=64", "TVL1_TB_CFG=0", "TVL1_TB_CFG=1",
+         "TVL1_TB_CFG=2", "TVL1_TB_CFG=3", "TVL1_WARP_TH=8", "TVL1_WARP_TH=32",
+         "TVL1_WARP_MODE=1", "TVL1_WARP_MODE=0", "TVL1_SPECULATE=1"]
+KNOBS = ("TVL1_ITER_MODE", "TVL1_ROLL_SEG", "TVL1_ROLL_WAVES", "TVL1_TB_CFG", "TVL1_WARP_MODE",
+         "TVL1_SPECULATE", "TVL1_WARP_TH")
 
 
-@pytest.mark.parametrize("env", MODES, ids=[f"{k}={v}" for k, v in MODES])
+@pytest.mark.parametrize("env", MODES)
 @pytest.mark.parametrize("W,H,seed,kw", [
     (250, 131, 21, dict(nscales=5, warps=5)),
     (97, 201, 22, dict(nscales=4, warps=3, gamma=0.1)),
@@ -84,12 +96,10 @@ MODES = [("TVL1_ITER_MODE", "1"), ("TVL1_TB_CFG", "0"), ("TVL1_TB_CFG", "1"),
     (300, 200, 24, dict(nscales=1, warps=2)),
 ])
 def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
-    monkeypatch.delenv("TVL1_ITER_MODE", raising=False)
-    monkeypatch.delenv("TVL1_TB_CFG", raising=False)
-    monkeypatch.delenv("TVL1_WARP_MODE", raising=False)
-    monkeypatch.delenv("TVL1_SPECULATE", raising=False)
-    monkeypatch.delenv("TVL1_WARP_TH", raising=False)
-    monkeypatch.setenv(*env)
+    for k in KNOBS:
+        monkeypatch.delenv(k, raising=False)
+    for kv in env.split(","):
+        monkeypatch.setenv(*kv.split("="))
     p = capi.make_params(**kw)
     eng = capi.Engine(p)
     I0, I1 = synth.gen_pair(W, H, seed=seed)
@@ -97,7 +107,7 @@ def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
     eng.close()
     ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
     np.testing.assert_array_equal(wi, wr)
-    assert np.array_equal(u, ur) and np.array_equal(v, vr)
+    assert bits_equal(u, ur) and bits_equal(v, vr)
 
 
 GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
@@ -112,7 +122,7 @@ def test_engine_reproduces_golden(engine, path):
     u, v, st, wi = engine.calc_host(g["I0"], g["I1"])
     assert st["levels"] == int(g["levels"])
     np.testing.assert_array_equal(wi, g["warp_iters"])
-    assert np.array_equal(u, g["u"]) and np.array_equal(v, g["v"])
+    assert bits_equal(u, g["u"]) and bits_equal(v, g["v"])
 
 
 def test_large_flow_uses_global_gather_fallback(engine):
@@ -130,4 +140,4 @@ def test_large_flow_uses_global_gather_fallback(engine):
     ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
     assert float(np.abs(ur).max()) > 5.0   # the case really leaves the window
     np.testing.assert_array_equal(wi, wr)
-    assert np.array_equal(u, ur) and np.array_equal(v, vr)
+    assert bits_equal(u, ur) and bits_equal(v, vr)
