@@ -70,13 +70,17 @@ struct tvl1_ctx {
                              // 2 = wavefront-pipelined passes (k_iterate_roll),
                              // 3 = hybrid: roll for passes of >= 3 iterations on large levels
   int roll_seg = 0;          // k_iterate_roll rows per segment (0 = auto, see roll_segment)
-  int roll_slots[kRollMax + 1][2] = {};   // resident k_iterate_roll<G, K> wavefronts per device
+  int roll_px = 2;           // px per lane of k_iterate_roll (1 or 2)
+  int roll_slots[kRollMax + 1][2][3] = {};   // resident k_iterate_roll<G, K, PX> wavefronts
   int roll_lds = 0;          // experiment: dummy dynamic LDS per k_iterate_roll block (bytes)
   int warp_mode = 2;         // 2 = k_warp_lds (LDS-staged G window; fastest measured),
                              // 0 = k_warp_img (gradient built in LDS from I1), 1 = k_warp (global)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
   int warp_th = 16;          // k_warp_lds tile height (8, 16, 32)
-  int tb_cfg = 0;            // k_iterate_tb shape: 0 = 64x32/512 thr, 1 = 64x32/256 thr, 2 = 64x64/1024 thr
+  // k_iterate_tb shape (0 = 64x32/512 thr, 1 = 64x32/256 thr, 2 = 64x64/1024 thr,
+  // 3 = 64x32/1024 thr 2 px each) for passes of <= 2 iterations (HBM-bound: 0 is
+  // fastest) and of >= 3 iterations (VALU-bound: 3 is fastest); TVL1_TB_CFG sets both
+  int tb_cfg = 0, tb_cfg_long = 3;
 
   // optional per-kernel-class HIP-event timing (tvl1_set_profiling)
   bool profiling = false;
@@ -458,13 +462,15 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     a.partials = c->partials;
     const int nblk = iterate_blocks(lw, lh);
     // k_iterate_roll addresses a plane with 32-bit buffer offsets (< 2 GiB per plane).
-    // Passes of >= 3 iterations are VALU-bound, where its smaller halo (x only) wins, as
-    // long as the level has enough rows for one round of >= 32-row segments; 2-iteration
-    // passes are HBM-bound, where k_iterate_tb's float4 streaming is faster (hybrid 3).
+    // Hybrid (3): 2-iteration passes (HBM-bound) stream best through k_iterate_roll's
+    // x-only halo; passes of >= 3 iterations are VALU-bound, where the roll kernel wins
+    // only while the level has enough rows for one round of >= 32-row segments (short
+    // segments repeat the 2K-row halo) and k_iterate_tb (64 x 32, 2 px/lane) wins below.
     const bool roll_ok = (size_t)P * lh * sizeof(float) < ((size_t)1 << 31) - 4096;
     const bool roll_all = roll_ok && c->iter_mode == 2;
-    const bool roll_long = roll_ok && c->iter_mode == 3 &&
-                           (long)((lw + 55) / 56) * ((lh + 31) / 32) >= c->roll_slots[4][gam];
+    const bool roll_short = roll_ok && c->iter_mode == 3;
+    const bool roll_long = roll_short &&
+                           (long)((lw + 55) / 56) * ((lh + 31) / 32) >= c->roll_slots[4][gam][1];
 
     for (int wp = 0; wp < prm.warps; ++wp) {
       if (median) {
@@ -488,7 +494,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         int k = 0;
         bool calc_end = false;
         double prev_sim = prevError;
-        const int kmax = c->iter_mode == 1 ? 1 : (roll_all || roll_long) ? kRollMax : kTbMax;
+        const int kmax = c->iter_mode == 1 ? 1 : (roll_all || roll_short) ? kRollMax : kTbMax;
         while (k < kmax && n + k < prm.iterations) {
           const bool calcError = (prm.epsilon > 0) && ((n + k) & 1) && (prev_sim < scaledEps);
           ++k;
@@ -517,13 +523,15 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           else
             hipLaunchKernelGGL(k_iterate<false>, dim3(nblk), dim3(kBlock), 0, st, a);
           hbm = Nl * 4.0 * (ld_planes + st_planes) * k;
-        } else if (roll_all || (roll_long && k >= 3)) {
+        } else if (roll_all || (roll_short && k <= 2) || (roll_long && k >= 3)) {
           RollArgs ra;
           ra.it = a;
-          const int out_w = 64 - 2 * k;
+          const int px = c->roll_px;
+          const int halo = (k + px - 1) / px * px;   // roll_halo<K, PX>
+          const int out_w = 64 * px - 2 * halo;
           ra.bands = (lw + out_w - 1) / out_w;
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam]);
+                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px]);
           ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           ra.waves = ra.bands * segs;
@@ -531,18 +539,27 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d wavefronts > partials capacity %d", blocks,
                            c->partials_cap);
-#define ROLL_LAUNCH(K)                                                                         \
+#define ROLL_LAUNCH(K, PX)                                                                     \
   if (gam)                                                                                     \
-    hipLaunchKernelGGL((k_iterate_roll<true, K>), dim3((ra.waves + 3) / 4), dim3(256),         \
+    hipLaunchKernelGGL((k_iterate_roll<true, K, PX>), dim3((ra.waves + 3) / 4), dim3(256),     \
                        c->roll_lds, st, ra);                                                   \
   else                                                                                         \
-    hipLaunchKernelGGL((k_iterate_roll<false, K>), dim3((ra.waves + 3) / 4), dim3(256),        \
+    hipLaunchKernelGGL((k_iterate_roll<false, K, PX>), dim3((ra.waves + 3) / 4), dim3(256),    \
                        c->roll_lds, st, ra);
-          switch (k) {
-            case 1: ROLL_LAUNCH(1) break;
-            case 2: ROLL_LAUNCH(2) break;
-            case 3: ROLL_LAUNCH(3) break;
-            default: ROLL_LAUNCH(4) break;
+          if (px == 1) {
+            switch (k) {
+              case 1: ROLL_LAUNCH(1, 1) break;
+              case 2: ROLL_LAUNCH(2, 1) break;
+              case 3: ROLL_LAUNCH(3, 1) break;
+              default: ROLL_LAUNCH(4, 1) break;
+            }
+          } else {
+            switch (k) {
+              case 1: ROLL_LAUNCH(1, 2) break;
+              case 2: ROLL_LAUNCH(2, 2) break;
+              case 3: ROLL_LAUNCH(3, 2) break;
+              default: ROLL_LAUNCH(4, 2) break;
+            }
           }
 #undef ROLL_LAUNCH
           // compulsory: every band lane loads its column over the segment's rows + halo
@@ -557,7 +574,8 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           t.it = a;
           t.niter = k;
           t.tiles_x = (lw + 55) / 56;
-          const int rh = tb_region_h(c->tb_cfg, k);
+          const int cfg = k >= 3 ? c->tb_cfg_long : c->tb_cfg;
+          const int rh = tb_region_h(cfg, k);
           t.out_h = rh - 2 * k;
           blocks = t.tiles_x * ((lh + t.out_h - 1) / t.out_h);
           if (blocks > c->partials_cap)
@@ -570,7 +588,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   else                                                                                         \
     hipLaunchKernelGGL((k_iterate_tb<false, RH, NG, PX>), dim3(blocks),                        \
                        dim3((64 / PX) * RH / NG), 0, st, t);
-          switch (c->tb_cfg) {
+          switch (cfg) {
             case 1: TB_LAUNCH(32, 2, 4) break;
             case 2: TB_LAUNCH(64, 1, 4) break;
             case 3: TB_LAUNCH(32, 1, 2) break;
@@ -728,7 +746,9 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   }
   if (const char *m = getenv("TVL1_ROLL_SEG")) c->roll_seg = atoi(m);
   if (const char *m = getenv("TVL1_ROLL_LDS")) c->roll_lds = std::max(0, atoi(m));
-  if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = atoi(m);
+  if (const char *m = getenv("TVL1_ROLL_PX")) c->roll_px = atoi(m) == 1 ? 1 : 2;
+  if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = c->tb_cfg_long = atoi(m);
+  if (const char *m = getenv("TVL1_TB_CFG_LONG")) c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
   if (const char *m = getenv("TVL1_WARP_TH")) c->warp_th = atoi(m);
   if (const char *m = getenv("TVL1_SPECULATE")) c->speculate = atoi(m) != 0;
@@ -748,14 +768,13 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
         nb = 0;
       return nb * 4 * prop.multiProcessorCount;
     };
-    c->roll_slots[1][0] = slots((const void *)k_iterate_roll<false, 1>);
-    c->roll_slots[2][0] = slots((const void *)k_iterate_roll<false, 2>);
-    c->roll_slots[3][0] = slots((const void *)k_iterate_roll<false, 3>);
-    c->roll_slots[4][0] = slots((const void *)k_iterate_roll<false, 4>);
-    c->roll_slots[1][1] = slots((const void *)k_iterate_roll<true, 1>);
-    c->roll_slots[2][1] = slots((const void *)k_iterate_roll<true, 2>);
-    c->roll_slots[3][1] = slots((const void *)k_iterate_roll<true, 3>);
-    c->roll_slots[4][1] = slots((const void *)k_iterate_roll<true, 4>);
+#define ROLL_SLOTS(G, K, PX) \
+  c->roll_slots[K][G][PX] = slots((const void *)k_iterate_roll<G, K, PX>);
+    ROLL_SLOTS(false, 1, 1) ROLL_SLOTS(false, 2, 1) ROLL_SLOTS(false, 3, 1) ROLL_SLOTS(false, 4, 1)
+    ROLL_SLOTS(true, 1, 1) ROLL_SLOTS(true, 2, 1) ROLL_SLOTS(true, 3, 1) ROLL_SLOTS(true, 4, 1)
+    ROLL_SLOTS(false, 1, 2) ROLL_SLOTS(false, 2, 2) ROLL_SLOTS(false, 3, 2) ROLL_SLOTS(false, 4, 2)
+    ROLL_SLOTS(true, 1, 2) ROLL_SLOTS(true, 2, 2) ROLL_SLOTS(true, 3, 2) ROLL_SLOTS(true, 4, 2)
+#undef ROLL_SLOTS
     (void)hipGetLastError();
   }
   *out = c;

@@ -894,29 +894,31 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
 }
 
 // ---------------------------------------------------------------- K6+K8 wavefront pipeline
-// k_iterate_roll<G, K>: K consecutive primal-dual iterations in ONE streaming pass.  One
-// wavefront owns a 64-px column band of one row segment and walks down it, one row per
-// step; no LDS, no barriers.
+// k_iterate_roll<G, K, PX>: K consecutive primal-dual iterations in ONE streaming pass.
+// One wavefront owns a column band of 64*PX px (PX adjacent px per lane) of one row
+// segment and walks down it, one row per step; no LDS, no barriers.
 //
 // Dependencies of iteration n of a pass (Jacobi: reads n-1, writes n):
 //   u^n(y) <- u^{n-1}(y), p^{n-1}(y), p^{n-1}(x-1, y), p^{n-1}(y-1)      (estimateU)
 //   p^n(y) <- p^{n-1}(y), u^n(y), u^n(x+1, y), u^n(y+1)                    (estimateDual)
 // so once input row r is loaded, stage n computes u^n at row r-n+1 and p^n at row r-n.
-// Per stage the wave keeps the two newest u rows and p rows in registers (one px per
-// lane), plus the warp constants of the K newest input rows, and it stores u^K and p^K.
-// x neighbours are DPP wavefront shifts.  Every iteration invalidates one lane at each
-// band edge, so a band carries a K-px halo on both sides and stores its 64 - 2K interior
-// lanes; a segment starts K rows above its output rows (their p^{n-1}(y-1) is missing)
-// and reads K rows below them.  At the image border OpenCV's clamp / special divergence
-// forms apply and nothing is invalidated.  HBM per px and pass: 36 B x 64/(64-2K) x
-// (rows + 2K)/rows loaded, 24 B stored -- for any K.  Arithmetic is estimate_u_px /
-// dual_px, the same as the other iteration kernels (bit-identical results).
+// Per stage the wave keeps the two newest u rows and p rows in registers, plus the warp
+// constants of the K newest input rows, and it stores u^K and p^K.  x neighbours across
+// lanes are DPP wavefront shifts.  Every iteration invalidates one px at each band edge,
+// so a band carries a halo of K px (rounded up to whole lanes) on both sides and stores
+// its interior; a segment starts K rows above its output rows (their p^{n-1}(y-1) is
+// missing) and reads K rows below them.  At the image border OpenCV's clamp / special
+// divergence forms apply and nothing is invalidated.  HBM per px and pass: 36 B x
+// 64PX/(64PX - 2 halo) x (rows + 2K)/rows loaded, 24 B stored -- for any K.  The pass is
+// VALU-bound for K >= 3 (the halo is recomputed, so a small one matters) and HBM-bound for
+// K <= 2.  Arithmetic is estimate_u_px / dual_px, the same as the other iteration kernels
+// (bit-identical results).
 constexpr int kRollMax = 4;
 constexpr int kRollAhead = 2;   // input rows loaded ahead of the row entering the pipeline
 
 struct RollArgs {
   IterArgs it;
-  int bands;      // column bands per row: ceil(W / (64 - 2K))
+  int bands;      // column bands per row: ceil(W / (64 PX - 2 halo))
   int seg_rows;   // output rows per segment
   int waves;      // bands * segments
 };
@@ -938,147 +940,208 @@ __device__ __forceinline__ int xcd_chunk(int b, int n) {
   return x * q + imin(x, rem) + i;
 }
 
-template <bool G>
-struct RollIn {   // one input row at this lane
-  float wx, wy, rh, u1, u2, u3, p11, p12, p21, p22, p31, p32;
-};
-
 // Buffer access to a plane: scalar descriptor (base, size in bytes), the row in the
 // scalar offset, the lane's column as one 32-bit VGPR byte offset.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)bytes, 0x00020000);
 }
-__device__ __forceinline__ float bload(const float *p, unsigned bytes, unsigned voff, unsigned soff) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(plane_rsrc(p, bytes), (int)voff, (int)soff, 0));
-}
 constexpr unsigned kOOB = 0x7ffffff0u;   // byte offset beyond every plane: store dropped
 __device__ __forceinline__ void bstore(float *p, unsigned bytes, unsigned voff, unsigned soff, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
 }
+// PX consecutive floats of a plane (4- or 8-byte store)
+template <int PX>
+__device__ __forceinline__ void bstorev(float *p, unsigned bytes, unsigned voff, const float (&v)[PX]) {
+  if constexpr (PX == 1) {
+    bstore(p, bytes, voff, 0, v[0]);
+  } else {
+    using T = decltype(__builtin_amdgcn_raw_buffer_load_b64(plane_rsrc(p, bytes), 0, 0, 0));
+    T t;
+    __builtin_memcpy(&t, v, 8);
+    __builtin_amdgcn_raw_buffer_store_b64(t, plane_rsrc(p, bytes), (int)voff, 0, 0);
+  }
+}
+// PX consecutive floats of a plane (4- or 8-byte load)
+template <int PX>
+__device__ __forceinline__ void bload(float (&d)[PX], const float *p, unsigned bytes, unsigned voff,
+                                      unsigned soff) {
+  if constexpr (PX == 1) {
+    d[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(plane_rsrc(p, bytes), (int)voff, (int)soff, 0));
+  } else {
+    static_assert(PX == 2, "1 or 2 px per lane");
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
+    static_assert(sizeof(v) == 8, "b64 load");
+    __builtin_memcpy(d, &v, 8);
+  }
+}
+
+template <bool G, int PX>
+struct RollIn {   // one input row at this lane's PX px
+  float wx[PX], wy[PX], rh[PX], u1[PX], u2[PX], u3[PX];
+  float p11[PX], p12[PX], p21[PX], p22[PX], p31[PX], p32[PX];
+};
 
 // p is loaded unconditionally and zeroed by a select when p == 0 (first pass of a level):
 // a branch here would make the compiler's wait counts conservative for every row.
-template <bool G>
-__device__ __forceinline__ void roll_load(RollIn<G> &v, const IterArgs &a, unsigned nb,
+template <bool G, int PX>
+__device__ __forceinline__ void roll_load(RollIn<G, PX> &v, const IterArgs &a, unsigned nb,
                                           unsigned soff, unsigned voff) {
-  v.wx = bload(a.I1wx, nb, voff, soff);
-  v.wy = bload(a.I1wy, nb, voff, soff);
-  v.rh = bload(a.rho, nb, voff, soff);
-  v.u1 = bload(a.u1s, nb, voff, soff);
-  v.u2 = bload(a.u2s, nb, voff, soff);
-  v.u3 = G ? bload(a.u3s, nb, voff, soff) : 0.0f;
-  v.p11 = bload(a.p11s, nb, voff, soff);
-  v.p12 = bload(a.p12s, nb, voff, soff);
-  v.p21 = bload(a.p21s, nb, voff, soff);
-  v.p22 = bload(a.p22s, nb, voff, soff);
-  v.p31 = G ? bload(a.p31s, nb, voff, soff) : 0.0f;
-  v.p32 = G ? bload(a.p32s, nb, voff, soff) : 0.0f;
+  bload<PX>(v.wx, a.I1wx, nb, voff, soff);
+  bload<PX>(v.wy, a.I1wy, nb, voff, soff);
+  bload<PX>(v.rh, a.rho, nb, voff, soff);
+  bload<PX>(v.u1, a.u1s, nb, voff, soff);
+  bload<PX>(v.u2, a.u2s, nb, voff, soff);
+  if (G) bload<PX>(v.u3, a.u3s, nb, voff, soff);
+  bload<PX>(v.p11, a.p11s, nb, voff, soff);
+  bload<PX>(v.p12, a.p12s, nb, voff, soff);
+  bload<PX>(v.p21, a.p21s, nb, voff, soff);
+  bload<PX>(v.p22, a.p22s, nb, voff, soff);
+  if (G) {
+    bload<PX>(v.p31, a.p31s, nb, voff, soff);
+    bload<PX>(v.p32, a.p32s, nb, voff, soff);
+  }
 }
 
-template <bool G>
-__device__ __forceinline__ void roll_pzero(RollIn<G> &v, bool z) {
-  v.p11 = z ? 0.0f : v.p11;
-  v.p12 = z ? 0.0f : v.p12;
-  v.p21 = z ? 0.0f : v.p21;
-  v.p22 = z ? 0.0f : v.p22;
-  v.p31 = z ? 0.0f : v.p31;
-  v.p32 = z ? 0.0f : v.p32;
+// Pipeline registers (see k_iterate_roll).  Index [n][j]: stage n, px j of the lane.
+template <bool G, int K, int PX>
+struct RollPipe {
+  float U1c[K + 1][PX], U2c[K + 1][PX], U3c[K + 1][PX];   // u^n(r-n+1)
+  float U1p[K + 1][PX], U2p[K + 1][PX], U3p[K + 1][PX];   // u^n(r-n); [0] = input u(r)
+  float P11c[K + 1][PX], P12c[K + 1][PX], P21c[K + 1][PX], P22c[K + 1][PX];   // p^n(r-n)
+  float P31c[K + 1][PX], P32c[K + 1][PX];                                     // [0] = input p(r)
+  float P11p[K + 1][PX], P12p[K + 1][PX], P21p[K + 1][PX], P22p[K + 1][PX];   // p^n(r-n-1)
+  float P31p[K + 1][PX], P32p[K + 1][PX];
+  float CX[K][PX], CY[K][PX], CR[K][PX];   // warp constants of input rows r, r-1, ...
+};
+
+// Lane geometry of a band: lane l holds px X + j, X = X0 + PX*l.
+struct RollLane {
+  int X;             // first px of the lane
+  unsigned vload;    // byte offset of the (clamped) load column
+  unsigned vst;      // byte offset of the lane's store column (out lanes only)
+  bool out;          // lane is in the band interior and its first px inside the image
+                     // (a second px at x = W lands in the row's pitch padding, which no
+                     // in-image px ever reads)
+  int ys, ye;        // output rows of the segment
+};
+
+// x neighbours of px j of the lane: left = px j-1 (previous lane's last px for j = 0),
+// right = px j+1 (next lane's first px for the last px).
+template <int PX>
+__device__ __forceinline__ float left_of(const float (&v)[PX], int j) {
+  return j == 0 ? from_left(v[PX - 1]) : v[j - 1];
+}
+template <int PX>
+__device__ __forceinline__ float right_of(const float (&v)[PX], int j) {
+  return j == PX - 1 ? from_right(v[0]) : v[j + 1];
 }
 
 // One step of the pipeline: input row r (in `in`) enters stage 0, every stage advances
 // one row, and input row r + kRollAhead is loaded into `ahead` (a ring of kRollAhead + 1
-// rows, so no register holding a load in flight is ever copied).  Every load and store is issued
-// unconditionally (rows clamped; masked stores use an out-of-range offset, which the
-// buffer unit drops), so the compiler can keep this step's stores and the next row's
-// loads in flight with counted waits.  Stages run every step: before a segment's first
-// rows reach them and past the image bottom they compute values that no stored cell
-// depends on (see the dependency list above; the border forms select, never combine).
-template <bool G, int K>
-struct RollPipe {
-  float U1c[K + 1], U2c[K + 1], U3c[K + 1], U1p[K + 1], U2p[K + 1], U3p[K + 1];
-  float P11c[K + 1], P12c[K + 1], P21c[K + 1], P22c[K + 1], P31c[K + 1], P32c[K + 1];
-  float P11p[K + 1], P12p[K + 1], P21p[K + 1], P22p[K + 1], P31p[K + 1], P32p[K + 1];
-  float CX[K], CY[K], CR[K];   // warp constants of input rows r, r-1, ...
-};
-
-template <bool G, int K>
-__device__ __forceinline__ void roll_step(RollPipe<G, K> &S, const RollIn<G> &in, RollIn<G> &ahead,
-                                          const IterArgs &a, int r, int X, unsigned Xc,
-                                          unsigned Xs, unsigned nb, unsigned rowb, bool out_col,
-                                          bool has_right, int ys, int ye, double &acc) {
-  roll_load<G>(ahead, a, nb, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, Xc);
+// rows, so no register holding a load in flight is ever copied).  Every load and store is
+// issued unconditionally (rows clamped; masked stores use an out-of-range offset, which
+// the buffer unit drops), so the compiler keeps this step's stores and the younger loads
+// in flight with counted waits.  Stages run every step: before a segment's first rows
+// reach them and past the image bottom they compute values no stored cell depends on (see
+// the dependency list above; the border forms select, never combine).
+template <bool G, int K, int PX>
+__device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
+                                          RollIn<G, PX> &ahead, const IterArgs &a, int r,
+                                          const RollLane &L, unsigned nb, unsigned rowb,
+                                          double &acc) {
+  roll_load<G, PX>(ahead, a, nb, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vload);
   // keep the loads of row r + kRollAhead ahead of this step's stores: waiting for them
   // kRollAhead steps later then leaves the younger stores and loads in flight (vmcnt
   // counts in issue order)
   __builtin_amdgcn_sched_barrier(0);
-  // shift every stage one row down
 #pragma unroll
-  for (int n = K; n >= 1; --n) {
-    S.U1p[n] = S.U1c[n]; S.U2p[n] = S.U2c[n]; if (G) S.U3p[n] = S.U3c[n];
+  for (int j = 0; j < PX; ++j) {
+    // shift every stage one row down
+#pragma unroll
+    for (int n = K; n >= 1; --n) {
+      S.U1p[n][j] = S.U1c[n][j]; S.U2p[n][j] = S.U2c[n][j]; if (G) S.U3p[n][j] = S.U3c[n][j];
+    }
+#pragma unroll
+    for (int n = K - 1; n >= 0; --n) {
+      S.P11p[n][j] = S.P11c[n][j]; S.P12p[n][j] = S.P12c[n][j];
+      S.P21p[n][j] = S.P21c[n][j]; S.P22p[n][j] = S.P22c[n][j];
+      if (G) { S.P31p[n][j] = S.P31c[n][j]; S.P32p[n][j] = S.P32c[n][j]; }
+    }
+#pragma unroll
+    for (int n = K - 1; n >= 1; --n) {
+      S.CX[n][j] = S.CX[n - 1][j]; S.CY[n][j] = S.CY[n - 1][j]; S.CR[n][j] = S.CR[n - 1][j];
+    }
+    const bool z = a.p_zero;
+    S.CX[0][j] = in.wx[j]; S.CY[0][j] = in.wy[j]; S.CR[0][j] = in.rh[j];
+    S.U1p[0][j] = in.u1[j]; S.U2p[0][j] = in.u2[j]; S.U3p[0][j] = G ? in.u3[j] : 0.0f;
+    S.P11c[0][j] = z ? 0.0f : in.p11[j]; S.P12c[0][j] = z ? 0.0f : in.p12[j];
+    S.P21c[0][j] = z ? 0.0f : in.p21[j]; S.P22c[0][j] = z ? 0.0f : in.p22[j];
+    S.P31c[0][j] = (z || !G) ? 0.0f : in.p31[j]; S.P32c[0][j] = (z || !G) ? 0.0f : in.p32[j];
   }
-#pragma unroll
-  for (int n = K - 1; n >= 0; --n) {
-    S.P11p[n] = S.P11c[n]; S.P12p[n] = S.P12c[n]; S.P21p[n] = S.P21c[n]; S.P22p[n] = S.P22c[n];
-    if (G) { S.P31p[n] = S.P31c[n]; S.P32p[n] = S.P32c[n]; }
-  }
-#pragma unroll
-  for (int n = K - 1; n >= 1; --n) { S.CX[n] = S.CX[n - 1]; S.CY[n] = S.CY[n - 1]; S.CR[n] = S.CR[n - 1]; }
-  RollIn<G> v = in;
-  roll_pzero<G>(v, a.p_zero);
-  S.CX[0] = v.wx; S.CY[0] = v.wy; S.CR[0] = v.rh;
-  S.U1p[0] = v.u1; S.U2p[0] = v.u2; S.U3p[0] = v.u3;
-  S.P11c[0] = v.p11; S.P12c[0] = v.p12; S.P21c[0] = v.p21; S.P22c[0] = v.p22;
-  S.P31c[0] = v.p31; S.P32c[0] = v.p32;
 
 #pragma unroll
   for (int n = 1; n <= K; ++n) {
     const int yU = r - n + 1;    // estimateU row of stage n
-    float n1, n2, n3 = 0.0f;
-    estimate_u_px<G>(S.CX[n - 1], S.CY[n - 1], S.CR[n - 1], S.U1p[n - 1], S.U2p[n - 1],
-                     S.U3p[n - 1], S.P11c[n - 1], from_left(S.P11c[n - 1]), S.P12c[n - 1],
-                     S.P12p[n - 1], S.P21c[n - 1], from_left(S.P21c[n - 1]), S.P22c[n - 1],
-                     S.P22p[n - 1], S.P31c[n - 1], G ? from_left(S.P31c[n - 1]) : 0.0f,
-                     S.P32c[n - 1], S.P32p[n - 1], X, yU, a, n1, n2, n3);
-    if (n == K) {
-      const bool st = out_col && yU >= ys && yU < ye;
-      if (a.calc_err) {
-        const float f1 = (S.U1p[n - 1] - n1) * (S.U1p[n - 1] - n1);
-        const float f2 = (S.U2p[n - 1] - n2) * (S.U2p[n - 1] - n2);
-        acc += st ? (double)(f1 + f2) : 0.0;
+    const bool stU = L.out && yU >= L.ys && yU < L.ye;
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      float n1, n2, n3 = 0.0f;
+      estimate_u_px<G>(S.CX[n - 1][j], S.CY[n - 1][j], S.CR[n - 1][j], S.U1p[n - 1][j],
+                       S.U2p[n - 1][j], S.U3p[n - 1][j], S.P11c[n - 1][j],
+                       left_of<PX>(S.P11c[n - 1], j), S.P12c[n - 1][j], S.P12p[n - 1][j],
+                       S.P21c[n - 1][j], left_of<PX>(S.P21c[n - 1], j), S.P22c[n - 1][j],
+                       S.P22p[n - 1][j], S.P31c[n - 1][j],
+                       G ? left_of<PX>(S.P31c[n - 1], j) : 0.0f, S.P32c[n - 1][j],
+                       S.P32p[n - 1][j], L.X + j, yU, a, n1, n2, n3);
+      if (n == K && a.calc_err) {
+        const float f1 = (S.U1p[n - 1][j] - n1) * (S.U1p[n - 1][j] - n1);
+        const float f2 = (S.U2p[n - 1][j] - n2) * (S.U2p[n - 1][j] - n2);
+        acc += stU && L.X + j < a.W ? (double)(f1 + f2) : 0.0;
       }
-      const unsigned vo = st ? (unsigned)yU * rowb + Xs : kOOB;
-      bstore(a.u1d, nb, vo, 0, n1);
-      bstore(a.u2d, nb, vo, 0, n2);
-      if (G) bstore(a.u3d, nb, vo, 0, n3);
+      S.U1c[n][j] = n1; S.U2c[n][j] = n2; if (G) S.U3c[n][j] = n3;
     }
-    S.U1c[n] = n1; S.U2c[n] = n2; if (G) S.U3c[n] = n3;
+    if (n == K) {
+      const unsigned vo = stU ? (unsigned)yU * rowb + L.vst : kOOB;
+      bstorev<PX>(a.u1d, nb, vo, S.U1c[n]);
+      bstorev<PX>(a.u2d, nb, vo, S.U2c[n]);
+      if (G) bstorev<PX>(a.u3d, nb, vo, S.U3c[n]);
+    }
 
     const int yD = r - n;        // estimateDualVariables row of stage n
     const bool has_down = yD + 1 < a.H;
-    dual_px(S.U1p[n], from_right(S.U1p[n]), S.U1c[n], has_right, has_down, a.taut, S.P11p[n - 1],
-            S.P12p[n - 1], S.P11c[n], S.P12c[n]);
-    dual_px(S.U2p[n], from_right(S.U2p[n]), S.U2c[n], has_right, has_down, a.taut, S.P21p[n - 1],
-            S.P22p[n - 1], S.P21c[n], S.P22c[n]);
-    if (G)
-      dual_px(S.U3p[n], from_right(S.U3p[n]), S.U3c[n], has_right, has_down, a.taut,
-              S.P31p[n - 1], S.P32p[n - 1], S.P31c[n], S.P32c[n]);
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      const bool has_right = L.X + j + 1 < a.W;
+      dual_px(S.U1p[n][j], right_of<PX>(S.U1p[n], j), S.U1c[n][j], has_right, has_down, a.taut,
+              S.P11p[n - 1][j], S.P12p[n - 1][j], S.P11c[n][j], S.P12c[n][j]);
+      dual_px(S.U2p[n][j], right_of<PX>(S.U2p[n], j), S.U2c[n][j], has_right, has_down, a.taut,
+              S.P21p[n - 1][j], S.P22p[n - 1][j], S.P21c[n][j], S.P22c[n][j]);
+      if (G)
+        dual_px(S.U3p[n][j], right_of<PX>(S.U3p[n], j), S.U3c[n][j], has_right, has_down,
+                a.taut, S.P31p[n - 1][j], S.P32p[n - 1][j], S.P31c[n][j], S.P32c[n][j]);
+    }
     if (n == K) {
-      const bool st = out_col && yD >= ys && yD < ye;
-      const unsigned vo = st ? (unsigned)yD * rowb + Xs : kOOB;
-      bstore(a.p11d, nb, vo, 0, S.P11c[n]);
-      bstore(a.p12d, nb, vo, 0, S.P12c[n]);
-      bstore(a.p21d, nb, vo, 0, S.P21c[n]);
-      bstore(a.p22d, nb, vo, 0, S.P22c[n]);
+      const unsigned vo = L.out && yD >= L.ys && yD < L.ye ? (unsigned)yD * rowb + L.vst : kOOB;
+      bstorev<PX>(a.p11d, nb, vo, S.P11c[n]);
+      bstorev<PX>(a.p12d, nb, vo, S.P12c[n]);
+      bstorev<PX>(a.p21d, nb, vo, S.P21c[n]);
+      bstorev<PX>(a.p22d, nb, vo, S.P22c[n]);
       if (G) {
-        bstore(a.p31d, nb, vo, 0, S.P31c[n]);
-        bstore(a.p32d, nb, vo, 0, S.P32c[n]);
+        bstorev<PX>(a.p31d, nb, vo, S.P31c[n]);
+        bstorev<PX>(a.p32d, nb, vo, S.P32c[n]);
       }
     }
   }
 }
 
-template <bool G, int K>
+// halo of a band: K px, rounded up to whole lanes' worth of px (8-byte aligned loads)
+template <int K, int PX>
+constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
+
+template <bool G, int K, int PX>
 __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
+  constexpr int HALO = roll_halo<K, PX>();
+  constexpr int BW = 64 * PX;            // band width (px)
   const IterArgs &a = ra.it;
   const int lane = threadIdx.x & 63;
   // wave-uniform (scalar) band / segment
@@ -1086,56 +1149,66 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
   if (wid >= ra.waves) return;                       // whole wavefronts only
   const int band = wid % ra.bands, seg = wid / ra.bands;
-  const int X = band * (64 - 2 * K) - K + lane;
-  const unsigned Xc = 4u * imin(imax(X, 0), a.W - 1);  // byte offset of the clamped load column
-  const unsigned Xs = 4u * imax(X, 0);                  // store column (out_col only)
+  RollLane L;
+  L.X = band * (BW - 2 * HALO) - HALO + PX * lane;
+  // load column: clamped so all PX px lie in the row's pitch (px >= W are never used by
+  // a px < W: the right clamp and the x = 0 divergence form select)
+  L.vload = 4u * imin(imax(L.X, 0), a.P - PX);
+  L.out = PX * lane >= HALO && PX * lane < BW - HALO && L.X < a.W;
+  L.vst = 4u * (unsigned)imax(L.X, 0);
   const unsigned nb = 4u * (unsigned)a.P * (unsigned)a.H;   // plane bytes
   const unsigned rowb = 4u * (unsigned)a.P;                 // row pitch in bytes
-  const bool out_col = lane >= K && lane < 64 - K && X < a.W;
-  const bool has_right = X + 1 < a.W;
-  const int ys = seg * ra.seg_rows, ye = imin(ys + ra.seg_rows, a.H);
-  const int r0 = imax(ys - K, 0);
+  L.ys = seg * ra.seg_rows;
+  L.ye = imin(L.ys + ra.seg_rows, a.H);
+  const int r0 = imax(L.ys - K, 0);
   // steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K (rows >= H drain the pipeline)
-  const int thirds = (ye + K - r0 + 2) / 3;
+  const int thirds = (L.ye + K - r0 + 2) / 3;
 
-  RollPipe<G, K> S;
+  RollPipe<G, K, PX> S;
 #pragma unroll
-  for (int n = 0; n <= K; ++n) {
-    S.U1c[n] = S.U2c[n] = S.U3c[n] = S.U1p[n] = S.U2p[n] = S.U3p[n] = 0.0f;
-    S.P11c[n] = S.P12c[n] = S.P21c[n] = S.P22c[n] = S.P31c[n] = S.P32c[n] = 0.0f;
-    S.P11p[n] = S.P12p[n] = S.P21p[n] = S.P22p[n] = S.P31p[n] = S.P32p[n] = 0.0f;
-  }
+  for (int n = 0; n <= K; ++n)
 #pragma unroll
-  for (int n = 0; n < K; ++n) S.CX[n] = S.CY[n] = S.CR[n] = 0.0f;
+    for (int j = 0; j < PX; ++j) {
+      S.U1c[n][j] = S.U2c[n][j] = S.U3c[n][j] = S.U1p[n][j] = S.U2p[n][j] = S.U3p[n][j] = 0.0f;
+      S.P11c[n][j] = S.P12c[n][j] = S.P21c[n][j] = S.P22c[n][j] = S.P31c[n][j] = S.P32c[n][j] = 0.0f;
+      S.P11p[n][j] = S.P12p[n][j] = S.P21p[n][j] = S.P22p[n][j] = S.P31p[n][j] = S.P32p[n][j] = 0.0f;
+    }
+#pragma unroll
+  for (int n = 0; n < K; ++n)
+#pragma unroll
+    for (int j = 0; j < PX; ++j) S.CX[n][j] = S.CY[n][j] = S.CR[n][j] = 0.0f;
 
   // Each prologue row load is followed by dropped (out-of-range) stores, as many as a
   // step issues: the loop is then entered with the same memory operations in flight as
   // its back edge carries, so the waits at the top of the loop are counted past the
   // younger stores and loads on both paths.
   auto dummy_stores = [&]() {
-    bstore(a.u1d, nb, kOOB, 0, 0.0f);
-    bstore(a.u2d, nb, kOOB, 0, 0.0f);
-    if (G) bstore(a.u3d, nb, kOOB, 0, 0.0f);
-    bstore(a.p11d, nb, kOOB, 0, 0.0f);
-    bstore(a.p12d, nb, kOOB, 0, 0.0f);
-    bstore(a.p21d, nb, kOOB, 0, 0.0f);
-    bstore(a.p22d, nb, kOOB, 0, 0.0f);
+    float z[PX];
+#pragma unroll
+    for (int j = 0; j < PX; ++j) z[j] = 0.0f;
+    bstorev<PX>(a.u1d, nb, kOOB, z);
+    bstorev<PX>(a.u2d, nb, kOOB, z);
+    if (G) bstorev<PX>(a.u3d, nb, kOOB, z);
+    bstorev<PX>(a.p11d, nb, kOOB, z);
+    bstorev<PX>(a.p12d, nb, kOOB, z);
+    bstorev<PX>(a.p21d, nb, kOOB, z);
+    bstorev<PX>(a.p22d, nb, kOOB, z);
     if (G) {
-      bstore(a.p31d, nb, kOOB, 0, 0.0f);
-      bstore(a.p32d, nb, kOOB, 0, 0.0f);
+      bstorev<PX>(a.p31d, nb, kOOB, z);
+      bstorev<PX>(a.p32d, nb, kOOB, z);
     }
   };
   static_assert(kRollAhead == 2, "the step loop below is unrolled for a 3-row ring");
-  RollIn<G> A, B, C;
-  roll_load<G>(A, a, nb, (unsigned)r0 * rowb, Xc);
+  RollIn<G, PX> A, B, C;
+  roll_load<G, PX>(A, a, nb, (unsigned)r0 * rowb, L.vload);
   dummy_stores();
-  roll_load<G>(B, a, nb, (unsigned)imin(r0 + 1, a.H - 1) * rowb, Xc);
+  roll_load<G, PX>(B, a, nb, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
   dummy_stores();
   double acc = 0.0;
   for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
-    roll_step<G, K>(S, A, C, a, r, X, Xc, Xs, nb, rowb, out_col, has_right, ys, ye, acc);
-    roll_step<G, K>(S, B, A, a, r + 1, X, Xc, Xs, nb, rowb, out_col, has_right, ys, ye, acc);
-    roll_step<G, K>(S, C, B, a, r + 2, X, Xc, Xs, nb, rowb, out_col, has_right, ys, ye, acc);
+    roll_step<G, K, PX>(S, A, C, a, r, L, nb, rowb, acc);
+    roll_step<G, K, PX>(S, B, A, a, r + 1, L, nb, rowb, acc);
+    roll_step<G, K, PX>(S, C, B, a, r + 2, L, nb, rowb, acc);
   }
   if (a.calc_err) {
 #pragma unroll

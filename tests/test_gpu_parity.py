@@ -75,16 +75,20 @@ def test_constant_images_give_zero_flow(engine):
 
 # Every kernel / schedule configuration must give the same bits (selected by env at
 # tvl1_create): TVL1_ITER_MODE=1 -> one iteration per launch (rolling-strip kernel),
-# TVL1_ITER_MODE=2 -> wavefront-pipelined passes (TVL1_ROLL_SEG rows per segment),
+# TVL1_ITER_MODE=2 -> wavefront-pipelined passes (TVL1_ROLL_SEG rows per segment,
+# TVL1_ROLL_PX px per lane), TVL1_ITER_MODE=3 -> hybrid (the default),
 # TVL1_TB_CFG = 0/1/2/3 -> temporally blocked regions 64x32/512thr, 64x32/256thr,
 # 64x64/1024thr, 2 px per lane; TVL1_WARP_MODE=1/0 -> global-memory gather / gradient
 # from I1 in LDS; TVL1_WARP_TH -> warp tile height; TVL1_SPECULATE=1 -> speculative
 # enqueueing at check iterations.
-MODES = ["TVL1_ITER_MODE=0", "TVL1_ITER_MODE=1", "TVL1_ITER_MODE=2", "TVL1_ITER_MODE=3", "TVL1_ITER_MODE=2,TVL1_ROLL_SEG=8",
-         "TVL1_ITER_MODE=2,TVL1_ROLL_SEG=64", "TVL1_TB_CFG=0", "TVL1_TB_CFG=1",
+MODES = ["TVL1_ITER_MODE=0", "TVL1_ITER_MODE=1", "TVL1_ITER_MODE=2", "TVL1_ITER_MODE=3",
+         "TVL1_ITER_MODE=2,TVL1_ROLL_SEG=8", "TVL1_ITER_MODE=2,TVL1_ROLL_SEG=64",
+         "TVL1_ITER_MODE=2,TVL1_ROLL_PX=1", "TVL1_ITER_MODE=2,TVL1_ROLL_PX=1,TVL1_ROLL_SEG=8",
+         "TVL1_ITER_MODE=0,TVL1_TB_CFG_LONG=0", "TVL1_TB_CFG=0", "TVL1_TB_CFG=1",
          "TVL1_TB_CFG=2", "TVL1_TB_CFG=3", "TVL1_WARP_TH=8", "TVL1_WARP_TH=32",
          "TVL1_WARP_MODE=1", "TVL1_WARP_MODE=0", "TVL1_SPECULATE=1"]
-KNOBS = ("TVL1_ITER_MODE", "TVL1_ROLL_SEG", "TVL1_ROLL_WAVES", "TVL1_TB_CFG", "TVL1_WARP_MODE",
+KNOBS = ("TVL1_ITER_MODE", "TVL1_ROLL_SEG", "TVL1_ROLL_PX", "TVL1_ROLL_LDS", "TVL1_TB_CFG",
+         "TVL1_TB_CFG_LONG", "TVL1_WARP_MODE",
          "TVL1_SPECULATE", "TVL1_WARP_TH")
 
 
