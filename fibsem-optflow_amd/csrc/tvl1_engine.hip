@@ -73,8 +73,12 @@ struct tvl1_ctx {
   int roll_px = 2;           // px per lane of k_iterate_roll (1 or 2)
   int roll_slots[kRollMax + 1][2][3] = {};   // resident k_iterate_roll<G, K, PX> wavefronts
   int roll_lds = 0;          // experiment: dummy dynamic LDS per k_iterate_roll block (bytes)
-  int warp_mode = 2;         // 2 = k_warp_lds (LDS-staged G window; fastest measured),
+  int warp_lds = 0;          // experiment: dummy dynamic LDS per k_warp_lds block (bytes)
+  int warp_margin = 6;       // k_warp_lds window margin (px): flows |u| < margin - 1 gather from LDS
+  int warp_mode = 3;         // 2 = k_warp_lds (LDS-staged G window per 64 x 16 tile),
+                             // 3 = k_warp_roll (streaming bands, LDS row ring),
                              // 0 = k_warp_img (gradient built in LDS from I1), 1 = k_warp (global)
+  int warp_roll_slots[8] = {};   // resident k_warp_roll<M> wavefronts per device, by margin M
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
   int warp_th = 16;          // k_warp_lds tile height (8, 16, 32)
   // k_iterate_tb shape (0 = 64x32/512 thr, 1 = 64x32/256 thr, 2 = 64x64/1024 thr,
@@ -400,18 +404,46 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       hipLaunchKernelGGL(k_warp_img, dim3(tx * ty), dim3(256), 0, st, c->I0s[s], c->I1s[s],
                          c->U[uset][0], c->U[uset][1], lw, lh, P, tx, c->C[cbuf][0],
                          c->C[cbuf][1], c->C[cbuf][2]);
+    } else if (c->warp_mode == 3) {
+      WarpRollArgs wa;
+      wa.I0 = c->I0s[s];
+      wa.G = c->G;
+      wa.u1 = c->U[uset][0];
+      wa.u2 = c->U[uset][1];
+      wa.I1wx = c->C[cbuf][0];
+      wa.I1wy = c->C[cbuf][1];
+      wa.rho = c->C[cbuf][2];
+      wa.W = lw;
+      wa.H = lh;
+      wa.P = P;
+      wa.bands = (lw + 63) / 64;
+      const int M = c->warp_margin == 4 ? 4 : c->warp_margin == 5 ? 5 : 6;
+      // every wavefront streams its rows + a 2M-row ring prologue
+      wa.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
+                                    : roll_segment(wa.bands, lh, M, c->warp_roll_slots[M]);
+      wa.waves = wa.bands * ((lh + wa.seg_rows - 1) / wa.seg_rows);
+      if (M == 4)
+        hipLaunchKernelGGL(k_warp_roll<4>, dim3(wa.waves), dim3(64), 0, st, wa);
+      else if (M == 5)
+        hipLaunchKernelGGL(k_warp_roll<5>, dim3(wa.waves), dim3(64), 0, st, wa);
+      else
+        hipLaunchKernelGGL(k_warp_roll<6>, dim3(wa.waves), dim3(64), 0, st, wa);
     } else if (c->warp_mode == 1) {
       hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[uset][0],
                          c->U[uset][1], lw, lh, P, c->C[cbuf][0], c->C[cbuf][1], c->C[cbuf][2]);
     } else {
-#define WARP_LDS(TH)                                                                            \
+#define WARP_LDS(TH, M)                                                                         \
   {                                                                                             \
     const int tx = (lw + kWarpTW - 1) / kWarpTW, ty = (lh + TH - 1) / TH;                       \
-    hipLaunchKernelGGL(k_warp_lds<TH>, dim3(tx * ty), dim3(256), 0, st, c->I0s[s], c->G,        \
-                       c->U[uset][0], c->U[uset][1], lw, lh, P, tx, c->C[cbuf][0],              \
-                       c->C[cbuf][1], c->C[cbuf][2]);                                           \
+    hipLaunchKernelGGL((k_warp_lds<TH, M>), dim3(tx * ty), dim3(256), c->warp_lds, st,          \
+                       c->I0s[s], c->G, c->U[uset][0], c->U[uset][1], lw, lh, P, tx,            \
+                       c->C[cbuf][0], c->C[cbuf][1], c->C[cbuf][2]);                            \
   }
-      if (c->warp_th == 8) WARP_LDS(8) else if (c->warp_th == 32) WARP_LDS(32) else WARP_LDS(16)
+      if (c->warp_th == 8) WARP_LDS(8, 6)
+      else if (c->warp_th == 32) WARP_LDS(32, 6)
+      else if (c->warp_margin == 4) WARP_LDS(16, 4)
+      else if (c->warp_margin == 5) WARP_LDS(16, 5)
+      else WARP_LDS(16, 6)
 #undef WARP_LDS
     }
     // algorithmic: 40 B/px per warp
@@ -747,6 +779,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_ROLL_SEG")) c->roll_seg = atoi(m);
   if (const char *m = getenv("TVL1_ROLL_LDS")) c->roll_lds = std::max(0, atoi(m));
   if (const char *m = getenv("TVL1_ROLL_PX")) c->roll_px = atoi(m) == 1 ? 1 : 2;
+  if (const char *m = getenv("TVL1_WARP_LDS")) c->warp_lds = std::max(0, atoi(m));
+  if (const char *m = getenv("TVL1_WARP_MARGIN")) c->warp_margin = atoi(m);
   if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_TB_CFG_LONG")) c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
@@ -775,6 +809,14 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     ROLL_SLOTS(false, 1, 2) ROLL_SLOTS(false, 2, 2) ROLL_SLOTS(false, 3, 2) ROLL_SLOTS(false, 4, 2)
     ROLL_SLOTS(true, 1, 2) ROLL_SLOTS(true, 2, 2) ROLL_SLOTS(true, 3, 2) ROLL_SLOTS(true, 4, 2)
 #undef ROLL_SLOTS
+    auto slots64 = [&](const void *fn) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64, 0) != hipSuccess) nb = 0;
+      return nb * prop.multiProcessorCount;
+    };
+    c->warp_roll_slots[4] = slots64((const void *)k_warp_roll<4>);
+    c->warp_roll_slots[5] = slots64((const void *)k_warp_roll<5>);
+    c->warp_roll_slots[6] = slots64((const void *)k_warp_roll<6>);
     (void)hipGetLastError();
   }
   *out = c;

@@ -55,6 +55,14 @@ __device__ __forceinline__ void tile_of_block(int bid, int nblocks, int tiles_x,
   bx = band * kBand + (in_band - by * width);
 }
 
+// XCD-contiguous block order: the blocks the hardware sends to one XCD (b % 8) get one
+// contiguous run of logical indices, so neighbouring bands share that XCD's L2.
+__device__ __forceinline__ int xcd_chunk(int b, int n) {
+  const int q = n / kXcds, rem = n % kXcds;
+  const int x = b % kXcds, i = b / kXcds;
+  return x * q + imin(x, rem) + i;
+}
+
 // ---------------------------------------------------------------- K1 convert
 // GpuMat::convertTo(CV_32F, 1.0) for both frames (blockIdx.z selects the frame).
 __global__ void k_convert_u8(const uint8_t *__restrict__ s0, size_t sp0,
@@ -216,10 +224,11 @@ __device__ __forceinline__ float cubic_out(float x) {
 // exactly 0.0f.  Summation order (rows outer, columns inner, ascending) and the
 // weight product cubic(wx-cx) * cubic(wy-cy) are unchanged, so the result is
 // bit-identical to the reference loop while being branch-free and unrollable.
-template <bool LDSPATH>
-__device__ __forceinline__ void warp_gather(const float4 *__restrict__ src, int sp, int ox, int oy,
-                                            int W, int H, float wx, float wy, int fx, int fy,
-                                            float &sum, float &sumx, float &sumy, float &wsum) {
+// The taps: row(cy) -> the row's float4 array, col(cx) -> its index in that row.
+template <class RowF, class ColF>
+__device__ __forceinline__ void warp_gather_taps(RowF row, ColF col, float wx, float wy, int fx,
+                                                 int fy, float &sum, float &sumx, float &sumy,
+                                                 float &wsum) {
   float kx[4], ky[4];
   kx[0] = cubic_out(wx - (float)(fx - 1));
   kx[1] = cubic_in(wx - (float)fx);
@@ -231,13 +240,10 @@ __device__ __forceinline__ void warp_gather(const float4 *__restrict__ src, int 
   ky[3] = cubic_out(wy - (float)(fy + 2));
   int cxs[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    cxs[i] = LDSPATH ? fx - 1 + i - ox : imin(imax(fx - 1 + i, 0), W - 1);
+  for (int i = 0; i < 4; ++i) cxs[i] = col(fx - 1 + i);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int cy = fy - 1 + j;
-    const int ry = LDSPATH ? cy - oy : imin(imax(cy, 0), H - 1);
-    const float4 *rowp = src + (size_t)ry * sp;
+    const float4 *rowp = row(fy - 1 + j);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float w = kx[i] * ky[j];
@@ -250,7 +256,17 @@ __device__ __forceinline__ void warp_gather(const float4 *__restrict__ src, int 
   }
 }
 
-template <int TH>
+template <bool LDSPATH>
+__device__ __forceinline__ void warp_gather(const float4 *__restrict__ src, int sp, int ox, int oy,
+                                            int W, int H, float wx, float wy, int fx, int fy,
+                                            float &sum, float &sumx, float &sumy, float &wsum) {
+  warp_gather_taps(
+      [&](int cy) { return src + (size_t)(LDSPATH ? cy - oy : imin(imax(cy, 0), H - 1)) * sp; },
+      [&](int cx) { return LDSPATH ? cx - ox : imin(imax(cx, 0), W - 1); }, wx, wy, fx, fy, sum,
+      sumx, sumy, wsum);
+}
+
+template <int TH, int M = kWarpHalo>
 __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
                                                   const float4 *__restrict__ G,
                                                   const float *__restrict__ u1,
@@ -258,12 +274,12 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
                                                   int P, int tiles_x, float *__restrict__ I1wx,
                                                   float *__restrict__ I1wy,
                                                   float *__restrict__ rho) {
-  constexpr int WH = TH + 2 * kWarpHalo;
-  __shared__ float4 win[WH * kWarpWW];
+  constexpr int WW = kWarpTW + 2 * M, WH = TH + 2 * M;   // window (margin M: |u| < M - 1 fits)
+  __shared__ float4 win[WH * WW];
   int bx, by;
   tile_of_block(blockIdx.x, gridDim.x, tiles_x, gridDim.x / tiles_x, bx, by);
   const int x0 = bx * kWarpTW, y0 = by * TH;
-  const int ox = x0 - kWarpHalo, oy = y0 - kWarpHalo;   // window origin (unclamped coords)
+  const int ox = x0 - M, oy = y0 - M;   // window origin (unclamped coords)
   // Issue this thread's own loads (u1, u2, I0 of its 4 rows) before the window fill so
   // their latency overlaps it.
   constexpr int R = TH / 4;
@@ -278,8 +294,8 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
     u2v[j] = u2[i];
     i0v[j] = I0[i];
   }
-  for (int i = threadIdx.x; i < WH * kWarpWW; i += 256) {
-    const int wy = i / kWarpWW, wx = i - wy * kWarpWW;
+  for (int i = threadIdx.x; i < WH * WW; i += 256) {
+    const int wy = i / WW, wx = i - wy * WW;
     const int cx = imin(imax(ox + wx, 0), W - 1);
     const int cy = imin(imax(oy + wy, 0), H - 1);
     win[i] = G[(size_t)cy * P + cx];
@@ -296,9 +312,9 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
     const int fx = tap_floor(wx);
     const int fy = tap_floor(wy);
     float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
-    const bool inwin = fx - 1 >= ox && fx + 2 < ox + kWarpWW && fy - 1 >= oy && fy + 2 < oy + WH;
+    const bool inwin = fx - 1 >= ox && fx + 2 < ox + WW && fy - 1 >= oy && fy + 2 < oy + WH;
     if (inwin)
-      warp_gather<true>(win, kWarpWW, ox, oy, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+      warp_gather<true>(win, WW, ox, oy, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
     else
       warp_gather<false>(G, P, 0, 0, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
     const float coeff = 1.0f / wsum;
@@ -308,6 +324,129 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
     I1wx[i] = I1wxv;
     I1wy[i] = I1wyv;
     rho[i] = I1wv - I1wxv * u1v[j] - I1wyv * u2v[j] - i0v[j];
+  }
+}
+
+// warpBackward, streaming: one wavefront owns a 64-px column band of a row segment and
+// walks down it, one output row per step (one px per lane), with no barriers.  Its LDS
+// holds a ring of kWarpRing rows of the (I1, I1x, I1y) window, (64 + 2M) columns wide
+// (clamped coordinates, exactly the texture-clamp values; ring row = image row & 15):
+// at step y the rows y-M .. y+M are resident, so a px whose taps stay within M - 1 px of
+// it gathers from LDS; any other px takes the global-memory path (same taps, same order).
+// G rows are loaded kWarpAhead rows ahead into registers and written to the ring when
+// they are needed, u1 / u2 / I0 likewise, so the step's loads are in flight while earlier
+// rows compute; a row of G is read from HBM once per band (x 1 + 2M/64).  The ring and
+// the register rings are unrolled (kWarpAhead + 1 steps per loop trip), so no register
+// holding a load in flight is copied.
+constexpr int kWarpRing = 16, kWarpAhead = 2;
+
+struct WarpRollArgs {
+  const float *I0;
+  const float4 *G;
+  const float *u1, *u2;
+  float *I1wx, *I1wy, *rho;
+  int W, H, P;
+  int bands, seg_rows, waves;
+};
+
+typedef float vf4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
+
+template <int M>
+struct WarpRow {   // this lane's share of window row y + M (2 slots) and of flow row y
+  vf4 g0, g1;
+  float u1, u2, i0;
+};
+
+template <int M>
+__device__ __forceinline__ void warp_row_load(WarpRow<M> &v, const WarpRollArgs &a, int y, int xg0,
+                                              int xg1, int xc) {
+  const vf4 *Gr = reinterpret_cast<const vf4 *>(a.G) + (size_t)imin(imax(y + M, 0), a.H - 1) * a.P;
+  v.g0 = Gr[xg0];
+  v.g1 = Gr[xg1];
+  const size_t o = (size_t)imin(y, a.H - 1) * a.P + xc;
+  v.u1 = a.u1[o];
+  v.u2 = a.u2[o];
+  v.i0 = a.I0[o];
+}
+
+template <int M>
+__device__ __forceinline__ void warp_roll_step(float4 *__restrict__ ring, const WarpRow<M> &cur,
+                                               WarpRow<M> &ahead, const WarpRollArgs &a, int y,
+                                               int ye, int lane, int x0, int xg0, int xg1, int xc) {
+  constexpr int WW = 64 + 2 * M;
+  // loads for step y + A: window row y + A + M, flow row y + A (in flight for A steps)
+  warp_row_load<M>(ahead, a, y + kWarpAhead, xg0, xg1, xc);
+  __builtin_amdgcn_sched_barrier(0);
+  // window row y + M enters the ring (it replaces row y + M - 16 < y - M); a wave's LDS
+  // accesses execute in order, so this step's gathers see it
+  vf4 *dst = reinterpret_cast<vf4 *>(ring) + ((y + M) & (kWarpRing - 1)) * WW;
+  dst[lane] = cur.g0;
+  if (lane < 2 * M) dst[64 + lane] = cur.g1;
+  const int x = x0 + lane;
+  const float wx = (float)x + cur.u1;
+  const float wy = (float)y + cur.u2;
+  const int fx = tap_floor(wx);
+  const int fy = tap_floor(wy);
+  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
+  const bool inwin = fx - 1 >= x0 - M && fx + 2 < x0 + 64 + M && fy - 1 >= y - M && fy + 2 <= y + M;
+  if (inwin)
+    warp_gather_taps([&](int cy) { return ring + (cy & (kWarpRing - 1)) * WW; },
+                     [&](int cx) { return cx - (x0 - M); }, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+  else
+    warp_gather<false>(a.G, a.P, 0, 0, a.W, a.H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+  const float coeff = 1.0f / wsum;
+  const float I1wv = sum * coeff;
+  const float I1wxv = sumx * coeff;
+  const float I1wyv = sumy * coeff;
+  if (x < a.W && y < ye) {
+    const size_t o = (size_t)y * a.P + x;
+    a.I1wx[o] = I1wxv;
+    a.I1wy[o] = I1wyv;
+    a.rho[o] = I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0;
+  }
+}
+
+template <int M>
+__global__ __launch_bounds__(64) void k_warp_roll(WarpRollArgs a) {
+  constexpr int WW = 64 + 2 * M;
+  static_assert(2 * M + 1 + kWarpAhead <= kWarpRing, "ring too small for the margin");
+  static_assert(2 * M <= 64, "second window slot per lane");
+  __shared__ float4 ring[kWarpRing * WW];
+  const int lane = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
+  if (wid >= a.waves) return;
+  const int band = wid % a.bands, seg = wid / a.bands;
+  const int x0 = band * 64;
+  const int xg0 = imin(imax(x0 - M + lane, 0), a.W - 1);        // window slot lane
+  const int xg1 = imin(imax(x0 - M + 64 + lane, 0), a.W - 1);   // window slot 64 + lane
+  const int xc = imin(x0 + lane, a.W - 1);
+  const int ys = seg * a.seg_rows, ye = imin(ys + a.seg_rows, a.H);
+  // ring prologue: window rows ys - M .. ys + M - 1 (row ys + M enters at step ys); all
+  // loads are issued before the first write, so the prologue costs one memory latency
+  {
+    vf4 t0[2 * M], t1[2 * M];
+#pragma unroll
+    for (int i = 0; i < 2 * M; ++i) {
+      const vf4 *Gr = reinterpret_cast<const vf4 *>(a.G) +
+                      (size_t)imin(imax(ys - M + i, 0), a.H - 1) * a.P;
+      t0[i] = Gr[xg0];
+      t1[i] = Gr[xg1];
+    }
+#pragma unroll
+    for (int i = 0; i < 2 * M; ++i) {
+      vf4 *dst = reinterpret_cast<vf4 *>(ring) + ((ys - M + i) & (kWarpRing - 1)) * WW;
+      dst[lane] = t0[i];
+      if (lane < 2 * M) dst[64 + lane] = t1[i];
+    }
+  }
+  static_assert(kWarpAhead == 2, "the step loop below is unrolled for a 3-row ring");
+  WarpRow<M> A, B, C;
+  warp_row_load<M>(A, a, ys, xg0, xg1, xc);
+  warp_row_load<M>(B, a, ys + 1, xg0, xg1, xc);
+  for (int y = ys; y < ye; y += 3) {
+    warp_roll_step<M>(ring, A, C, a, y, ye, lane, x0, xg0, xg1, xc);
+    warp_roll_step<M>(ring, B, A, a, y + 1, ye, lane, x0, xg0, xg1, xc);
+    warp_roll_step<M>(ring, C, B, a, y + 2, ye, lane, x0, xg0, xg1, xc);
   }
 }
 
@@ -930,14 +1069,6 @@ __device__ __forceinline__ float from_left(float v) {
 // lane i <- lane i+1 (DPP wave_shl:1; lane 63 gets 0)
 __device__ __forceinline__ float from_right(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
-}
-
-// XCD-contiguous block order: the blocks the hardware sends to one XCD (b % 8) get one
-// contiguous run of logical indices, so neighbouring bands share that XCD's L2.
-__device__ __forceinline__ int xcd_chunk(int b, int n) {
-  const int q = n / kXcds, rem = n % kXcds;
-  const int x = b % kXcds, i = b / kXcds;
-  return x * q + imin(x, rem) + i;
 }
 
 // Buffer access to a plane: scalar descriptor (base, size in bytes), the row in the

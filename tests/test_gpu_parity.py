@@ -86,10 +86,12 @@ MODES = ["TVL1_ITER_MODE=0", "TVL1_ITER_MODE=1", "TVL1_ITER_MODE=2", "TVL1_ITER_
          "TVL1_ITER_MODE=2,TVL1_ROLL_PX=1", "TVL1_ITER_MODE=2,TVL1_ROLL_PX=1,TVL1_ROLL_SEG=8",
          "TVL1_ITER_MODE=0,TVL1_TB_CFG_LONG=0", "TVL1_TB_CFG=0", "TVL1_TB_CFG=1",
          "TVL1_TB_CFG=2", "TVL1_TB_CFG=3", "TVL1_WARP_TH=8", "TVL1_WARP_TH=32",
-         "TVL1_WARP_MODE=1", "TVL1_WARP_MODE=0", "TVL1_SPECULATE=1"]
+         "TVL1_WARP_MODE=1", "TVL1_WARP_MODE=0", "TVL1_WARP_MODE=3",
+         "TVL1_WARP_MODE=3,TVL1_WARP_MARGIN=4", "TVL1_WARP_MODE=3,TVL1_ROLL_SEG=8",
+         "TVL1_WARP_MARGIN=4", "TVL1_SPECULATE=1"]
 KNOBS = ("TVL1_ITER_MODE", "TVL1_ROLL_SEG", "TVL1_ROLL_PX", "TVL1_ROLL_LDS", "TVL1_TB_CFG",
          "TVL1_TB_CFG_LONG", "TVL1_WARP_MODE",
-         "TVL1_SPECULATE", "TVL1_WARP_TH")
+         "TVL1_SPECULATE", "TVL1_WARP_TH", "TVL1_WARP_MARGIN", "TVL1_WARP_LDS")
 
 
 @pytest.mark.parametrize("env", MODES)
@@ -129,9 +131,16 @@ def test_engine_reproduces_golden(engine, path):
     assert bits_equal(u, g["u"]) and bits_equal(v, g["v"])
 
 
-def test_large_flow_uses_global_gather_fallback(engine):
-    """A ~7 px shift puts taps outside the warp kernel's LDS window (margin 4 px):
+@pytest.mark.parametrize("env", ["TVL1_WARP_MODE=2", "TVL1_WARP_MODE=3",
+                                 "TVL1_WARP_MODE=3,TVL1_WARP_MARGIN=4"])
+def test_large_flow_uses_global_gather_fallback(built, monkeypatch, env):
+    """A ~7 px shift puts taps outside the warp kernels' LDS windows (margin 4-6 px):
     the global-memory fallback must give the same bits."""
+    for k in KNOBS:
+        monkeypatch.delenv(k, raising=False)
+    for kv in env.split(","):
+        monkeypatch.setenv(*kv.split("="))
+    engine = capi.Engine(capi.make_params())
     from scipy import ndimage
     base = synth.base_texture(192, 160, seed=31)
     ys, xs = np.mgrid[0:160, 0:192].astype(np.float32)
@@ -141,6 +150,7 @@ def test_large_flow_uses_global_gather_fallback(engine):
     p = capi.make_params(nscales=4, warps=6)
     engine.set_params(p)
     u, v, st, wi = engine.calc_host(I0, I1)
+    engine.close()
     ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
     assert float(np.abs(ur).max()) > 5.0   # the case really leaves the window
     np.testing.assert_array_equal(wi, wr)
