@@ -75,10 +75,13 @@ struct tvl1_ctx {
   int roll_lds = 0;          // experiment: dummy dynamic LDS per k_iterate_roll block (bytes)
   int warp_lds = 0;          // experiment: dummy dynamic LDS per k_warp_lds block (bytes)
   int warp_margin = 6;       // k_warp_lds window margin (px): flows |u| < margin - 1 gather from LDS
-  int warp_mode = 3;         // 2 = k_warp_lds (LDS-staged G window per 64 x 16 tile),
-                             // 3 = k_warp_roll (streaming bands, LDS row ring),
+  int warp_mode = 4;         // 2 = k_warp_lds (LDS-staged G window per 64 x 16 tile),
+                             // 3 = k_warp_roll (streaming bands, LDS row ring of G),
+                             // 4 = k_warp_ring (streaming bands, ring built from I1; no G),
                              // 0 = k_warp_img (gradient built in LDS from I1), 1 = k_warp (global)
-  int warp_roll_slots[8] = {};   // resident k_warp_roll<M> wavefronts per device, by margin M
+  int warp_roll_slots[8][5] = {};   // resident k_warp_roll<M, NW> blocks per device
+  int warp_ring_slots[8][5] = {};   // resident k_warp_ring<M, NW> blocks per device
+  int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
   int warp_th = 16;          // k_warp_lds tile height (8, 16, 32)
   // k_iterate_tb shape (0 = 64x32/512 thr, 1 = 64x32/256 thr, 2 = 64x64/1024 thr,
@@ -388,7 +391,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
 
   // ---- launch helpers
   auto gradient = [&](int s) -> tvl1_status {  // interleaved G plane for warp modes 1, 2
-    if (c->warp_mode == 0) return TVL1_OK;     // k_warp_img derives it from I1 in LDS
+    if (c->warp_mode == 0 || c->warp_mode == 4) return TVL1_OK;   // derived from I1 in LDS
     const int lw = g.ws[s], lh = g.hs[s];
     size_t t0 = prof_begin(c, st);
     hipLaunchKernelGGL(k_gradient, grid2(lw, lh), kBlk2, 0, st, c->I1s[s], lw, lh, g.ps[s], c->G);
@@ -418,16 +421,49 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       wa.P = P;
       wa.bands = (lw + 63) / 64;
       const int M = c->warp_margin == 4 ? 4 : c->warp_margin == 5 ? 5 : 6;
-      // every wavefront streams its rows + a 2M-row ring prologue
+      const int NW = c->warp_nw == 1 ? 1 : c->warp_nw == 4 ? 4 : 2;
+      // every block streams its rows + a 2M-row ring prologue
       wa.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                    : roll_segment(wa.bands, lh, M, c->warp_roll_slots[M]);
+                                    : roll_segment(wa.bands, lh, M, c->warp_roll_slots[M][NW]);
       wa.waves = wa.bands * ((lh + wa.seg_rows - 1) / wa.seg_rows);
-      if (M == 4)
-        hipLaunchKernelGGL(k_warp_roll<4>, dim3(wa.waves), dim3(64), 0, st, wa);
-      else if (M == 5)
-        hipLaunchKernelGGL(k_warp_roll<5>, dim3(wa.waves), dim3(64), 0, st, wa);
-      else
-        hipLaunchKernelGGL(k_warp_roll<6>, dim3(wa.waves), dim3(64), 0, st, wa);
+#define WARP_ROLL(MM, NN)                                                                      \
+  hipLaunchKernelGGL((k_warp_roll<MM, NN>), dim3(wa.waves), dim3(64 * NN), c->warp_lds, st, wa);
+      if (M == 4) {
+        if (NW == 1) WARP_ROLL(4, 1) else if (NW == 4) WARP_ROLL(4, 4) else WARP_ROLL(4, 2)
+      } else if (M == 5) {
+        if (NW == 1) WARP_ROLL(5, 1) else if (NW == 4) WARP_ROLL(5, 4) else WARP_ROLL(5, 2)
+      } else {
+        if (NW == 1) WARP_ROLL(6, 1) else if (NW == 4) WARP_ROLL(6, 4) else WARP_ROLL(6, 2)
+      }
+#undef WARP_ROLL
+    } else if (c->warp_mode == 4) {
+      WarpRingArgs wa;
+      wa.I0 = c->I0s[s];
+      wa.I1 = c->I1s[s];
+      wa.u1 = c->U[uset][0];
+      wa.u2 = c->U[uset][1];
+      wa.I1wx = c->C[cbuf][0];
+      wa.I1wy = c->C[cbuf][1];
+      wa.rho = c->C[cbuf][2];
+      wa.W = lw;
+      wa.H = lh;
+      wa.P = P;
+      wa.bands = (lw + 63) / 64;
+      const int M = c->warp_margin == 4 ? 4 : c->warp_margin == 5 ? 5 : 6;
+      const int NW = c->warp_nw == 1 ? 1 : c->warp_nw == 4 ? 4 : 2;
+      wa.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
+                                    : roll_segment(wa.bands, lh, M, c->warp_ring_slots[M][NW]);
+      wa.waves = wa.bands * ((lh + wa.seg_rows - 1) / wa.seg_rows);
+#define WARP_RING(MM, NN)                                                                      \
+  hipLaunchKernelGGL((k_warp_ring<MM, NN>), dim3(wa.waves), dim3(64 * NN), c->warp_lds, st, wa);
+      if (M == 4) {
+        if (NW == 1) WARP_RING(4, 1) else if (NW == 4) WARP_RING(4, 4) else WARP_RING(4, 2)
+      } else if (M == 5) {
+        if (NW == 1) WARP_RING(5, 1) else if (NW == 4) WARP_RING(5, 4) else WARP_RING(5, 2)
+      } else {
+        if (NW == 1) WARP_RING(6, 1) else if (NW == 4) WARP_RING(6, 4) else WARP_RING(6, 2)
+      }
+#undef WARP_RING
     } else if (c->warp_mode == 1) {
       hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[uset][0],
                          c->U[uset][1], lw, lh, P, c->C[cbuf][0], c->C[cbuf][1], c->C[cbuf][2]);
@@ -448,7 +484,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     }
     // algorithmic: 40 B/px per warp
     prof_end(c, st, t0, 1, (double)lw * lh * 40.0,
-             (double)lw * lh * (c->warp_mode == 0 ? 28.0 : 40.0));
+             (double)lw * lh * (c->warp_mode == 0 || c->warp_mode == 4 ? 28.0 : 40.0));
     DIAG(c, st, "warp kernel", s, wp, -1);
     return TVL1_OK;
   };
@@ -781,6 +817,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_ROLL_PX")) c->roll_px = atoi(m) == 1 ? 1 : 2;
   if (const char *m = getenv("TVL1_WARP_LDS")) c->warp_lds = std::max(0, atoi(m));
   if (const char *m = getenv("TVL1_WARP_MARGIN")) c->warp_margin = atoi(m);
+  if (const char *m = getenv("TVL1_WARP_NW")) c->warp_nw = atoi(m);
   if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_TB_CFG_LONG")) c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
@@ -809,14 +846,24 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     ROLL_SLOTS(false, 1, 2) ROLL_SLOTS(false, 2, 2) ROLL_SLOTS(false, 3, 2) ROLL_SLOTS(false, 4, 2)
     ROLL_SLOTS(true, 1, 2) ROLL_SLOTS(true, 2, 2) ROLL_SLOTS(true, 3, 2) ROLL_SLOTS(true, 4, 2)
 #undef ROLL_SLOTS
-    auto slots64 = [&](const void *fn) {
+    auto blocks_of = [&](const void *fn, int threads) {
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64, 0) != hipSuccess) nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, c->warp_lds) != hipSuccess)
+        nb = 0;
       return nb * prop.multiProcessorCount;
     };
-    c->warp_roll_slots[4] = slots64((const void *)k_warp_roll<4>);
-    c->warp_roll_slots[5] = slots64((const void *)k_warp_roll<5>);
-    c->warp_roll_slots[6] = slots64((const void *)k_warp_roll<6>);
+#define WARP_SLOTS(MM, NN) \
+  c->warp_roll_slots[MM][NN] = blocks_of((const void *)k_warp_roll<MM, NN>, 64 * NN);
+    WARP_SLOTS(4, 1) WARP_SLOTS(4, 2) WARP_SLOTS(4, 4)
+    WARP_SLOTS(5, 1) WARP_SLOTS(5, 2) WARP_SLOTS(5, 4)
+    WARP_SLOTS(6, 1) WARP_SLOTS(6, 2) WARP_SLOTS(6, 4)
+#undef WARP_SLOTS
+#define RING_SLOTS(MM, NN) \
+  c->warp_ring_slots[MM][NN] = blocks_of((const void *)k_warp_ring<MM, NN>, 64 * NN);
+    RING_SLOTS(4, 1) RING_SLOTS(4, 2) RING_SLOTS(4, 4)
+    RING_SLOTS(5, 1) RING_SLOTS(5, 2) RING_SLOTS(5, 4)
+    RING_SLOTS(6, 1) RING_SLOTS(6, 2) RING_SLOTS(6, 4)
+#undef RING_SLOTS
     (void)hipGetLastError();
   }
   *out = c;

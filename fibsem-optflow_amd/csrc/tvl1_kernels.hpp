@@ -224,11 +224,13 @@ __device__ __forceinline__ float cubic_out(float x) {
 // exactly 0.0f.  Summation order (rows outer, columns inner, ascending) and the
 // weight product cubic(wx-cx) * cubic(wy-cy) are unchanged, so the result is
 // bit-identical to the reference loop while being branch-free and unrollable.
-// The taps: row(cy) -> the row's float4 array, col(cx) -> its index in that row.
-template <class RowF, class ColF>
-__device__ __forceinline__ void warp_gather_taps(RowF row, ColF col, float wx, float wy, int fx,
-                                                 int fy, float &sum, float &sumx, float &sumy,
-                                                 float &wsum) {
+// The 4x4 taps: tap(cy, cx) -> (I1, I1x, I1y) at that (unclamped) tap coordinate.
+struct Tap3 {
+  float x, y, z;
+};
+template <class TapF>
+__device__ __forceinline__ void warp_gather_fn(TapF tap, float wx, float wy, int fx, int fy,
+                                               float &sum, float &sumx, float &sumy, float &wsum) {
   float kx[4], ky[4];
   kx[0] = cubic_out(wx - (float)(fx - 1));
   kx[1] = cubic_in(wx - (float)fx);
@@ -238,22 +240,31 @@ __device__ __forceinline__ void warp_gather_taps(RowF row, ColF col, float wx, f
   ky[1] = cubic_in(wy - (float)fy);
   ky[2] = cubic_in(wy - (float)(fy + 1));
   ky[3] = cubic_out(wy - (float)(fy + 2));
-  int cxs[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) cxs[i] = col(fx - 1 + i);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float4 *rowp = row(fy - 1 + j);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float w = kx[i] * ky[j];
-      const float4 g = rowp[cxs[i]];
+      const Tap3 g = tap(fy - 1 + j, fx - 1 + i);
       sum = sum + w * g.x;
       sumx = sumx + w * g.y;
       sumy = sumy + w * g.z;
       wsum = wsum + w;
     }
   }
+}
+
+// The taps from a float4 (I1, I1x, I1y, -) plane: row(cy) -> the row, col(cx) -> index.
+template <class RowF, class ColF>
+__device__ __forceinline__ void warp_gather_taps(RowF row, ColF col, float wx, float wy, int fx,
+                                                 int fy, float &sum, float &sumx, float &sumy,
+                                                 float &wsum) {
+  warp_gather_fn(
+      [&](int cy, int cx) {
+        const float4 g = row(cy)[col(cx)];
+        return Tap3{g.x, g.y, g.z};
+      },
+      wx, wy, fx, fy, sum, sumx, sumy, wsum);
 }
 
 template <bool LDSPATH>
@@ -327,18 +338,24 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
   }
 }
 
-// warpBackward, streaming: one wavefront owns a 64-px column band of a row segment and
-// walks down it, one output row per step (one px per lane), with no barriers.  Its LDS
-// holds a ring of kWarpRing rows of the (I1, I1x, I1y) window, (64 + 2M) columns wide
-// (clamped coordinates, exactly the texture-clamp values; ring row = image row & 15):
-// at step y the rows y-M .. y+M are resident, so a px whose taps stay within M - 1 px of
-// it gathers from LDS; any other px takes the global-memory path (same taps, same order).
-// G rows are loaded kWarpAhead rows ahead into registers and written to the ring when
-// they are needed, u1 / u2 / I0 likewise, so the step's loads are in flight while earlier
-// rows compute; a row of G is read from HBM once per band (x 1 + 2M/64).  The ring and
-// the register rings are unrolled (kWarpAhead + 1 steps per loop trip), so no register
+// warpBackward, streaming: a block of NW wavefronts owns a 64-px column band of a row
+// segment and walks down it, NW output rows per step (one row per wavefront, one px per
+// lane).  The block's LDS holds a ring of R rows of the (I1, I1x, I1y) window, (64 + 2M)
+// columns wide (clamped coordinates, exactly the texture-clamp values; ring row = image
+// row mod R): at step s the rows y0-M .. y0+NW-1+M are resident (y0 = first row of the
+// step), so a px whose taps stay within M - 1 px of it gathers from LDS; any other px
+// takes the global-memory path (same taps, same order).  Each wavefront loads one new
+// window row and its own u1 / u2 / I0 row kWarpAhead steps ahead into registers and writes
+// the window row when its step comes, so loads are in flight while earlier rows compute;
+// a row of G is read from HBM once per band (x 1 + 2M/64).  One LDS-only barrier per step
+// (NW > 1): rows written at step s+1 are >= 1 and < 2NW + 2M <= R rows past any row a
+// slower wavefront still reads at step s, so they never land on a slot in use.  The
+// register rings are unrolled (kWarpAhead + 1 steps per loop trip), so no register
 // holding a load in flight is copied.
-constexpr int kWarpRing = 16, kWarpAhead = 2;
+constexpr int kWarpAhead = 2;
+
+template <int M, int NW>
+constexpr int warp_ring_rows() { return 2 * NW + 2 * M <= 16 ? 16 : 32; }
 
 struct WarpRollArgs {
   const float *I0;
@@ -346,43 +363,51 @@ struct WarpRollArgs {
   const float *u1, *u2;
   float *I1wx, *I1wy, *rho;
   int W, H, P;
-  int bands, seg_rows, waves;
+  int bands, seg_rows, waves;   // waves = blocks (bands x segments)
 };
 
 typedef float vf4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
 
-template <int M>
-struct WarpRow {   // this lane's share of window row y + M (2 slots) and of flow row y
+struct WarpRow {   // this lane's share of one window row (2 slots) and of one flow row
   vf4 g0, g1;
   float u1, u2, i0;
 };
 
 template <int M>
-__device__ __forceinline__ void warp_row_load(WarpRow<M> &v, const WarpRollArgs &a, int y, int xg0,
-                                              int xg1, int xc) {
-  const vf4 *Gr = reinterpret_cast<const vf4 *>(a.G) + (size_t)imin(imax(y + M, 0), a.H - 1) * a.P;
+__device__ __forceinline__ void warp_row_load(WarpRow &v, const WarpRollArgs &a, int gy, int fy,
+                                              int xg0, int xg1, int xc) {
+  const vf4 *Gr = reinterpret_cast<const vf4 *>(a.G) + (size_t)imin(imax(gy, 0), a.H - 1) * a.P;
   v.g0 = Gr[xg0];
   v.g1 = Gr[xg1];
-  const size_t o = (size_t)imin(y, a.H - 1) * a.P + xc;
+  const size_t o = (size_t)imin(fy, a.H - 1) * a.P + xc;
   v.u1 = a.u1[o];
   v.u2 = a.u2[o];
   v.i0 = a.I0[o];
 }
 
-template <int M>
-__device__ __forceinline__ void warp_roll_step(float4 *__restrict__ ring, const WarpRow<M> &cur,
-                                               WarpRow<M> &ahead, const WarpRollArgs &a, int y,
-                                               int ye, int lane, int x0, int xg0, int xg1, int xc) {
-  constexpr int WW = 64 + 2 * M;
-  // loads for step y + A: window row y + A + M, flow row y + A (in flight for A steps)
-  warp_row_load<M>(ahead, a, y + kWarpAhead, xg0, xg1, xc);
+// LDS-only workgroup barrier: waits for this wave's LDS writes, not for its global loads
+// in flight (a plain __syncthreads() would drain the prefetch).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int M, int NW>
+__device__ __forceinline__ void warp_roll_step(vf4 *__restrict__ ring, const WarpRow &cur,
+                                               WarpRow &ahead, const WarpRollArgs &a, int y0,
+                                               int ye, int w, int lane, int x0, int xg0, int xg1,
+                                               int xc) {
+  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>();
+  // loads for step + A: window row y0 + NW*A + M + w, flow row y0 + NW*A + w
+  warp_row_load<M>(ahead, a, y0 + NW * kWarpAhead + M + w, y0 + NW * kWarpAhead + w, xg0, xg1, xc);
   __builtin_amdgcn_sched_barrier(0);
-  // window row y + M enters the ring (it replaces row y + M - 16 < y - M); a wave's LDS
-  // accesses execute in order, so this step's gathers see it
-  vf4 *dst = reinterpret_cast<vf4 *>(ring) + ((y + M) & (kWarpRing - 1)) * WW;
+  // window row y0 + M + w enters the ring
+  vf4 *dst = ring + ((y0 + M + w) & (R - 1)) * WW;
   dst[lane] = cur.g0;
   if (lane < 2 * M) dst[64 + lane] = cur.g1;
-  const int x = x0 + lane;
+  if (NW > 1) lds_barrier();   // (a wave's own LDS accesses execute in order)
+  const int x = x0 + lane, y = y0 + w;
   const float wx = (float)x + cur.u1;
   const float wy = (float)y + cur.u2;
   const int fx = tap_floor(wx);
@@ -390,7 +415,7 @@ __device__ __forceinline__ void warp_roll_step(float4 *__restrict__ ring, const 
   float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
   const bool inwin = fx - 1 >= x0 - M && fx + 2 < x0 + 64 + M && fy - 1 >= y - M && fy + 2 <= y + M;
   if (inwin)
-    warp_gather_taps([&](int cy) { return ring + (cy & (kWarpRing - 1)) * WW; },
+    warp_gather_taps([&](int cy) { return reinterpret_cast<const float4 *>(ring + (cy & (R - 1)) * WW); },
                      [&](int cx) { return cx - (x0 - M); }, wx, wy, fx, fy, sum, sumx, sumy, wsum);
   else
     warp_gather<false>(a.G, a.P, 0, 0, a.W, a.H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
@@ -406,47 +431,214 @@ __device__ __forceinline__ void warp_roll_step(float4 *__restrict__ ring, const 
   }
 }
 
-template <int M>
-__global__ __launch_bounds__(64) void k_warp_roll(WarpRollArgs a) {
-  constexpr int WW = 64 + 2 * M;
-  static_assert(2 * M + 1 + kWarpAhead <= kWarpRing, "ring too small for the margin");
+template <int M, int NW>
+__global__ __launch_bounds__(64 * NW) void k_warp_roll(WarpRollArgs a) {
+  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>();
+  static_assert(2 * NW + 2 * M <= R, "ring too small for the margin");
   static_assert(2 * M <= 64, "second window slot per lane");
-  __shared__ float4 ring[kWarpRing * WW];
-  const int lane = threadIdx.x;
+  __shared__ vf4 ring[R * WW];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
-  if (wid >= a.waves) return;
+  if (wid >= a.waves) return;   // whole blocks
   const int band = wid % a.bands, seg = wid / a.bands;
   const int x0 = band * 64;
   const int xg0 = imin(imax(x0 - M + lane, 0), a.W - 1);        // window slot lane
   const int xg1 = imin(imax(x0 - M + 64 + lane, 0), a.W - 1);   // window slot 64 + lane
   const int xc = imin(x0 + lane, a.W - 1);
   const int ys = seg * a.seg_rows, ye = imin(ys + a.seg_rows, a.H);
-  // ring prologue: window rows ys - M .. ys + M - 1 (row ys + M enters at step ys); all
-  // loads are issued before the first write, so the prologue costs one memory latency
+  // ring prologue: window rows ys - M .. ys + M - 1, wave w taking rows w, w + NW, ...;
+  // all loads are issued before the first write
   {
-    vf4 t0[2 * M], t1[2 * M];
+    constexpr int PR = (2 * M + NW - 1) / NW;
+    vf4 t0[PR], t1[PR];
 #pragma unroll
-    for (int i = 0; i < 2 * M; ++i) {
+    for (int i = 0; i < PR; ++i) {
       const vf4 *Gr = reinterpret_cast<const vf4 *>(a.G) +
-                      (size_t)imin(imax(ys - M + i, 0), a.H - 1) * a.P;
+                      (size_t)imin(imax(ys - M + w + NW * i, 0), a.H - 1) * a.P;
       t0[i] = Gr[xg0];
       t1[i] = Gr[xg1];
     }
 #pragma unroll
-    for (int i = 0; i < 2 * M; ++i) {
-      vf4 *dst = reinterpret_cast<vf4 *>(ring) + ((ys - M + i) & (kWarpRing - 1)) * WW;
-      dst[lane] = t0[i];
-      if (lane < 2 * M) dst[64 + lane] = t1[i];
+    for (int i = 0; i < PR; ++i) {
+      const int r = ys - M + w + NW * i;
+      if (r < ys + M) {
+        vf4 *dst = ring + (r & (R - 1)) * WW;
+        dst[lane] = t0[i];
+        if (lane < 2 * M) dst[64 + lane] = t1[i];
+      }
     }
   }
   static_assert(kWarpAhead == 2, "the step loop below is unrolled for a 3-row ring");
-  WarpRow<M> A, B, C;
-  warp_row_load<M>(A, a, ys, xg0, xg1, xc);
-  warp_row_load<M>(B, a, ys + 1, xg0, xg1, xc);
-  for (int y = ys; y < ye; y += 3) {
-    warp_roll_step<M>(ring, A, C, a, y, ye, lane, x0, xg0, xg1, xc);
-    warp_roll_step<M>(ring, B, A, a, y + 1, ye, lane, x0, xg0, xg1, xc);
-    warp_roll_step<M>(ring, C, B, a, y + 2, ye, lane, x0, xg0, xg1, xc);
+  WarpRow A, B, C;
+  warp_row_load<M>(A, a, ys + M + w, ys + w, xg0, xg1, xc);
+  warp_row_load<M>(B, a, ys + NW + M + w, ys + NW + w, xg0, xg1, xc);
+  for (int y0 = ys; y0 < ye; y0 += 3 * NW) {
+    warp_roll_step<M, NW>(ring, A, C, a, y0, ye, w, lane, x0, xg0, xg1, xc);
+    warp_roll_step<M, NW>(ring, B, A, a, y0 + NW, ye, w, lane, x0, xg0, xg1, xc);
+    warp_roll_step<M, NW>(ring, C, B, a, y0 + 2 * NW, ye, w, lane, x0, xg0, xg1, xc);
+  }
+}
+
+// warpBackward, streaming from the level image: k_warp_roll's schedule, but the window
+// ring is filled from I1 and holds three float planes (I1, I1x, I1y) -- each window slot's
+// centred gradient is computed when its row enters the ring with centeredGradient's
+// exact formula at the clamped slot coordinate (the texture-clamp value of the gradient
+// image), so there is no G plane: HBM per px and warp is I1 (4 B x 1 + 2M/64) + u1, u2,
+// I0 + the three outputs, instead of 16 B of G.  Taps are 2-cycle ds_read_b32s.
+struct WarpRingArgs {
+  const float *I0, *I1;
+  const float *u1, *u2;
+  float *I1wx, *I1wy, *rho;
+  int W, H, P;
+  int bands, seg_rows, waves;   // waves = blocks (bands x segments)
+};
+
+struct WarpRowI {   // this lane's 2 window slots of one row (raw I1 stencils) + one flow row
+  float c0, l0, r0, n0, s0;   // slot lane:      centre, x-1, x+1, y-1, y+1 (clamped)
+  float c1, l1, r1, n1, s1;   // slot 64 + lane
+  float u1, u2, i0;
+};
+
+__device__ __forceinline__ void warp_ring_load(WarpRowI &v, const WarpRingArgs &a, int gy,
+                                               const int (&xs)[2][3]) {
+  const int r = imin(imax(gy, 0), a.H - 1);
+  const float *row = a.I1 + (size_t)r * a.P;
+  const float *up = a.I1 + (size_t)imax(r - 1, 0) * a.P;
+  const float *dn = a.I1 + (size_t)imin(r + 1, a.H - 1) * a.P;
+  v.c0 = row[xs[0][0]]; v.l0 = row[xs[0][1]]; v.r0 = row[xs[0][2]];
+  v.n0 = up[xs[0][0]]; v.s0 = dn[xs[0][0]];
+  // the second slot only exists for lanes < 2M; other lanes re-read slot 0's column
+  v.c1 = row[xs[1][0]]; v.l1 = row[xs[1][1]]; v.r1 = row[xs[1][2]];
+  v.n1 = up[xs[1][0]]; v.s1 = dn[xs[1][0]];
+}
+
+template <int M, int NW>
+__device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const WarpRowI &cur,
+                                               WarpRowI &ahead, const WarpRingArgs &a, int y0,
+                                               int ye, int w, int lane, int x0,
+                                               const int (&xs)[2][3], int xc) {
+  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>(), PL = R * WW;
+  // loads for step + A: window row y0 + NW*A + M + w, flow row y0 + NW*A + w
+  warp_ring_load(ahead, a, y0 + NW * kWarpAhead + M + w, xs);
+  {
+    const size_t o = (size_t)imin(y0 + NW * kWarpAhead + w, a.H - 1) * a.P + xc;
+    ahead.u1 = a.u1[o];
+    ahead.u2 = a.u2[o];
+    ahead.i0 = a.I0[o];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // window row y0 + M + w enters the ring: centeredGradient at each clamped slot
+  float *dst = ring + ((y0 + M + w) & (R - 1)) * WW;
+  dst[lane] = cur.c0;
+  dst[PL + lane] = 0.5f * (cur.r0 - cur.l0);
+  dst[2 * PL + lane] = 0.5f * (cur.s0 - cur.n0);
+  if (lane < 2 * M) {
+    dst[64 + lane] = cur.c1;
+    dst[PL + 64 + lane] = 0.5f * (cur.r1 - cur.l1);
+    dst[2 * PL + 64 + lane] = 0.5f * (cur.s1 - cur.n1);
+  }
+  if (NW > 1) lds_barrier();   // (a wave's own LDS accesses execute in order)
+  const int x = x0 + lane, y = y0 + w;
+  const float wx = (float)x + cur.u1;
+  const float wy = (float)y + cur.u2;
+  const int fx = tap_floor(wx);
+  const int fy = tap_floor(wy);
+  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
+  const bool inwin = fx - 1 >= x0 - M && fx + 2 < x0 + 64 + M && fy - 1 >= y - M && fy + 2 <= y + M;
+  if (inwin) {
+    warp_gather_fn(
+        [&](int cy, int cx) {
+          const float *p = ring + (cy & (R - 1)) * WW + (cx - (x0 - M));
+          return Tap3{p[0], p[PL], p[2 * PL]};
+        },
+        wx, wy, fx, fy, sum, sumx, sumy, wsum);
+  } else {
+    warp_gather_fn(
+        [&](int cy, int cx) {
+          const int rx = imin(imax(cx, 0), a.W - 1), ry = imin(imax(cy, 0), a.H - 1);
+          const float *row = a.I1 + (size_t)ry * a.P;
+          const float gx = 0.5f * (row[imin(rx + 1, a.W - 1)] - row[imax(rx - 1, 0)]);
+          const float gy = 0.5f * (a.I1[(size_t)imin(ry + 1, a.H - 1) * a.P + rx] -
+                                   a.I1[(size_t)imax(ry - 1, 0) * a.P + rx]);
+          return Tap3{row[rx], gx, gy};
+        },
+        wx, wy, fx, fy, sum, sumx, sumy, wsum);
+  }
+  const float coeff = 1.0f / wsum;
+  const float I1wv = sum * coeff;
+  const float I1wxv = sumx * coeff;
+  const float I1wyv = sumy * coeff;
+  if (x < a.W && y < ye) {
+    const size_t o = (size_t)y * a.P + x;
+    a.I1wx[o] = I1wxv;
+    a.I1wy[o] = I1wyv;
+    a.rho[o] = I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0;
+  }
+}
+
+template <int M, int NW>
+__global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
+  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>(), PL = R * WW;
+  static_assert(2 * NW + 2 * M <= R, "ring too small for the margin");
+  static_assert(2 * M <= 64, "second window slot per lane");
+  __shared__ float ring[3 * PL];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
+  if (wid >= a.waves) return;   // whole blocks
+  const int band = wid % a.bands, seg = wid / a.bands;
+  const int x0 = band * 64;
+  // the lane's two window slots: clamped column, its clamped x-1 and x+1
+  int xs[2][3];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int slot = k == 0 || lane < 2 * M ? lane + 64 * k : lane;
+    const int cc = imin(imax(x0 - M + slot, 0), a.W - 1);
+    xs[k][0] = cc;
+    xs[k][1] = imax(cc - 1, 0);
+    xs[k][2] = imin(cc + 1, a.W - 1);
+  }
+  const int xc = imin(x0 + lane, a.W - 1);
+  const int ys = seg * a.seg_rows, ye = imin(ys + a.seg_rows, a.H);
+  // ring prologue: window rows ys - M .. ys + M - 1, wave w taking rows w, w + NW, ...;
+  // all loads are issued before the first write
+  {
+    constexpr int PR = (2 * M + NW - 1) / NW;
+    WarpRowI t[PR];
+#pragma unroll
+    for (int i = 0; i < PR; ++i) warp_ring_load(t[i], a, ys - M + w + NW * i, xs);
+#pragma unroll
+    for (int i = 0; i < PR; ++i) {
+      const int r = ys - M + w + NW * i;
+      if (r < ys + M) {
+        float *dst = ring + (r & (R - 1)) * WW;
+        dst[lane] = t[i].c0;
+        dst[PL + lane] = 0.5f * (t[i].r0 - t[i].l0);
+        dst[2 * PL + lane] = 0.5f * (t[i].s0 - t[i].n0);
+        if (lane < 2 * M) {
+          dst[64 + lane] = t[i].c1;
+          dst[PL + 64 + lane] = 0.5f * (t[i].r1 - t[i].l1);
+          dst[2 * PL + 64 + lane] = 0.5f * (t[i].s1 - t[i].n1);
+        }
+      }
+    }
+  }
+  static_assert(kWarpAhead == 2, "the step loop below is unrolled for a 3-row ring");
+  WarpRowI A, B, C;
+  auto first = [&](WarpRowI &v, int step) {
+    warp_ring_load(v, a, ys + NW * step + M + w, xs);
+    const size_t o = (size_t)imin(ys + NW * step + w, a.H - 1) * a.P + xc;
+    v.u1 = a.u1[o];
+    v.u2 = a.u2[o];
+    v.i0 = a.I0[o];
+  };
+  first(A, 0);
+  first(B, 1);
+  for (int y0 = ys; y0 < ye; y0 += 3 * NW) {
+    warp_ring_step<M, NW>(ring, A, C, a, y0, ye, w, lane, x0, xs, xc);
+    warp_ring_step<M, NW>(ring, B, A, a, y0 + NW, ye, w, lane, x0, xs, xc);
+    warp_ring_step<M, NW>(ring, C, B, a, y0 + 2 * NW, ye, w, lane, x0, xs, xc);
   }
 }
 
