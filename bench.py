@@ -38,12 +38,13 @@ HBM_PEAK_GBS = 8000.0
 
 
 def _traffic():
-    """HBM bytes per k_iterate_tb launch measured with rocprofv3 PMC counters
-    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile.sh +
-    tools/pmc_summary.py), committed under profiles/.  None if not measured."""
+    """HBM bytes per iteration-pass launch (k_iterate_roll / k_iterate_tb) measured with
+    rocprofv3 PMC counters (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE;
+    tools/profile.sh + tools/pmc_summary.py), committed under profiles/.  None if not
+    measured."""
     p = ROOT / "profiles" / "traffic.json"
     try:
-        return json.loads(p.read_text())["k_iterate_tb_hbm_bytes_per_launch"]
+        return json.loads(p.read_text())["iterate_hbm_bytes_per_launch"]
     except Exception:
         return None
 
@@ -203,8 +204,9 @@ def main():
         achieved = k_bytes / (k_ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": TRAFFIC,
-                "kernel": "k_iterate_tb (temporally blocked estimateU + estimateDualVariables "
-                          "+ residual partials, <= 4 iterations per HBM pass)",
+                "kernel": "iteration passes: estimateU + estimateDualVariables + residual "
+                          "partials, <= 4 iterations per HBM pass (k_iterate_roll wavefront "
+                          "pipeline / k_iterate_tb blocked regions, hybrid)",
                 "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
                 "algorithmic_bytes_per_launch": round(k_bytes / k_launch),
                 "algorithmic_model": "SURVEY 8(d): 64 B/px per executed iteration",

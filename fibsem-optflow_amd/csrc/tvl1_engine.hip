@@ -636,7 +636,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
             const int ys = sg * seg, ye = std::min(ys + seg, lh);
             rows += std::min(ye - 1 + k, lh - 1) - std::max(ys - k, 0) + 1;
           }
-          hbm = (double)ra.bands * 64.0 * rows * 4.0 * ld_planes + Nl * 4.0 * st_planes;
+          hbm = (double)ra.bands * 64.0 * px * rows * 4.0 * ld_planes + Nl * 4.0 * st_planes;
         } else {
           TBArgs t;
           t.it = a;

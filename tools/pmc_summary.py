@@ -62,16 +62,33 @@ def main():
         if "SQ_WAVE_CYCLES" in c and "SQ_ACTIVE_INST_VALU" in c:
             res["valu_active_frac"] = round(c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"], 3)
         out[k] = res
+    # kernel classes as bench.py / tvl1_stats report them: every iteration pass
+    # (k_iterate_roll + k_iterate_tb of the hybrid) and every warpBackward
+    classes = {}
+    for cls, prefix in (("iterate", "k_iterate"), ("warp", "k_warp")):
+        ks = [k for k in out if k.startswith(prefix)]
+        if not ks:
+            continue
+        n = sum(out[k]["dispatches"] for k in ks)
+        tot_ns = sum(sum(dur.get(k, [])) for k in ks)
+        ndur = sum(len(dur.get(k, [])) for k in ks)
+        res = {"kernels": ks, "dispatches": n, "avg_us_trace": round(tot_ns / max(1, ndur) / 1e3, 2)}
+        if all("hbm_bytes_per_dispatch" in out[k] for k in ks):
+            hb = sum(out[k]["hbm_bytes_per_dispatch"] * out[k]["dispatches"] for k in ks) / n
+            res["hbm_bytes_per_dispatch"] = round(hb)
+            res["hbm_GBs_at_trace_avg"] = round(hb / (tot_ns / max(1, ndur)), 1)
+        classes[cls] = res
+    out["classes"] = classes
     print(json.dumps(out, indent=1))
     # profiles/traffic.json for bench.py's roofline.traffic
-    tb = [k for k in out if k.startswith("k_iterate_tb") and "hbm_bytes_per_dispatch" in out[k]]
-    if "--emit-traffic" in sys.argv and tb:
-        k = max(tb, key=lambda k: out[k]["dispatches"])
+    it = classes.get("iterate", {})
+    if "--emit-traffic" in sys.argv and "hbm_bytes_per_dispatch" in it:
         path = sys.argv[sys.argv.index("--emit-traffic") + 1]
-        json.dump({"k_iterate_tb_hbm_bytes_per_launch": out[k]["hbm_bytes_per_dispatch"],
-                   "kernel": k, "dispatches": out[k]["dispatches"],
+        json.dump({"iterate_hbm_bytes_per_launch": it["hbm_bytes_per_dispatch"],
+                   "iterate_kernels": it["kernels"], "dispatches": it["dispatches"],
+                   "warp_hbm_bytes_per_launch": classes.get("warp", {}).get("hbm_bytes_per_dispatch"),
                    "source": d, "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
-                   "separate passes, average over every dispatch of the bench run"},
+                   "separate passes, average over every iteration-pass dispatch of the bench run"},
                   open(path, "w"), indent=1)
 
 
