@@ -71,6 +71,14 @@ def parse():
                          "thread each); a step = one batch of this many pairs")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip per-kernel HIP events (roofline fields become null)")
+    ap.add_argument("--workload", choices=("pair", "stack"), default="pair",
+                    help="pair: BASELINE configs[1] (C2, the headline); stack: adjacent / "
+                         "strided pairs of a synthetic stack (C3: --slices 256; C4: --slices "
+                         "4096 on 8 GPUs; C5: --strides 1,4,16), slices made on the device")
+    ap.add_argument("--slices", type=int, default=256)
+    ap.add_argument("--strides", default="1")
+    ap.add_argument("--chunk", type=int, default=8,
+                    help="stack: contiguous pairs per work item (slice reuse within it)")
     return ap.parse_args()
 
 
@@ -101,6 +109,131 @@ def cpu_baseline(I0, I1, params, sample: str):
     }
 
 
+def run_stack(args, rank, world, local_rank, dist):
+    """C3/C4/C5: every pair (z, z + s) of a synthetic Z-slice stack for each stride s,
+    in contiguous chunks of --chunk pairs pulled from one work queue shared by all
+    ranks; each rank keeps --inflight chunks in flight (one engine ctx + stream + host
+    thread each).  Slices are generated on the device per chunk and reused by the
+    chunk's pairs (slice z is I1 of (z - s, z) and I0 of (z, z + s))."""
+    import threading
+    import torch
+    from optflow_amd import capi
+    from optflow_amd.stack import WorkQueue
+    from optflow_amd.synth_device import DeviceStack
+
+    W, H, Z = args.width, args.height, args.slices
+    strides = [int(t) for t in args.strides.split(",")]
+    params = capi.make_params(nscales=args.nscales, warps=args.warps,
+                              iterations=args.iterations, epsilon=args.epsilon)
+    dev = torch.device("cuda", local_rank)
+    gen = DeviceStack(W, H, dev)
+    items = []
+    for s_ in strides:
+        for z0 in range(0, Z - s_, args.chunk):
+            items.append((s_, z0, min(z0 + args.chunk, Z - s_)))
+    npairs = sum(z1 - z0 for _, z0, z1 in items)
+    F = max(1, args.inflight)
+    engines = [capi.Engine(params, device=local_rank) for _ in range(F)]
+    u = [torch.empty((H, W), dtype=torch.float32, device=dev) for _ in range(F)]
+    v = [torch.empty((H, W), dtype=torch.float32, device=dev) for _ in range(F)]
+    # warm-up: one pair per slot (kernels loaded, arenas sized)
+    a0, a1 = gen.slice(0), gen.slice(1)
+    torch.cuda.synchronize(dev)
+    for j in range(F):
+        engines[j].calc_device(a0.data_ptr(), W, a1.data_ptr(), W, W, H, u[j].data_ptr(),
+                               v[j].data_ptr(), 4 * W, stream=engines[j].stream)
+    torch.cuda.synchronize(dev)
+    del a0, a1
+    store = None
+    if dist:
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("stack_q", "0")
+        dist.barrier()
+    q = WorkQueue(len(items), store)
+    done = [0] * F
+    iters = [0] * F
+    errors = []
+
+    def worker(j):
+        eng, st = engines[j], engines[j].stream
+        torch_stream = torch.cuda.ExternalStream(st, device=dev)
+        try:
+            while True:
+                i = q.pop()
+                if i is None:
+                    return
+                s_, z0, z1 = items[i]
+                with torch.cuda.stream(torch_stream):
+                    sl = {z: gen.slice(z) for z in range(z0, z1 + s_)}
+                for z in range(z0, z1):
+                    r = eng.calc_device(sl[z].data_ptr(), W, sl[z + s_].data_ptr(), W, W, H,
+                                        u[j].data_ptr(), v[j].data_ptr(), 4 * W, stream=st)
+                    iters[j] += r["iterations_total"]
+                    done[j] += 1
+                torch_stream.synchronize()
+                del sl
+        except Exception as e:   # surfaced below, after the other workers finish
+            errors.append(repr(e))
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    threads = [threading.Thread(target=worker, args=(j,)) for j in range(F)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if errors:
+        raise RuntimeError("; ".join(errors))
+    mine = torch.tensor([float(sum(done)), float(sum(iters)), elapsed], dtype=torch.float64,
+                        device=dev)
+    if dist:
+        tot = mine[:2].clone()
+        dist.all_reduce(tot)
+        t = mine[2:].clone()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        pairs_done, iters_done, elapsed = float(tot[0]), float(tot[1]), float(t[0])
+    else:
+        pairs_done, iters_done = float(mine[0]), float(mine[1])
+    if dist:
+        dist.destroy_process_group()
+    if rank != 0:
+        return
+    assert int(pairs_done) == npairs, (pairs_done, npairs)
+    name = {1: "C3" if Z <= 512 else "C4"}.get(len(strides) == 1 and strides[0], "C5")
+    out = {
+        "metric": METRIC,
+        "value": round(pairs_done / elapsed, 4),
+        "unit": "slice-pairs/s",
+        "n_gpus": world,
+        "steps": 1,
+        "warmup": 1,
+        "ms_per_step": round(1e3 * elapsed, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (slices generated on the device)",
+        "config": {
+            "workload": (f"{name}: {npairs} pairs (z, z+s), s in {strides}, of a {Z}-slice "
+                         f"{W}x{H} stack, nscales {args.nscales}, warps {args.warps}, "
+                         f"iterations {args.iterations}, epsilon {args.epsilon}"),
+            "parallelism": (f"{world} rank(s), {F} chunk(s) in flight per GPU, chunks of "
+                            f"{args.chunk} pairs from one shared work queue"),
+            "step": "the whole stack",
+            "pairs": int(pairs_done),
+            "iterations_per_pair": round(iters_done / max(1.0, pairs_done), 1),
+        },
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
     import numpy as np
@@ -118,6 +251,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(local_rank)
+    if args.workload == "stack":
+        return run_stack(args, rank, world, local_rank, dist)
 
     from optflow_amd import capi, synth
 

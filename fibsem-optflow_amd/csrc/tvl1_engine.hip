@@ -73,6 +73,8 @@ struct tvl1_ctx {
   int roll_px = 2;           // px per lane of k_iterate_roll (1 or 2)
   int roll_slots[kRollMax + 1][2][3] = {};   // resident k_iterate_roll<G, K, PX> wavefronts
   int roll_lds = 0;          // experiment: dummy dynamic LDS per k_iterate_roll block (bytes)
+  int roll_fill = 100;       // % of the resident slots one streaming launch is sized for
+  int warp_fill = 100;
   int warp_lds = 0;          // experiment: dummy dynamic LDS per k_warp_lds block (bytes)
   int warp_margin = 6;       // k_warp_lds window margin (px): flows |u| < margin - 1 gather from LDS
   int warp_mode = 4;         // 2 = k_warp_lds (LDS-staged G window per 64 x 16 tile),
@@ -452,7 +454,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       const int M = c->warp_margin == 4 ? 4 : c->warp_margin == 5 ? 5 : 6;
       const int NW = c->warp_nw == 1 ? 1 : c->warp_nw == 4 ? 4 : 2;
       wa.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                    : roll_segment(wa.bands, lh, M, c->warp_ring_slots[M][NW]);
+                                    : roll_segment(wa.bands, lh, M, c->warp_ring_slots[M][NW] * c->warp_fill / 100);
       wa.waves = wa.bands * ((lh + wa.seg_rows - 1) / wa.seg_rows);
 #define WARP_RING(MM, NN)                                                                      \
   hipLaunchKernelGGL((k_warp_ring<MM, NN>), dim3(wa.waves), dim3(64 * NN), c->warp_lds, st, wa);
@@ -599,7 +601,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           const int out_w = 64 * px - 2 * halo;
           ra.bands = (lw + out_w - 1) / out_w;
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px]);
+                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px] * c->roll_fill / 100);
           ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           ra.waves = ra.bands * segs;
@@ -815,6 +817,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_ROLL_SEG")) c->roll_seg = atoi(m);
   if (const char *m = getenv("TVL1_ROLL_LDS")) c->roll_lds = std::max(0, atoi(m));
   if (const char *m = getenv("TVL1_ROLL_PX")) c->roll_px = atoi(m) == 1 ? 1 : 2;
+  if (const char *m = getenv("TVL1_ROLL_FILL")) c->roll_fill = std::max(10, atoi(m));
+  if (const char *m = getenv("TVL1_WARP_FILL")) c->warp_fill = std::max(10, atoi(m));
   if (const char *m = getenv("TVL1_WARP_LDS")) c->warp_lds = std::max(0, atoi(m));
   if (const char *m = getenv("TVL1_WARP_MARGIN")) c->warp_margin = atoi(m);
   if (const char *m = getenv("TVL1_WARP_NW")) c->warp_nw = atoi(m);

@@ -55,3 +55,22 @@ def uploads_needed(pairs: Sequence[Pair], order: Sequence[int]) -> int:
         n += (p not in have) + (q not in have)
         resident = (p, q)
     return n
+
+
+class WorkQueue:
+    """Work items handed out in order to whoever asks next: within a rank by a locked
+    counter, across ranks by an atomic add on torch.distributed's key-value store (the
+    rendezvous store: host TCP, no data-path collective)."""
+
+    def __init__(self, n: int, store=None, key: str = "stack_q"):
+        import threading
+        self.n, self.store, self.key = n, store, key
+        self.lock, self.next = threading.Lock(), 0
+
+    def pop(self):
+        if self.store is not None:
+            i = int(self.store.add(self.key, 1)) - 1
+        else:
+            with self.lock:
+                i, self.next = self.next, self.next + 1
+        return i if i < self.n else None

@@ -64,3 +64,53 @@ def test_gloo_two_ranks_cover_every_pair_once():
         assert p.exitcode == 0
     assert cnt == [n, n * (n - 1) // 2]
     assert union == list(range(n))
+
+
+def _queue_worker(rank, world, port, n, q):
+    import threading
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    store = dist.distributed_c10d._get_default_store()
+    if rank == 0:
+        store.set("stack_q", "0")
+    dist.barrier()
+    wq = stack.WorkQueue(n, store)
+    got = [[] for _ in range(2)]
+
+    def pull(j):
+        while (i := wq.pop()) is not None:
+            got[j].append(i)
+
+    ts = [threading.Thread(target=pull, args=(j,)) for j in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    gathered = [None] * world
+    dist.all_gather_object(gathered, got[0] + got[1])
+    if rank == 0:
+        q.put(gathered)
+    dist.destroy_process_group()
+
+
+def test_work_queue_two_ranks_two_threads_each_item_once():
+    """bench.py --workload stack: chunks pulled from one atomic counter on the
+    distributed store by every thread of every rank -- each handed out exactly once."""
+    n, world = 97, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_queue_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    allitems = sorted(i for g in gathered for i in g)
+    assert allitems == list(range(n))
+
+
+def test_work_queue_local_counter():
+    wq = stack.WorkQueue(5)
+    assert [wq.pop() for _ in range(7)] == [0, 1, 2, 3, 4, None, None]
