@@ -83,6 +83,8 @@ struct tvl1_ctx {
                              // 0 = k_warp_img (gradient built in LDS from I1), 1 = k_warp (global)
   int warp_roll_slots[8][5] = {};   // resident k_warp_roll<M, NW> blocks per device
   int warp_ring_slots[8][5] = {};   // resident k_warp_ring<M, NW> blocks per device
+  int fuse_first = 0;        // warpBackward fused into each warp's first pass (k_warp_pass; opt-in: slower)
+  int fuse_slots[8] = {};    // resident k_warp_pass<M> wavefronts per device
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
   int warp_th = 16;          // k_warp_lds tile height (8, 16, 32)
@@ -552,7 +554,11 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         }
         ui ^= 1;
       }
-      if (!have_gather) TRY(gather(s, ui, cb, wp));
+      // warpBackward fused into the warp's first pass (2 iterations ending in the first
+      // check) when that pass would stream through k_iterate_roll anyway
+      const bool fuse = c->fuse_first && !gam && !have_gather && roll_short &&
+                        prm.epsilon > 0 && prm.iterations >= 2;
+      if (!have_gather && !fuse) TRY(gather(s, ui, cb, wp));
       have_gather = false;
       a.I1wx = c->C[cb][0];
       a.I1wy = c->C[cb][1];
@@ -587,7 +593,41 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         double hbm;
         const int nu = gam ? 3 : 2, np = gam ? 6 : 4;
         const double ld_planes = 3 + nu + (p_zero ? 0 : np), st_planes = nu + np;
-        if (c->iter_mode == 1) {
+        double alg_extra = 0.0;   // the fused warpBackward's algorithmic bytes
+        if (fuse && n == 0 && k == 2 && calc_end) {
+          WarpPassArgs w;
+          w.ra.it = a;
+          w.ra.it.I1wx = c->C[cb][0];
+          w.ra.it.I1wy = c->C[cb][1];
+          w.ra.it.rho = c->C[cb][2];
+          w.I0 = c->I0s[s];
+          w.I1 = c->I1s[s];
+          const int M = c->warp_margin == 4 ? 4 : 6;
+          w.ra.bands = (lw + 59) / 60;
+          const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
+                                          : roll_segment(w.ra.bands, lh, 2 + M, c->fuse_slots[M]);
+          w.ra.seg_rows = seg;
+          const int segs = (lh + seg - 1) / seg;
+          w.ra.waves = w.ra.bands * segs;
+          blocks = w.ra.waves;
+          if (blocks > c->partials_cap)
+            return set_err(c, TVL1_EHIP, "internal: %d wavefronts > partials capacity %d", blocks,
+                           c->partials_cap);
+          if (M == 4)
+            hipLaunchKernelGGL(k_warp_pass<4>, dim3(w.ra.waves), dim3(64), 0, st, w);
+          else
+            hipLaunchKernelGGL(k_warp_pass<6>, dim3(w.ra.waves), dim3(64), 0, st, w);
+          // compulsory: u, p, I0 and the I1 window (x 1 + 2M/64) per band lane and row,
+          // u, p and the constants stored
+          double rows = 0.0;
+          for (int sg = 0; sg < segs; ++sg) {
+            const int ys = sg * seg, ye = std::min(ys + seg, lh);
+            rows += std::min(ye - 1 + 2, lh - 1) - std::max(ys - 2, 0) + 1;
+          }
+          hbm = (double)w.ra.bands * 64.0 * rows * 4.0 * ((p_zero ? 3 : 7) + (64.0 + 2 * M) / 64.0) +
+                Nl * 4.0 * 9.0;
+          alg_extra = Nl * 40.0;   // 40 B/px per warp
+        } else if (c->iter_mode == 1) {
           if (gam)
             hipLaunchKernelGGL(k_iterate<true>, dim3(nblk), dim3(kBlock), 0, st, a);
           else
@@ -669,8 +709,9 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           // u (+p unless p == 0), every px stores u and p once per pass
           hbm = (double)blocks * 64.0 * rh * 4.0 * ld_planes + Nl * 4.0 * st_planes;
         }
-        // algorithmic: 64 B/px per executed iteration
-        prof_end(c, st, tk, 0, Nl * 64.0 * k, hbm);
+        // algorithmic: 64 B/px per executed iteration (+ 40 B/px for a
+        // fused warpBackward)
+        prof_end(c, st, tk, 0, Nl * 64.0 * k + alg_extra, hbm);
         DIAG(c, st, "iteration pass", s, wp, n);
         p_zero = false;
         ui ^= 1;
@@ -822,6 +863,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_WARP_LDS")) c->warp_lds = std::max(0, atoi(m));
   if (const char *m = getenv("TVL1_WARP_MARGIN")) c->warp_margin = atoi(m);
   if (const char *m = getenv("TVL1_WARP_NW")) c->warp_nw = atoi(m);
+  if (const char *m = getenv("TVL1_FUSE")) c->fuse_first = atoi(m) != 0;
   if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_TB_CFG_LONG")) c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
@@ -868,6 +910,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     RING_SLOTS(5, 1) RING_SLOTS(5, 2) RING_SLOTS(5, 4)
     RING_SLOTS(6, 1) RING_SLOTS(6, 2) RING_SLOTS(6, 4)
 #undef RING_SLOTS
+    c->fuse_slots[4] = blocks_of((const void *)k_warp_pass<4>, 64);
+    c->fuse_slots[6] = blocks_of((const void *)k_warp_pass<6>, 64);
     (void)hipGetLastError();
   }
   *out = c;

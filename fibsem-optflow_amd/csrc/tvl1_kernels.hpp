@@ -353,6 +353,7 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
 // register rings are unrolled (kWarpAhead + 1 steps per loop trip), so no register
 // holding a load in flight is copied.
 constexpr int kWarpAhead = 2;
+constexpr int kWarpRing16 = 16;   // k_warp_pass ring rows
 
 template <int M, int NW>
 constexpr int warp_ring_rows() { return 2 * NW + 2 * M <= 16 ? 16 : 32; }
@@ -1368,6 +1369,11 @@ __device__ __forceinline__ float right_of(const float (&v)[PX], int j) {
 // reach them and past the image bottom they compute values no stored cell depends on (see
 // the dependency list above; the border forms select, never combine).
 template <bool G, int K, int PX>
+__device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
+                                             const IterArgs &a, int r, const RollLane &L,
+                                             unsigned nb, unsigned rowb, double &acc);
+
+template <bool G, int K, int PX>
 __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                           RollIn<G, PX> &ahead, const IterArgs &a, int r,
                                           const RollLane &L, unsigned nb, unsigned rowb,
@@ -1377,6 +1383,15 @@ __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G,
   // kRollAhead steps later then leaves the younger stores and loads in flight (vmcnt
   // counts in issue order)
   __builtin_amdgcn_sched_barrier(0);
+  roll_advance<G, K, PX>(S, in, a, r, L, nb, rowb, acc);
+}
+
+// The compute and stores of one step: input row r (in `in`) enters stage 0 and every
+// stage advances one row.
+template <bool G, int K, int PX>
+__device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
+                                             const IterArgs &a, int r, const RollLane &L,
+                                             unsigned nb, unsigned rowb, double &acc) {
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     // shift every stage one row down
@@ -1532,6 +1547,204 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
     roll_step<G, K, PX>(S, A, C, a, r, L, nb, rowb, acc);
     roll_step<G, K, PX>(S, B, A, a, r + 1, L, nb, rowb, acc);
     roll_step<G, K, PX>(S, C, B, a, r + 2, L, nb, rowb, acc);
+  }
+  if (a.calc_err) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) a.partials[wid] = acc;
+  }
+}
+
+// ---------------------------------------------------------------- K5 + first K6/K8 pass
+// k_warp_pass<M>: warpBackward of a warp fused into that warp's first iteration pass,
+// which always runs 2 iterations (procOneScale's first check is at n = 1).  One
+// wavefront = one k_iterate_roll<false, 2, 1> band (64 lanes, 2-px halo, 60 output px) of
+// a row segment.  Before input row r enters the pipeline, its warp constants are gathered
+// from an LDS ring of the (I1, I1x, I1y) window rows r-M .. r+M that the same wavefront
+// streams (k_warp_ring's per-slot centeredGradient, same taps and order), so the
+// constants reach their first use without a round trip through HBM.  They are still
+// stored (output columns / rows) for the warp's later passes.  HBM per px: I1 + I0 + u +
+// p in, u + p + constants out (~71 B) instead of ~92 B for k_warp_ring + the first pass.
+struct WarpPassArgs {
+  RollArgs ra;              // pass geometry and planes; ra.it.I1wx / I1wy / rho are written
+  const float *I0, *I1;     // level images
+};
+
+struct WinRow {   // this lane's 2 window slots of one I1 row: centre, x-1, x+1, y-1, y+1
+  float c0, l0, r0, n0, s0, c1, l1, r1, n1, s1;
+};
+
+struct PassIn {   // one pipeline input row at this lane (constants are computed) + window row
+  float u1, u2, p11, p12, p21, p22, i0;
+  WinRow g;
+};
+
+__device__ __forceinline__ void win_load(WinRow &v, const float *__restrict__ I1, int P, int H,
+                                         int gy, const int (&xs)[2][3]) {
+  const int r = imin(imax(gy, 0), H - 1);
+  const float *row = I1 + (size_t)r * P;
+  const float *up = I1 + (size_t)imax(r - 1, 0) * P;
+  const float *dn = I1 + (size_t)imin(r + 1, H - 1) * P;
+  v.c0 = row[xs[0][0]]; v.l0 = row[xs[0][1]]; v.r0 = row[xs[0][2]];
+  v.n0 = up[xs[0][0]]; v.s0 = dn[xs[0][0]];
+  v.c1 = row[xs[1][0]]; v.l1 = row[xs[1][1]]; v.r1 = row[xs[1][2]];
+  v.n1 = up[xs[1][0]]; v.s1 = dn[xs[1][0]];
+}
+
+template <int M>
+__device__ __forceinline__ void win_store(float *__restrict__ ring, const WinRow &v, int r, int lane) {
+  constexpr int WW = 64 + 2 * M, PL = kWarpRing16 * WW;
+  float *dst = ring + (r & (kWarpRing16 - 1)) * WW;
+  dst[lane] = v.c0;
+  dst[PL + lane] = 0.5f * (v.r0 - v.l0);
+  dst[2 * PL + lane] = 0.5f * (v.s0 - v.n0);
+  if (lane < 2 * M) {
+    dst[64 + lane] = v.c1;
+    dst[PL + 64 + lane] = 0.5f * (v.r1 - v.l1);
+    dst[2 * PL + 64 + lane] = 0.5f * (v.s1 - v.n1);
+  }
+}
+
+template <int M>
+__device__ __forceinline__ void pass_load(PassIn &v, const WarpPassArgs &w, unsigned nb,
+                                          unsigned rowb, int r, const RollLane &L,
+                                          const int (&xs)[2][3]) {
+  const IterArgs &a = w.ra.it;
+  const unsigned so = (unsigned)imin(r, a.H - 1) * rowb;
+  float t[1];
+  bload<1>(t, a.u1s, nb, L.vload, so); v.u1 = t[0];
+  bload<1>(t, a.u2s, nb, L.vload, so); v.u2 = t[0];
+  bload<1>(t, a.p11s, nb, L.vload, so); v.p11 = t[0];
+  bload<1>(t, a.p12s, nb, L.vload, so); v.p12 = t[0];
+  bload<1>(t, a.p21s, nb, L.vload, so); v.p21 = t[0];
+  bload<1>(t, a.p22s, nb, L.vload, so); v.p22 = t[0];
+  bload<1>(t, w.I0, nb, L.vload, so); v.i0 = t[0];
+  win_load(v.g, w.I1, a.P, a.H, r + M, xs);
+}
+
+template <int M>
+__device__ __forceinline__ void pass_step(RollPipe<false, 2, 1> &S, float *__restrict__ ring,
+                                          const PassIn &cur, PassIn &ahead,
+                                          const WarpPassArgs &w, int r, const RollLane &L,
+                                          int lane, int x0w, unsigned nb, unsigned rowb,
+                                          const int (&xs)[2][3], double &acc) {
+  constexpr int WW = 64 + 2 * M, PL = kWarpRing16 * WW;
+  const IterArgs &a = w.ra.it;
+  pass_load<M>(ahead, w, nb, rowb, r + kRollAhead, L, xs);
+  __builtin_amdgcn_sched_barrier(0);
+  // window row r + M enters the ring (it replaces row r + M - 16 < r - M)
+  win_store<M>(ring, cur.g, r + M, lane);
+  // warpBackward of input row r at this lane's column
+  const int x = L.X;
+  const float wx = (float)x + cur.u1;
+  const float wy = (float)r + cur.u2;
+  const int fx = tap_floor(wx);
+  const int fy = tap_floor(wy);
+  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
+  const bool inwin = fx - 1 >= x0w && fx + 2 < x0w + WW && fy - 1 >= r - M && fy + 2 <= r + M;
+  if (inwin) {
+    warp_gather_fn(
+        [&](int cy, int cx) {
+          const float *q = ring + (cy & (kWarpRing16 - 1)) * WW + (cx - x0w);
+          return Tap3{q[0], q[PL], q[2 * PL]};
+        },
+        wx, wy, fx, fy, sum, sumx, sumy, wsum);
+  } else {
+    warp_gather_fn(
+        [&](int cy, int cx) {
+          const int rx = imin(imax(cx, 0), a.W - 1), ry = imin(imax(cy, 0), a.H - 1);
+          const float *row = w.I1 + (size_t)ry * a.P;
+          const float gx = 0.5f * (row[imin(rx + 1, a.W - 1)] - row[imax(rx - 1, 0)]);
+          const float gy = 0.5f * (w.I1[(size_t)imin(ry + 1, a.H - 1) * a.P + rx] -
+                                   w.I1[(size_t)imax(ry - 1, 0) * a.P + rx]);
+          return Tap3{row[rx], gx, gy};
+        },
+        wx, wy, fx, fy, sum, sumx, sumy, wsum);
+  }
+  const float coeff = 1.0f / wsum;
+  const float I1wv = sum * coeff;
+  RollIn<false, 1> in;
+  in.wx[0] = sumx * coeff;
+  in.wy[0] = sumy * coeff;
+  in.rh[0] = I1wv - in.wx[0] * cur.u1 - in.wy[0] * cur.u2 - cur.i0;
+  in.u1[0] = cur.u1; in.u2[0] = cur.u2; in.u3[0] = 0.0f;
+  in.p11[0] = cur.p11; in.p12[0] = cur.p12; in.p21[0] = cur.p21; in.p22[0] = cur.p22;
+  in.p31[0] = in.p32[0] = 0.0f;
+  // the constants of output cells, for the warp's later passes
+  const unsigned vo = L.out && r >= L.ys && r < L.ye ? (unsigned)r * rowb + L.vst : kOOB;
+  bstore((float *)a.I1wx, nb, vo, 0, in.wx[0]);
+  bstore((float *)a.I1wy, nb, vo, 0, in.wy[0]);
+  bstore((float *)a.rho, nb, vo, 0, in.rh[0]);
+  roll_advance<false, 2, 1>(S, in, a, r, L, nb, rowb, acc);
+}
+
+template <int M>
+__global__ __launch_bounds__(64) void k_warp_pass(WarpPassArgs w) {
+  constexpr int K = 2, HALO = 2, WW = 64 + 2 * M, PL = kWarpRing16 * WW;
+  static_assert(2 * M + 1 + kRollAhead <= kWarpRing16, "ring too small for the margin");
+  __shared__ float ring[3 * PL];
+  const RollArgs &ra = w.ra;
+  const IterArgs &a = ra.it;
+  const int lane = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
+  if (wid >= ra.waves) return;
+  const int band = wid % ra.bands, seg = wid / ra.bands;
+  RollLane L;
+  L.X = band * (64 - 2 * HALO) - HALO + lane;
+  L.vload = 4u * imin(imax(L.X, 0), a.P - 1);
+  L.out = lane >= HALO && lane < 64 - HALO && L.X < a.W;
+  L.vst = 4u * (unsigned)imax(L.X, 0);
+  const unsigned nb = 4u * (unsigned)a.P * (unsigned)a.H;
+  const unsigned rowb = 4u * (unsigned)a.P;
+  L.ys = seg * ra.seg_rows;
+  L.ye = imin(L.ys + ra.seg_rows, a.H);
+  const int r0 = imax(L.ys - K, 0);
+  const int thirds = (L.ye + K - r0 + 2) / 3;
+  const int x0w = L.X - lane - M;                   // window column of slot 0
+  int xs[2][3];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int slot = k == 0 || lane < 2 * M ? lane + 64 * k : lane;
+    const int cc = imin(imax(x0w + slot, 0), a.W - 1);
+    xs[k][0] = cc;
+    xs[k][1] = imax(cc - 1, 0);
+    xs[k][2] = imin(cc + 1, a.W - 1);
+  }
+  // ring prologue: window rows r0 - M .. r0 + M - 1, loads issued in two batches
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    WinRow t[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) win_load(t[i], w.I1, a.P, a.H, r0 - M + b * M + i, xs);
+#pragma unroll
+    for (int i = 0; i < M; ++i) win_store<M>(ring, t[i], r0 - M + b * M + i, lane);
+  }
+  RollPipe<false, K, 1> S;
+#pragma unroll
+  for (int n = 0; n <= K; ++n) {
+    S.U1c[n][0] = S.U2c[n][0] = S.U3c[n][0] = S.U1p[n][0] = S.U2p[n][0] = S.U3p[n][0] = 0.0f;
+    S.P11c[n][0] = S.P12c[n][0] = S.P21c[n][0] = S.P22c[n][0] = S.P31c[n][0] = S.P32c[n][0] = 0.0f;
+    S.P11p[n][0] = S.P12p[n][0] = S.P21p[n][0] = S.P22p[n][0] = S.P31p[n][0] = S.P32p[n][0] = 0.0f;
+  }
+#pragma unroll
+  for (int n = 0; n < K; ++n) S.CX[n][0] = S.CY[n][0] = S.CR[n][0] = 0.0f;
+  // as many dropped stores after each prologue load as a step issues (see k_iterate_roll)
+  auto dummy_stores = [&]() {
+    float *outs[9] = {(float *)a.I1wx, (float *)a.I1wy, (float *)a.rho, a.u1d, a.u2d,
+                      a.p11d, a.p12d, a.p21d, a.p22d};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) bstore(outs[k], nb, kOOB, 0, 0.0f);
+  };
+  PassIn A, B, C;
+  pass_load<M>(A, w, nb, rowb, r0, L, xs);
+  dummy_stores();
+  pass_load<M>(B, w, nb, rowb, r0 + 1, L, xs);
+  dummy_stores();
+  double acc = 0.0;
+  for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
+    pass_step<M>(S, ring, A, C, w, r, L, lane, x0w, nb, rowb, xs, acc);
+    pass_step<M>(S, ring, B, A, w, r + 1, L, lane, x0w, nb, rowb, xs, acc);
+    pass_step<M>(S, ring, C, B, w, r + 2, L, lane, x0w, nb, rowb, xs, acc);
   }
   if (a.calc_err) {
 #pragma unroll
