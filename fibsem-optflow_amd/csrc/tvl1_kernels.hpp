@@ -63,6 +63,41 @@ __device__ __forceinline__ int xcd_chunk(int b, int n) {
   return x * q + imin(x, rem) + i;
 }
 
+// Buffer access to a plane: scalar descriptor (base, size in bytes), the row in the
+// scalar offset, the lane's column as one 32-bit VGPR byte offset.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)bytes, 0x00020000);
+}
+constexpr unsigned kOOB = 0x7ffffff0u;   // byte offset beyond every plane: store dropped
+__device__ __forceinline__ void bstore(float *p, unsigned bytes, unsigned voff, unsigned soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
+}
+// PX consecutive floats of a plane (4- or 8-byte store)
+template <int PX>
+__device__ __forceinline__ void bstorev(float *p, unsigned bytes, unsigned voff, const float (&v)[PX]) {
+  if constexpr (PX == 1) {
+    bstore(p, bytes, voff, 0, v[0]);
+  } else {
+    using T = decltype(__builtin_amdgcn_raw_buffer_load_b64(plane_rsrc(p, bytes), 0, 0, 0));
+    T t;
+    __builtin_memcpy(&t, v, 8);
+    __builtin_amdgcn_raw_buffer_store_b64(t, plane_rsrc(p, bytes), (int)voff, 0, 0);
+  }
+}
+// PX consecutive floats of a plane (4- or 8-byte load)
+template <int PX>
+__device__ __forceinline__ void bload(float (&d)[PX], const float *p, unsigned bytes, unsigned voff,
+                                      unsigned soff) {
+  if constexpr (PX == 1) {
+    d[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(plane_rsrc(p, bytes), (int)voff, (int)soff, 0));
+  } else {
+    static_assert(PX == 2, "1 or 2 px per lane");
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
+    static_assert(sizeof(v) == 8, "b64 load");
+    __builtin_memcpy(d, &v, 8);
+  }
+}
+
 // ---------------------------------------------------------------- K1 convert
 // GpuMat::convertTo(CV_32F, 1.0) for both frames (blockIdx.z selects the frame).
 __global__ void k_convert_u8(const uint8_t *__restrict__ s0, size_t sp0,
@@ -501,33 +536,46 @@ struct WarpRowI {   // this lane's 2 window slots of one row (raw I1 stencils) +
   float u1, u2, i0;
 };
 
-__device__ __forceinline__ void warp_ring_load(WarpRowI &v, const WarpRingArgs &a, int gy,
-                                               const int (&xs)[2][3]) {
+// xs: byte offsets of the lane's 2 window slots: clamped column, its clamped x-1 and x+1.
+// The row is a scalar offset, so the 10 loads need no per-lane address arithmetic.
+__device__ __forceinline__ void warp_ring_load(WarpRowI &v, const WarpRingArgs &a, unsigned nb,
+                                               unsigned rowb, int gy, const unsigned (&xs)[2][3]) {
   const int r = imin(imax(gy, 0), a.H - 1);
-  const float *row = a.I1 + (size_t)r * a.P;
-  const float *up = a.I1 + (size_t)imax(r - 1, 0) * a.P;
-  const float *dn = a.I1 + (size_t)imin(r + 1, a.H - 1) * a.P;
-  v.c0 = row[xs[0][0]]; v.l0 = row[xs[0][1]]; v.r0 = row[xs[0][2]];
-  v.n0 = up[xs[0][0]]; v.s0 = dn[xs[0][0]];
+  const unsigned so = (unsigned)r * rowb, su = (unsigned)imax(r - 1, 0) * rowb,
+                 sd = (unsigned)imin(r + 1, a.H - 1) * rowb;
+  float t[1];
+  bload<1>(t, a.I1, nb, xs[0][0], so); v.c0 = t[0];
+  bload<1>(t, a.I1, nb, xs[0][1], so); v.l0 = t[0];
+  bload<1>(t, a.I1, nb, xs[0][2], so); v.r0 = t[0];
+  bload<1>(t, a.I1, nb, xs[0][0], su); v.n0 = t[0];
+  bload<1>(t, a.I1, nb, xs[0][0], sd); v.s0 = t[0];
   // the second slot only exists for lanes < 2M; other lanes re-read slot 0's column
-  v.c1 = row[xs[1][0]]; v.l1 = row[xs[1][1]]; v.r1 = row[xs[1][2]];
-  v.n1 = up[xs[1][0]]; v.s1 = dn[xs[1][0]];
+  bload<1>(t, a.I1, nb, xs[1][0], so); v.c1 = t[0];
+  bload<1>(t, a.I1, nb, xs[1][1], so); v.l1 = t[0];
+  bload<1>(t, a.I1, nb, xs[1][2], so); v.r1 = t[0];
+  bload<1>(t, a.I1, nb, xs[1][0], su); v.n1 = t[0];
+  bload<1>(t, a.I1, nb, xs[1][0], sd); v.s1 = t[0];
+}
+
+__device__ __forceinline__ void warp_flow_load(WarpRowI &v, const WarpRingArgs &a, unsigned nb,
+                                               unsigned rowb, int fy, unsigned xcb) {
+  const unsigned so = (unsigned)imin(fy, a.H - 1) * rowb;
+  float t[1];
+  bload<1>(t, a.u1, nb, xcb, so); v.u1 = t[0];
+  bload<1>(t, a.u2, nb, xcb, so); v.u2 = t[0];
+  bload<1>(t, a.I0, nb, xcb, so); v.i0 = t[0];
 }
 
 template <int M, int NW>
 __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const WarpRowI &cur,
                                                WarpRowI &ahead, const WarpRingArgs &a, int y0,
                                                int ye, int w, int lane, int x0,
-                                               const int (&xs)[2][3], int xc) {
+                                               const unsigned (&xs)[2][3], unsigned xcb,
+                                               unsigned nb, unsigned rowb) {
   constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>(), PL = R * WW;
   // loads for step + A: window row y0 + NW*A + M + w, flow row y0 + NW*A + w
-  warp_ring_load(ahead, a, y0 + NW * kWarpAhead + M + w, xs);
-  {
-    const size_t o = (size_t)imin(y0 + NW * kWarpAhead + w, a.H - 1) * a.P + xc;
-    ahead.u1 = a.u1[o];
-    ahead.u2 = a.u2[o];
-    ahead.i0 = a.I0[o];
-  }
+  warp_ring_load(ahead, a, nb, rowb, y0 + NW * kWarpAhead + M + w, xs);
+  warp_flow_load(ahead, a, nb, rowb, y0 + NW * kWarpAhead + w, xcb);
   __builtin_amdgcn_sched_barrier(0);
   // window row y0 + M + w enters the ring: centeredGradient at each clamped slot
   float *dst = ring + ((y0 + M + w) & (R - 1)) * WW;
@@ -570,12 +618,10 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
-  if (x < a.W && y < ye) {
-    const size_t o = (size_t)y * a.P + x;
-    a.I1wx[o] = I1wxv;
-    a.I1wy[o] = I1wyv;
-    a.rho[o] = I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0;
-  }
+  const unsigned vo = x < a.W && y < ye ? (unsigned)y * rowb + 4u * (unsigned)x : kOOB;
+  bstore(a.I1wx, nb, vo, 0, I1wxv);
+  bstore(a.I1wy, nb, vo, 0, I1wyv);
+  bstore(a.rho, nb, vo, 0, I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0);
 }
 
 template <int M, int NW>
@@ -590,17 +636,19 @@ __global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
   if (wid >= a.waves) return;   // whole blocks
   const int band = wid % a.bands, seg = wid / a.bands;
   const int x0 = band * 64;
-  // the lane's two window slots: clamped column, its clamped x-1 and x+1
-  int xs[2][3];
+  // the lane's two window slots: clamped column, its clamped x-1 and x+1 (byte offsets)
+  unsigned xs[2][3];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int slot = k == 0 || lane < 2 * M ? lane + 64 * k : lane;
     const int cc = imin(imax(x0 - M + slot, 0), a.W - 1);
-    xs[k][0] = cc;
-    xs[k][1] = imax(cc - 1, 0);
-    xs[k][2] = imin(cc + 1, a.W - 1);
+    xs[k][0] = 4u * cc;
+    xs[k][1] = 4u * imax(cc - 1, 0);
+    xs[k][2] = 4u * imin(cc + 1, a.W - 1);
   }
-  const int xc = imin(x0 + lane, a.W - 1);
+  const unsigned xcb = 4u * imin(x0 + lane, a.W - 1);
+  const unsigned nb = 4u * (unsigned)a.P * (unsigned)a.H;   // plane bytes
+  const unsigned rowb = 4u * (unsigned)a.P;
   const int ys = seg * a.seg_rows, ye = imin(ys + a.seg_rows, a.H);
   // ring prologue: window rows ys - M .. ys + M - 1, wave w taking rows w, w + NW, ...;
   // all loads are issued before the first write
@@ -608,7 +656,7 @@ __global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
     constexpr int PR = (2 * M + NW - 1) / NW;
     WarpRowI t[PR];
 #pragma unroll
-    for (int i = 0; i < PR; ++i) warp_ring_load(t[i], a, ys - M + w + NW * i, xs);
+    for (int i = 0; i < PR; ++i) warp_ring_load(t[i], a, nb, rowb, ys - M + w + NW * i, xs);
 #pragma unroll
     for (int i = 0; i < PR; ++i) {
       const int r = ys - M + w + NW * i;
@@ -628,18 +676,15 @@ __global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
   static_assert(kWarpAhead == 2, "the step loop below is unrolled for a 3-row ring");
   WarpRowI A, B, C;
   auto first = [&](WarpRowI &v, int step) {
-    warp_ring_load(v, a, ys + NW * step + M + w, xs);
-    const size_t o = (size_t)imin(ys + NW * step + w, a.H - 1) * a.P + xc;
-    v.u1 = a.u1[o];
-    v.u2 = a.u2[o];
-    v.i0 = a.I0[o];
+    warp_ring_load(v, a, nb, rowb, ys + NW * step + M + w, xs);
+    warp_flow_load(v, a, nb, rowb, ys + NW * step + w, xcb);
   };
   first(A, 0);
   first(B, 1);
   for (int y0 = ys; y0 < ye; y0 += 3 * NW) {
-    warp_ring_step<M, NW>(ring, A, C, a, y0, ye, w, lane, x0, xs, xc);
-    warp_ring_step<M, NW>(ring, B, A, a, y0 + NW, ye, w, lane, x0, xs, xc);
-    warp_ring_step<M, NW>(ring, C, B, a, y0 + 2 * NW, ye, w, lane, x0, xs, xc);
+    warp_ring_step<M, NW>(ring, A, C, a, y0, ye, w, lane, x0, xs, xcb, nb, rowb);
+    warp_ring_step<M, NW>(ring, B, A, a, y0 + NW, ye, w, lane, x0, xs, xcb, nb, rowb);
+    warp_ring_step<M, NW>(ring, C, B, a, y0 + 2 * NW, ye, w, lane, x0, xs, xcb, nb, rowb);
   }
 }
 
@@ -1262,41 +1307,6 @@ __device__ __forceinline__ float from_left(float v) {
 // lane i <- lane i+1 (DPP wave_shl:1; lane 63 gets 0)
 __device__ __forceinline__ float from_right(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
-}
-
-// Buffer access to a plane: scalar descriptor (base, size in bytes), the row in the
-// scalar offset, the lane's column as one 32-bit VGPR byte offset.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)bytes, 0x00020000);
-}
-constexpr unsigned kOOB = 0x7ffffff0u;   // byte offset beyond every plane: store dropped
-__device__ __forceinline__ void bstore(float *p, unsigned bytes, unsigned voff, unsigned soff, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
-}
-// PX consecutive floats of a plane (4- or 8-byte store)
-template <int PX>
-__device__ __forceinline__ void bstorev(float *p, unsigned bytes, unsigned voff, const float (&v)[PX]) {
-  if constexpr (PX == 1) {
-    bstore(p, bytes, voff, 0, v[0]);
-  } else {
-    using T = decltype(__builtin_amdgcn_raw_buffer_load_b64(plane_rsrc(p, bytes), 0, 0, 0));
-    T t;
-    __builtin_memcpy(&t, v, 8);
-    __builtin_amdgcn_raw_buffer_store_b64(t, plane_rsrc(p, bytes), (int)voff, 0, 0);
-  }
-}
-// PX consecutive floats of a plane (4- or 8-byte load)
-template <int PX>
-__device__ __forceinline__ void bload(float (&d)[PX], const float *p, unsigned bytes, unsigned voff,
-                                      unsigned soff) {
-  if constexpr (PX == 1) {
-    d[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(plane_rsrc(p, bytes), (int)voff, (int)soff, 0));
-  } else {
-    static_assert(PX == 2, "1 or 2 px per lane");
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
-    static_assert(sizeof(v) == 8, "b64 load");
-    __builtin_memcpy(d, &v, 8);
-  }
 }
 
 template <bool G, int PX>
