@@ -266,15 +266,18 @@ struct Tap3 {
 template <class TapF>
 __device__ __forceinline__ void warp_gather_fn(TapF tap, float wx, float wy, int fx, int fy,
                                                float &sum, float &sumx, float &sumy, float &wsum) {
+  // (float)(fx + k) == (float)fx + k exactly: |fx| <= 2^24 (tap_floor), and both round
+  // the same integer once
+  const float fxf = (float)fx, fyf = (float)fy;
   float kx[4], ky[4];
-  kx[0] = cubic_out(wx - (float)(fx - 1));
-  kx[1] = cubic_in(wx - (float)fx);
-  kx[2] = cubic_in(wx - (float)(fx + 1));
-  kx[3] = cubic_out(wx - (float)(fx + 2));
-  ky[0] = cubic_out(wy - (float)(fy - 1));
-  ky[1] = cubic_in(wy - (float)fy);
-  ky[2] = cubic_in(wy - (float)(fy + 1));
-  ky[3] = cubic_out(wy - (float)(fy + 2));
+  kx[0] = cubic_out(wx - (fxf - 1.0f));
+  kx[1] = cubic_in(wx - fxf);
+  kx[2] = cubic_in(wx - (fxf + 1.0f));
+  kx[3] = cubic_out(wx - (fxf + 2.0f));
+  ky[0] = cubic_out(wy - (fyf - 1.0f));
+  ky[1] = cubic_in(wy - fyf);
+  ky[2] = cubic_in(wy - (fyf + 1.0f));
+  ky[3] = cubic_out(wy - (fyf + 2.0f));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -566,27 +569,36 @@ __device__ __forceinline__ void warp_flow_load(WarpRowI &v, const WarpRingArgs &
   bload<1>(t, a.I0, nb, xcb, so); v.i0 = t[0];
 }
 
+// Ring layout: [ring row][plane (I1, I1x, I1y)][WW]: one tap row's 12 values are within
+// 3 * WW < 256 dwords of one base, so they load with ds_read2_b32 immediate offsets.
+template <int M, int NW>
+__device__ __forceinline__ void warp_ring_put(float *__restrict__ ring, const WarpRowI &v, int r,
+                                              int lane) {
+  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>();
+  float *dst = ring + (r & (R - 1)) * (3 * WW);
+  dst[lane] = v.c0;
+  dst[WW + lane] = 0.5f * (v.r0 - v.l0);
+  dst[2 * WW + lane] = 0.5f * (v.s0 - v.n0);
+  if (lane < 2 * M) {
+    dst[64 + lane] = v.c1;
+    dst[WW + 64 + lane] = 0.5f * (v.r1 - v.l1);
+    dst[2 * WW + 64 + lane] = 0.5f * (v.s1 - v.n1);
+  }
+}
+
 template <int M, int NW>
 __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const WarpRowI &cur,
                                                WarpRowI &ahead, const WarpRingArgs &a, int y0,
                                                int ye, int w, int lane, int x0,
                                                const unsigned (&xs)[2][3], unsigned xcb,
                                                unsigned nb, unsigned rowb) {
-  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>(), PL = R * WW;
+  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>();
   // loads for step + A: window row y0 + NW*A + M + w, flow row y0 + NW*A + w
   warp_ring_load(ahead, a, nb, rowb, y0 + NW * kWarpAhead + M + w, xs);
   warp_flow_load(ahead, a, nb, rowb, y0 + NW * kWarpAhead + w, xcb);
   __builtin_amdgcn_sched_barrier(0);
   // window row y0 + M + w enters the ring: centeredGradient at each clamped slot
-  float *dst = ring + ((y0 + M + w) & (R - 1)) * WW;
-  dst[lane] = cur.c0;
-  dst[PL + lane] = 0.5f * (cur.r0 - cur.l0);
-  dst[2 * PL + lane] = 0.5f * (cur.s0 - cur.n0);
-  if (lane < 2 * M) {
-    dst[64 + lane] = cur.c1;
-    dst[PL + 64 + lane] = 0.5f * (cur.r1 - cur.l1);
-    dst[2 * PL + 64 + lane] = 0.5f * (cur.s1 - cur.n1);
-  }
+  warp_ring_put<M, NW>(ring, cur, y0 + M + w, lane);
   if (NW > 1) lds_barrier();   // (a wave's own LDS accesses execute in order)
   const int x = x0 + lane, y = y0 + w;
   const float wx = (float)x + cur.u1;
@@ -598,8 +610,8 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
   if (inwin) {
     warp_gather_fn(
         [&](int cy, int cx) {
-          const float *p = ring + (cy & (R - 1)) * WW + (cx - (x0 - M));
-          return Tap3{p[0], p[PL], p[2 * PL]};
+          const float *p = ring + (cy & (R - 1)) * (3 * WW) + (cx - (x0 - M));
+          return Tap3{p[0], p[WW], p[2 * WW]};
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
   } else {
@@ -627,6 +639,7 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
 template <int M, int NW>
 __global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
   constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>(), PL = R * WW;
+  static_assert(3 * WW < 256, "one tap row within ds_read2_b32 offsets");
   static_assert(2 * NW + 2 * M <= R, "ring too small for the margin");
   static_assert(2 * M <= 64, "second window slot per lane");
   __shared__ float ring[3 * PL];
@@ -660,17 +673,7 @@ __global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
 #pragma unroll
     for (int i = 0; i < PR; ++i) {
       const int r = ys - M + w + NW * i;
-      if (r < ys + M) {
-        float *dst = ring + (r & (R - 1)) * WW;
-        dst[lane] = t[i].c0;
-        dst[PL + lane] = 0.5f * (t[i].r0 - t[i].l0);
-        dst[2 * PL + lane] = 0.5f * (t[i].s0 - t[i].n0);
-        if (lane < 2 * M) {
-          dst[64 + lane] = t[i].c1;
-          dst[PL + 64 + lane] = 0.5f * (t[i].r1 - t[i].l1);
-          dst[2 * PL + 64 + lane] = 0.5f * (t[i].s1 - t[i].n1);
-        }
-      }
+      if (r < ys + M) warp_ring_put<M, NW>(ring, t[i], r, lane);
     }
   }
   static_assert(kWarpAhead == 2, "the step loop below is unrolled for a 3-row ring");

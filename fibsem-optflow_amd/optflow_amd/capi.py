@@ -138,7 +138,8 @@ def load_oracle() -> C.CDLL:
 def load_engine() -> C.CDLL:
     """The product: libtvl1_hip.so (HIP kernels for gfx950 + C-ABI).  Raises
     if it was not built — there is no CPU fallback."""
-    lib = Library(ENGINE_SO).lib
+    # TVL1_ENGINE_SO: another build of the same engine (A/B runs of tools/ab_lib.sh)
+    lib = Library(Path(os.environ.get("TVL1_ENGINE_SO", ENGINE_SO))).lib
     lib.tvl1_params_default.argtypes = [C.POINTER(TVL1Params)]
     lib.tvl1_params_default.restype = None
     lib.tvl1_create.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.POINTER(TVL1Params)]
