@@ -83,6 +83,7 @@ struct tvl1_ctx {
                              // 0 = k_warp_img (gradient built in LDS from I1), 1 = k_warp (global)
   int warp_roll_slots[8][5] = {};   // resident k_warp_roll<M, NW> blocks per device
   int warp_ring_slots[8][5] = {};   // resident k_warp_ring<M, NW> blocks per device
+  size_t buf_limit = ((size_t)1 << 31) - 4096;   // plane bytes the buffer-addressed kernels take
   int fuse_first = 0;        // warpBackward fused into each warp's first pass (k_warp_pass; opt-in: slower)
   int fuse_slots[8] = {};    // resident k_warp_pass<M> wavefronts per device
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
@@ -394,8 +395,15 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   int64_t checks = 0, spec_miss = 0;
 
   // ---- launch helpers
-  auto gradient = [&](int s) -> tvl1_status {  // interleaved G plane for warp modes 1, 2
-    if (c->warp_mode == 0 || c->warp_mode == 4) return TVL1_OK;   // derived from I1 in LDS
+  // Buffer-addressed kernels (k_iterate_roll, k_warp_ring, k_warp_pass) take 32-bit byte
+  // offsets: a level whose planes reach c->buf_limit bytes uses the 64-bit-addressed ones.
+  auto buffer_ok = [&](int s) {
+    return (size_t)g.ps[s] * g.hs[s] * sizeof(float) < c->buf_limit;
+  };
+  auto warp_mode_of = [&](int s) { return c->warp_mode == 4 && !buffer_ok(s) ? 2 : c->warp_mode; };
+  auto gradient = [&](int s) -> tvl1_status {  // interleaved G plane for warp modes 1, 2, 3
+    const int wm = warp_mode_of(s);
+    if (wm == 0 || wm == 4) return TVL1_OK;     // derived from I1 in LDS
     const int lw = g.ws[s], lh = g.hs[s];
     size_t t0 = prof_begin(c, st);
     hipLaunchKernelGGL(k_gradient, grid2(lw, lh), kBlk2, 0, st, c->I1s[s], lw, lh, g.ps[s], c->G);
@@ -406,12 +414,13 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   auto gather = [&](int s, int uset, int cbuf, int wp) -> tvl1_status {  // K5 warpBackward
     const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
     size_t t0 = prof_begin(c, st);
-    if (c->warp_mode == 0) {
+    const int wm = warp_mode_of(s);
+    if (wm == 0) {
       const int tx = (lw + kWarpTW - 1) / kWarpTW, ty = (lh + kWarpTH - 1) / kWarpTH;
       hipLaunchKernelGGL(k_warp_img, dim3(tx * ty), dim3(256), 0, st, c->I0s[s], c->I1s[s],
                          c->U[uset][0], c->U[uset][1], lw, lh, P, tx, c->C[cbuf][0],
                          c->C[cbuf][1], c->C[cbuf][2]);
-    } else if (c->warp_mode == 3) {
+    } else if (wm == 3) {
       WarpRollArgs wa;
       wa.I0 = c->I0s[s];
       wa.G = c->G;
@@ -440,7 +449,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         if (NW == 1) WARP_ROLL(6, 1) else if (NW == 4) WARP_ROLL(6, 4) else WARP_ROLL(6, 2)
       }
 #undef WARP_ROLL
-    } else if (c->warp_mode == 4) {
+    } else if (wm == 4) {
       WarpRingArgs wa;
       wa.I0 = c->I0s[s];
       wa.I1 = c->I1s[s];
@@ -468,7 +477,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         if (NW == 1) WARP_RING(6, 1) else if (NW == 4) WARP_RING(6, 4) else WARP_RING(6, 2)
       }
 #undef WARP_RING
-    } else if (c->warp_mode == 1) {
+    } else if (wm == 1) {
       hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[uset][0],
                          c->U[uset][1], lw, lh, P, c->C[cbuf][0], c->C[cbuf][1], c->C[cbuf][2]);
     } else {
@@ -488,7 +497,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     }
     // algorithmic: 40 B/px per warp
     prof_end(c, st, t0, 1, (double)lw * lh * 40.0,
-             (double)lw * lh * (c->warp_mode == 0 || c->warp_mode == 4 ? 28.0 : 40.0));
+             (double)lw * lh * (wm == 0 || wm == 4 ? 28.0 : 40.0));
     DIAG(c, st, "warp kernel", s, wp, -1);
     return TVL1_OK;
   };
@@ -538,7 +547,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     // x-only halo; passes of >= 3 iterations are VALU-bound, where the roll kernel wins
     // only while the level has enough rows for one round of >= 32-row segments (short
     // segments repeat the 2K-row halo) and k_iterate_tb (64 x 32, 2 px/lane) wins below.
-    const bool roll_ok = (size_t)P * lh * sizeof(float) < ((size_t)1 << 31) - 4096;
+    const bool roll_ok = buffer_ok(s);
     const bool roll_all = roll_ok && c->iter_mode == 2;
     const bool roll_short = roll_ok && c->iter_mode == 3;
     const bool roll_long = roll_short &&
@@ -864,6 +873,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_WARP_MARGIN")) c->warp_margin = atoi(m);
   if (const char *m = getenv("TVL1_WARP_NW")) c->warp_nw = atoi(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse_first = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_BUF_LIMIT"))   // tests: force the 64-bit-addressed kernels
+    c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_TB_CFG_LONG")) c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
