@@ -379,7 +379,8 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": (f"C2: one {W}x{H} u8 slice pair per GPU per step, nscales "
+            "workload": (("C2" if (W, H, args.nscales, args.warps) == (6144, 4096, 5, 30)
+                          else "pair") + f": one {W}x{H} u8 slice pair per GPU per step, nscales "
                          f"{args.nscales}, warps {args.warps}, iterations {args.iterations}, "
                          f"epsilon {args.epsilon} (reference defaults otherwise)"),
             "pair": f"{W}x{H}",
