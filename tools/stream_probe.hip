@@ -65,6 +65,63 @@ __global__ __launch_bounds__(256) void probe(Planes pl, int bands, int seg) {
   }
 }
 
+// Same bytes, but R rows are loaded, then R rows stored (stores in bursts per wave).
+template <int R>
+__global__ __launch_bounds__(256) void probe_burst(Planes pl, int bands, int seg) {
+  constexpr int NIN = 9, NOUT = 6;
+  typedef unsigned long long V;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int band = wid % bands, sg = wid / bands;
+  const int X = band * 124 - 4 + 2 * lane;
+  const unsigned vo = 4u * (unsigned)min(max(X, 0), P - 2);
+  const int y0 = sg * seg, y1 = min(y0 + seg + 4, H);
+  V d[R][NIN];
+  for (int y = y0; y < y1; y += R) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int k = 0; k < NIN; ++k)
+        d[r][k] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(rs(pl.in[k]), (int)vo, (int)(4u * P * min(y + r, H - 1)), 0));
+    __builtin_amdgcn_sched_barrier(0);
+    const bool okl = 2 * lane >= 4 && 2 * lane < 124;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int k = 0; k < NOUT; ++k) {
+        V v = d[r][k] ^ d[r][(k + 3) % NIN];
+        using T = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs(pl.in[0]), 0, 0, 0));
+        const int o = okl && y + r < y1 ? (int)(vo + 4u * P * (y + r)) : 0x7ffffff0;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(T, v), rs(pl.out[k]), o, 0, 0);
+      }
+  }
+}
+
+template <int R>
+void run_burst(const Planes &pl) {
+  const int bands = (W + 123) / 124;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (int seg : {64, 128}) {
+    const int waves = bands * ((H + seg - 1) / seg);
+    float best = 1e30f;
+    for (int rep = 0; rep < 4; ++rep) {
+      (void)hipEventRecord(e0);
+      hipLaunchKernelGGL((probe_burst<R>), dim3((waves + 3) / 4), dim3(256), 0, 0, pl, bands, seg);
+      (void)hipEventRecord(e1);
+      (void)hipEventSynchronize(e1);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (rep) best = ms < best ? ms : best;
+    }
+    const double rows = (double)bands * 128 * ((double)H + 4.0 * ((H + seg - 1) / seg));
+    const double bytes = rows * 4 * 9 + (double)W * H * 4 * 6;
+    printf("burst R=%d b64 9 in 6 out   seg %3d waves %5d: %7.1f us %6.0f GB/s\n", R, seg, waves,
+           best * 1e3, bytes / (best * 1e-3) / 1e9);
+  }
+}
+
 template <int B, int NIN, int NOUT>
 void run(const Planes &pl, const char *name) {
   constexpr int PX = B / 4, OUT = 64 * PX - 4;
@@ -100,5 +157,9 @@ int main() {
   run<16, 9, 6>(pl, "4px b128 9 planes in, 6 out");
   run<16, 5, 3>(pl, "2px-pairs b128 5 in, 3 out");
   run<8, 5, 3>(pl, "1px-pairs b64 5 in, 3 out");
+  run_burst<1>(pl);
+  run_burst<2>(pl);
+  run_burst<4>(pl);
+  run_burst<8>(pl);
   return 0;
 }
