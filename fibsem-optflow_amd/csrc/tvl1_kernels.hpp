@@ -907,7 +907,9 @@ __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rh
   const float Ix2 = I1wxv * I1wxv;
   const float Iy2 = I1wyv * I1wyv;
   const float gradv = Ix2 + Iy2;
-  const float rho = rhoc + (I1wxv * u1o + I1wyv * u2o) + a.gamma * (G ? u3o : 0.0f);
+  // gamma*u3 inside the parentheses (with gamma = 0 either association gives
+  // the same bits, signed zeros included)
+  const float rho = rhoc + (I1wxv * u1o + I1wyv * u2o + a.gamma * (G ? u3o : 0.0f));
   // TH operator, branch-free: the three candidate steps are computed with the
   // reference's exact expressions and the applicable one selected.
   const bool lo = rho < -a.l_t * gradv;
@@ -919,10 +921,10 @@ __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rh
   float d3 = mid ? fi * a.gamma : 0.0f;
   d1 = hi ? -a.l_t * I1wxv : d1;
   d2 = hi ? -a.l_t * I1wyv : d2;
-  d3 = hi ? -a.theta * a.gamma : d3;
+  d3 = hi ? -a.l_t * a.gamma : d3;     // +-l_t*gamma
   d1 = lo ? a.l_t * I1wxv : d1;
   d2 = lo ? a.l_t * I1wyv : d2;
-  d3 = lo ? a.theta * a.gamma : d3;
+  d3 = lo ? a.l_t * a.gamma : d3;
   const float v1 = u1o + d1;
   const float v2 = u2o + d2;
   const float div1 = divergence(p11, p11l, p12, p12u, x, y);

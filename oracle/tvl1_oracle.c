@@ -203,16 +203,18 @@ double orc_estimate_u(const float *I1wx, const float *I1wy, const float *grad,
       const float u1o = u1[i];
       const float u2o = u2[i];
       const float u3o = gamma != 0.0f ? u3[i] : 0.0f;
-      const float rho = rho_c[i] + (I1wxv * u1o + I1wyv * u2o) + gamma * u3o;
+      /* rho = rho_c + (I1wx*u1 + I1wy*u2 + gamma*u3) -- gamma*u3 inside the
+       * parentheses (with gamma = 0 either association gives the same bits) */
+      const float rho = rho_c[i] + (I1wxv * u1o + I1wyv * u2o + gamma * u3o);
       float d1 = 0.0f, d2 = 0.0f, d3 = 0.0f;
       if (rho < -l_t * gradv) {
         d1 = l_t * I1wxv;
         d2 = l_t * I1wyv;
-        if (gamma != 0.0f) d3 = theta * gamma;
+        if (gamma != 0.0f) d3 = l_t * gamma;       /* +-l_t*gamma */
       } else if (rho > l_t * gradv) {
         d1 = -l_t * I1wxv;
         d2 = -l_t * I1wyv;
-        if (gamma != 0.0f) d3 = -theta * gamma;
+        if (gamma != 0.0f) d3 = -l_t * gamma;
       } else if (gradv > FLT_EPSILON) {
         const float fi = -rho / gradv;
         d1 = fi * I1wxv;
