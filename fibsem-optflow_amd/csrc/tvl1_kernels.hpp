@@ -69,8 +69,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *p, uns
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)bytes, 0x00020000);
 }
 constexpr unsigned kOOB = 0x7ffffff0u;   // byte offset beyond every plane: store dropped
+#ifndef TVL1_STORE_AUX
+#define TVL1_STORE_AUX 2
+#endif
+constexpr int kWarpStoreAux = TVL1_STORE_AUX;   // cache policy of warp constant stores (2 = nt)
+template <int AUX = 0>
 __device__ __forceinline__ void bstore(float *p, unsigned bytes, unsigned voff, unsigned soff, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), plane_rsrc(p, bytes), (int)voff, (int)soff, AUX);
 }
 // PX consecutive floats of a plane (4- or 8-byte store)
 template <int PX>
@@ -631,9 +636,9 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
   const unsigned vo = x < a.W && y < ye ? (unsigned)y * rowb + 4u * (unsigned)x : kOOB;
-  bstore(a.I1wx, nb, vo, 0, I1wxv);
-  bstore(a.I1wy, nb, vo, 0, I1wyv);
-  bstore(a.rho, nb, vo, 0, I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0);
+  bstore<kWarpStoreAux>(a.I1wx, nb, vo, 0, I1wxv);
+  bstore<kWarpStoreAux>(a.I1wy, nb, vo, 0, I1wyv);
+  bstore<kWarpStoreAux>(a.rho, nb, vo, 0, I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0);
 }
 
 template <int M, int NW>
