@@ -62,8 +62,8 @@ struct tvl1_ctx {
   float *outu = nullptr, *outv = nullptr;
   double *partials = nullptr;
   int partials_cap = 0;
-  double *red = nullptr;
-  double *pinned = nullptr;  // host-pinned residual landing slot
+  double *pinned = nullptr;      // host-pinned residual landing slot (coherent, mapped)
+  double *pinned_dev = nullptr;  // its device address: k_reduce stores the residual there
   hipEvent_t ev_check = nullptr;  // recorded after each residual copy
   int speculate = 0;         // TVL1_SPECULATE=1 enables speculative enqueueing (measured slower)
   int iter_mode = 3;         // 0 = temporally blocked passes, 1 = one iteration per launch,
@@ -241,7 +241,7 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
   const int tb_blocks = ((W + 55) / 56) * ((H + 23) / 24);
   const int roll_waves = ((W + 55) / 56) * ((H + kRollMinSeg - 1) / kRollMinSeg);
   const int nblk = std::max(std::max(iterate_blocks(W, H), tb_blocks), roll_waves) + 64;
-  bytes += align_up((size_t)nblk * sizeof(double), 256) + 256;
+  bytes += align_up((size_t)nblk * sizeof(double), 256);
   bytes += 4096;                            // alignment slack
 
   if (bytes > c->arena_bytes) {
@@ -288,7 +288,6 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
   c->outv = (float *)take(plane);
   c->partials = (double *)take((size_t)nblk * sizeof(double));
   c->partials_cap = nblk;
-  c->red = (double *)take(256);
   c->geo = g;
   c->geo_valid = true;
   return TVL1_OK;
@@ -727,8 +726,10 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         pi ^= 1;
         n += k;
         if (calc_end) {
-          hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, blocks, c->red);
-          HIP_TRY(c, hipMemcpyAsync(c->pinned, c->red, sizeof(double), hipMemcpyDeviceToHost, st));
+          // the residual lands in coherent host memory (no copy launch); the event below
+          // orders the host's read after the kernel
+          hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, blocks,
+                             c->pinned_dev);
           HIP_TRY(c, hipEventRecord(c->ev_check, st));
           // enqueue what follows if this check ends the warp (see the comment above)
           int spec = 0;  // 1 = next warp's gather, 2 = next level's upsample/gradient/gather
@@ -883,7 +884,9 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_WARP_MODE")) c->warp_mode = atoi(m);
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void **)&c->pinned, sizeof(double) * 8, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&c->pinned, sizeof(double) * 8,
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&c->pinned_dev, c->pinned, 0) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_check, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return set_err(nullptr, TVL1_EHIP, "HIP initialisation failed on device %d", device);
