@@ -71,7 +71,9 @@ struct tvl1_ctx {
                              // 3 = hybrid: roll for passes of >= 3 iterations on large levels
   int roll_seg = 0;          // k_iterate_roll rows per segment (0 = auto, see roll_segment)
   int roll_px = 2;           // px per lane of k_iterate_roll (1 or 2)
-  int roll_slots[kRollMax + 1][2][3] = {};   // resident k_iterate_roll<G, K, PX> wavefronts
+  int roll_px_short = 4;     // px per lane of k_iterate_roll for passes of <= 2 iterations (1, 2, 4)
+  long roll_px4_min = 5000000;   // ... on levels of at least this many px (2 px below: more waves)
+  int roll_slots[kRollMax + 1][2][5] = {};   // resident k_iterate_roll<G, K, PX> wavefronts
   int roll_lds = 0;          // experiment: dummy dynamic LDS per k_iterate_roll block (bytes)
   int roll_fill = 100;       // % of the resident slots one streaming launch is sized for
   int warp_fill = 100;
@@ -644,7 +646,9 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         } else if (roll_all || (roll_short && k <= 2) || (roll_long && k >= 3)) {
           RollArgs ra;
           ra.it = a;
-          const int px = c->roll_px;
+          const int px = k > 2 ? c->roll_px
+                         : c->roll_px_short == 4 && (long)lw * lh < c->roll_px4_min ? 2
+                                                                                   : c->roll_px_short;
           const int halo = (k + px - 1) / px * px;   // roll_halo<K, PX>
           const int out_w = 64 * px - 2 * halo;
           ra.bands = (lw + out_w - 1) / out_w;
@@ -664,7 +668,13 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   else                                                                                         \
     hipLaunchKernelGGL((k_iterate_roll<false, K, PX>), dim3((ra.waves + 3) / 4), dim3(256),    \
                        c->roll_lds, st, ra);
-          if (px == 1) {
+          if (px == 4) {   // k <= 2
+            if (k == 1) {
+              ROLL_LAUNCH(1, 4)
+            } else {
+              ROLL_LAUNCH(2, 4)
+            }
+          } else if (px == 1) {
             switch (k) {
               case 1: ROLL_LAUNCH(1, 1) break;
               case 2: ROLL_LAUNCH(2, 1) break;
@@ -867,7 +877,12 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   }
   if (const char *m = getenv("TVL1_ROLL_SEG")) c->roll_seg = atoi(m);
   if (const char *m = getenv("TVL1_ROLL_LDS")) c->roll_lds = std::max(0, atoi(m));
-  if (const char *m = getenv("TVL1_ROLL_PX")) c->roll_px = atoi(m) == 1 ? 1 : 2;
+  if (const char *m = getenv("TVL1_ROLL_PX")) c->roll_px = c->roll_px_short = atoi(m) == 1 ? 1 : 2;
+  if (const char *m = getenv("TVL1_ROLL_PX_SHORT")) {
+    const int v = atoi(m);
+    c->roll_px_short = v == 1 ? 1 : v == 4 ? 4 : 2;
+  }
+  if (const char *m = getenv("TVL1_ROLL_PX4_MIN")) c->roll_px4_min = atol(m);
   if (const char *m = getenv("TVL1_ROLL_FILL")) c->roll_fill = std::max(10, atoi(m));
   if (const char *m = getenv("TVL1_WARP_FILL")) c->warp_fill = std::max(10, atoi(m));
   if (const char *m = getenv("TVL1_WARP_LDS")) c->warp_lds = std::max(0, atoi(m));
@@ -905,6 +920,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     ROLL_SLOTS(true, 1, 1) ROLL_SLOTS(true, 2, 1) ROLL_SLOTS(true, 3, 1) ROLL_SLOTS(true, 4, 1)
     ROLL_SLOTS(false, 1, 2) ROLL_SLOTS(false, 2, 2) ROLL_SLOTS(false, 3, 2) ROLL_SLOTS(false, 4, 2)
     ROLL_SLOTS(true, 1, 2) ROLL_SLOTS(true, 2, 2) ROLL_SLOTS(true, 3, 2) ROLL_SLOTS(true, 4, 2)
+    ROLL_SLOTS(false, 1, 4) ROLL_SLOTS(false, 2, 4) ROLL_SLOTS(true, 1, 4) ROLL_SLOTS(true, 2, 4)
 #undef ROLL_SLOTS
     auto blocks_of = [&](const void *fn, int threads) {
       int nb = 0;

@@ -77,11 +77,16 @@ template <int AUX = 0>
 __device__ __forceinline__ void bstore(float *p, unsigned bytes, unsigned voff, unsigned soff, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), plane_rsrc(p, bytes), (int)voff, (int)soff, AUX);
 }
-// PX consecutive floats of a plane (4- or 8-byte store)
+// PX consecutive floats of a plane (4-, 8- or 16-byte store)
 template <int PX>
 __device__ __forceinline__ void bstorev(float *p, unsigned bytes, unsigned voff, const float (&v)[PX]) {
   if constexpr (PX == 1) {
     bstore(p, bytes, voff, 0, v[0]);
+  } else if constexpr (PX == 4) {
+    using T = decltype(__builtin_amdgcn_raw_buffer_load_b128(plane_rsrc(p, bytes), 0, 0, 0));
+    T t;
+    __builtin_memcpy(&t, v, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(t, plane_rsrc(p, bytes), (int)voff, 0, 0);
   } else {
     using T = decltype(__builtin_amdgcn_raw_buffer_load_b64(plane_rsrc(p, bytes), 0, 0, 0));
     T t;
@@ -89,14 +94,18 @@ __device__ __forceinline__ void bstorev(float *p, unsigned bytes, unsigned voff,
     __builtin_amdgcn_raw_buffer_store_b64(t, plane_rsrc(p, bytes), (int)voff, 0, 0);
   }
 }
-// PX consecutive floats of a plane (4- or 8-byte load)
+// PX consecutive floats of a plane (4-, 8- or 16-byte load)
 template <int PX>
 __device__ __forceinline__ void bload(float (&d)[PX], const float *p, unsigned bytes, unsigned voff,
                                       unsigned soff) {
   if constexpr (PX == 1) {
     d[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(plane_rsrc(p, bytes), (int)voff, (int)soff, 0));
+  } else if constexpr (PX == 4) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
+    static_assert(sizeof(v) == 16, "b128 load");
+    __builtin_memcpy(d, &v, 16);
   } else {
-    static_assert(PX == 2, "1 or 2 px per lane");
+    static_assert(PX == 2, "1, 2 or 4 px per lane");
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
     static_assert(sizeof(v) == 8, "b64 load");
     __builtin_memcpy(d, &v, 8);
@@ -1302,6 +1311,10 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
 // (bit-identical results).
 constexpr int kRollMax = 4;
 constexpr int kRollAhead = 2;   // input rows loaded ahead of the row entering the pipeline
+// rows loaded ahead by k_iterate_roll<.., PX>: 16-byte loads (PX = 4) keep as many bytes in
+// flight one row ahead as 8-byte loads two rows ahead, with one ring row less
+template <int PX>
+constexpr int roll_ahead() { return PX == 4 ? 1 : kRollAhead; }
 
 struct RollArgs {
   IterArgs it;
@@ -1398,9 +1411,9 @@ __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G,
                                           RollIn<G, PX> &ahead, const IterArgs &a, int r,
                                           const RollLane &L, unsigned nb, unsigned rowb,
                                           double &acc) {
-  roll_load<G, PX>(ahead, a, nb, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vload);
-  // keep the loads of row r + kRollAhead ahead of this step's stores: waiting for them
-  // kRollAhead steps later then leaves the younger stores and loads in flight (vmcnt
+  roll_load<G, PX>(ahead, a, nb, (unsigned)imin(r + roll_ahead<PX>(), a.H - 1) * rowb, L.vload);
+  // keep the loads of row r + roll_ahead ahead of this step's stores: waiting for them
+  // roll_ahead steps later then leaves the younger stores and loads in flight (vmcnt
   // counts in issue order)
   __builtin_amdgcn_sched_barrier(0);
   roll_advance<G, K, PX>(S, in, a, r, L, nb, rowb, acc);
@@ -1519,8 +1532,6 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
   L.ys = seg * ra.seg_rows;
   L.ye = imin(L.ys + ra.seg_rows, a.H);
   const int r0 = imax(L.ys - K, 0);
-  // steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K (rows >= H drain the pipeline)
-  const int thirds = (L.ye + K - r0 + 2) / 3;
 
   RollPipe<G, K, PX> S;
 #pragma unroll
@@ -1556,17 +1567,30 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
       bstorev<PX>(a.p32d, nb, kOOB, z);
     }
   };
-  static_assert(kRollAhead == 2, "the step loop below is unrolled for a 3-row ring");
-  RollIn<G, PX> A, B, C;
-  roll_load<G, PX>(A, a, nb, (unsigned)r0 * rowb, L.vload);
-  dummy_stores();
-  roll_load<G, PX>(B, a, nb, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
-  dummy_stores();
   double acc = 0.0;
-  for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
-    roll_step<G, K, PX>(S, A, C, a, r, L, nb, rowb, acc);
-    roll_step<G, K, PX>(S, B, A, a, r + 1, L, nb, rowb, acc);
-    roll_step<G, K, PX>(S, C, B, a, r + 2, L, nb, rowb, acc);
+  if constexpr (roll_ahead<PX>() == 1) {   // 2-row ring, steps unrolled by 2
+    RollIn<G, PX> A, B;
+    roll_load<G, PX>(A, a, nb, (unsigned)r0 * rowb, L.vload);
+    dummy_stores();
+    const int halves = (L.ye + K - r0 + 1) / 2;
+    for (int h = 0, r = r0; h < halves; ++h, r += 2) {
+      roll_step<G, K, PX>(S, A, B, a, r, L, nb, rowb, acc);
+      roll_step<G, K, PX>(S, B, A, a, r + 1, L, nb, rowb, acc);
+    }
+  } else {   // 3-row ring, steps unrolled by 3
+    static_assert(roll_ahead<PX>() == 2, "the step loop below is unrolled for a 3-row ring");
+    RollIn<G, PX> A, B, C;
+    roll_load<G, PX>(A, a, nb, (unsigned)r0 * rowb, L.vload);
+    dummy_stores();
+    roll_load<G, PX>(B, a, nb, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
+    dummy_stores();
+    // steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K (rows >= H drain the pipeline)
+    const int thirds = (L.ye + K - r0 + 2) / 3;
+    for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
+      roll_step<G, K, PX>(S, A, C, a, r, L, nb, rowb, acc);
+      roll_step<G, K, PX>(S, B, A, a, r + 1, L, nb, rowb, acc);
+      roll_step<G, K, PX>(S, C, B, a, r + 2, L, nb, rowb, acc);
+    }
   }
   if (a.calc_err) {
 #pragma unroll

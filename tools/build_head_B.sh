@@ -1,0 +1,10 @@
+# Builds the engine as committed at a git revision (default HEAD) into ab_B/, for
+# tools/ab_lib.sh A/B runs of the working tree against it.
+set -e
+REV=${1:-HEAD}
+T=$(mktemp -d)
+git archive "$REV" fibsem-optflow_amd/csrc include | tar -x -C "$T"
+mkdir -p ab_B
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall --offload-arch=gfx950 \
+  -shared -o ab_B/libtvl1_hip.so "$T/fibsem-optflow_amd/csrc/tvl1_engine.hip"
+rm -rf "$T"
