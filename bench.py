@@ -341,10 +341,12 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": TRAFFIC,
                 "kernel": "iteration passes: estimateU + estimateDualVariables + residual "
                           "partials, <= 4 iterations per HBM pass (k_iterate_roll wavefront "
-                          "pipeline / k_iterate_tb blocked regions, hybrid)",
+                          "pipeline / k_iterate_tb blocked regions, hybrid; on levels >= 5 Mpx "
+                          "each warp's first pass is k_warp_iter, warpBackward fused in)",
                 "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
                 "algorithmic_bytes_per_launch": round(k_bytes / k_launch),
-                "algorithmic_model": "SURVEY 8(d): 64 B/px per executed iteration",
+                "algorithmic_model": "SURVEY 8(d): 64 B/px per executed iteration "
+                                     "(+ 40 B/px for a fused warpBackward)",
                 # what this kernel must move with its temporal blocking (tile loads incl.
                 # halos + interior stores): the bandwidth-efficiency figure
                 "compulsory_bytes_per_launch": round(k_hbm / k_launch),

@@ -86,8 +86,13 @@ struct tvl1_ctx {
   int warp_roll_slots[8][5] = {};   // resident k_warp_roll<M, NW> blocks per device
   int warp_ring_slots[8][5] = {};   // resident k_warp_ring<M, NW> blocks per device
   size_t buf_limit = ((size_t)1 << 31) - 4096;   // plane bytes the buffer-addressed kernels take
-  int fuse_first = 0;        // warpBackward fused into each warp's first pass (k_warp_pass; opt-in: slower)
+  int fuse_first = 2;        // warpBackward fused into each warp's first pass: 1 = k_warp_pass
+                             // (opt-in: slower), 2 = k_warp_iter (levels >= fuse_min px)
+  long fuse_min = 5000000;   // smaller levels: k_warp_ring + the pass (as fast, and their
+                             // warps mostly run past the first check)
   int fuse_slots[8] = {};    // resident k_warp_pass<M> wavefronts per device
+  int witer_slots[8] = {};   // resident k_warp_iter<M> blocks per device
+  int fuse_store = 0;        // TVL1_FUSE_STORE=1: k_warp_iter always stores the constants
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
   int warp_th = 16;          // k_warp_lds tile height (8, 16, 32)
@@ -554,6 +559,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     const bool roll_long = roll_short &&
                            (long)((lw + 55) / 56) * ((lh + 31) / 32) >= c->roll_slots[4][gam][1];
 
+    int last_warp_n = -1;   // iterations of the level's previous warp
     for (int wp = 0; wp < prm.warps; ++wp) {
       if (median) {
         hipLaunchKernelGGL(k_median, grid2(lw, lh, 2), kBlk2, 0, st, c->U[ui][0], c->U[ui][1],
@@ -567,7 +573,9 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       // warpBackward fused into the warp's first pass (2 iterations ending in the first
       // check) when that pass would stream through k_iterate_roll anyway
       const bool fuse = c->fuse_first && !gam && !have_gather && roll_short &&
-                        prm.epsilon > 0 && prm.iterations >= 2;
+                        prm.epsilon > 0 && prm.iterations >= 2 &&
+                        (c->fuse_first == 1 || (long)lw * lh >= c->fuse_min);
+      bool fused_nostore = false;   // k_warp_iter ran without storing the constants
       if (!have_gather && !fuse) TRY(gather(s, ui, cb, wp));
       have_gather = false;
       a.I1wx = c->C[cb][0];
@@ -604,7 +612,45 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         const int nu = gam ? 3 : 2, np = gam ? 6 : 4;
         const double ld_planes = 3 + nu + (p_zero ? 0 : np), st_planes = nu + np;
         double alg_extra = 0.0;   // the fused warpBackward's algorithmic bytes
-        if (fuse && n == 0 && k == 2 && calc_end) {
+        if (fuse && c->fuse_first == 2 && n == 0 && k == 2 && calc_end) {
+          WarpIterArgs w;
+          w.ra.it = a;
+          w.ra.it.I1wx = c->C[cb][0];
+          w.ra.it.I1wy = c->C[cb][1];
+          w.ra.it.rho = c->C[cb][2];
+          w.I0 = c->I0s[s];
+          w.I1 = c->I1s[s];
+          // the constants go to HBM only when the warp may run further passes: always for
+          // a level's first warp, else when the previous warp did not stop at its first
+          // check (a wrong guess recomputes them with the warp kernel after the check)
+          w.store_c = c->fuse_store || wp == 0 || last_warp_n != 2;
+          fused_nostore = !w.store_c;
+          const int M = c->warp_margin == 4 ? 4 : 6;
+          w.ra.bands = (lw + 123) / 124;
+          const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
+                                          : roll_segment(w.ra.bands, lh, 2 + M, c->witer_slots[M]);
+          w.ra.seg_rows = seg;
+          const int segs = (lh + seg - 1) / seg;
+          w.ra.waves = w.ra.bands * segs;
+          blocks = w.ra.waves;
+          if (blocks > c->partials_cap)
+            return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
+                           c->partials_cap);
+          if (M == 4)
+            hipLaunchKernelGGL(k_warp_iter<4>, dim3(w.ra.waves), dim3(192), 0, st, w);
+          else
+            hipLaunchKernelGGL(k_warp_iter<6>, dim3(w.ra.waves), dim3(192), 0, st, w);
+          // compulsory: p, u, I0 and the I1 window (x 1 + 2M/128) per band column and row;
+          // u, p (+ the constants) stored
+          double rows = 0.0;
+          for (int sg = 0; sg < segs; ++sg) {
+            const int ys = sg * seg, ye = std::min(ys + seg, lh);
+            rows += std::min(ye - 1 + 2, lh - 1) - std::max(ys - 2, 0) + 1;
+          }
+          hbm = (double)w.ra.bands * 128.0 * rows * 4.0 * ((p_zero ? 3 : 7) + (128.0 + 2 * M) / 128.0) +
+                Nl * 4.0 * (6.0 + (w.store_c ? 3.0 : 0.0));
+          alg_extra = Nl * 40.0;   // 40 B/px per warp
+        } else if (fuse && n == 0 && k == 2 && calc_end) {
           WarpPassArgs w;
           w.ra.it = a;
           w.ra.it.I1wx = c->C[cb][0];
@@ -761,6 +807,10 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           prevError = error;
           ++checks;
           const bool ends = !(error > scaledEps && n < prm.iterations);
+          // k_warp_iter guessed that this warp stops here; it continues: compute its
+          // constants (from its input u, the set the pass just read) before the next pass
+          if (fused_nostore && !ends) TRY(gather(s, ui ^ 1, cb, wp));
+          fused_nostore = false;
           if (spec && !ends) ++spec_miss;
           if (spec == 1 && ends) have_gather = true;
           if (spec == 2 && ends) have_level = have_gather = true;
@@ -770,6 +820,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         }
       }
       level_iters[s] += n;
+      last_warp_n = n;
       if (stats && stats->warp_iterations && s * prm.warps + wp < stats->warp_iterations_capacity)
         stats->warp_iterations[s * prm.warps + wp] = n;
       cb ^= 1;  // every warp gets the other constants buffer
@@ -888,7 +939,9 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_WARP_LDS")) c->warp_lds = std::max(0, atoi(m));
   if (const char *m = getenv("TVL1_WARP_MARGIN")) c->warp_margin = atoi(m);
   if (const char *m = getenv("TVL1_WARP_NW")) c->warp_nw = atoi(m);
-  if (const char *m = getenv("TVL1_FUSE")) c->fuse_first = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_FUSE_STORE")) c->fuse_store = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
+  if (const char *m = getenv("TVL1_FUSE")) c->fuse_first = atoi(m) == 1 ? 1 : atoi(m) == 2 ? 2 : 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // tests: force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = c->tb_cfg_long = atoi(m);
@@ -942,6 +995,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
 #undef RING_SLOTS
     c->fuse_slots[4] = blocks_of((const void *)k_warp_pass<4>, 64);
     c->fuse_slots[6] = blocks_of((const void *)k_warp_pass<6>, 64);
+    c->witer_slots[4] = blocks_of((const void *)k_warp_iter<4>, 192);
+    c->witer_slots[6] = blocks_of((const void *)k_warp_iter<6>, 192);
     (void)hipGetLastError();
   }
   *out = c;

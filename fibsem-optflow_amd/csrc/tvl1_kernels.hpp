@@ -1797,6 +1797,287 @@ __global__ __launch_bounds__(64) void k_warp_pass(WarpPassArgs w) {
   }
 }
 
+// ---------------------------------------------------------------- K5 + first pass, two roles
+// k_warp_iter<M>: warpBackward and the warp's first pass (2 iterations ending in the first
+// check) in one launch, the two jobs on different wavefronts of a block.  A block owns one
+// k_iterate_roll<false, 2, 2> band (128 px: 124 output px + a 2-px halo each side) over a
+// segment of rows, with three wavefronts:
+//   * two producers run k_warp_ring's streaming warpBackward for the band's 128 columns
+//     of one row per step (64 each): an LDS ring of I1 window rows r-M .. r+M (slots
+//     x0-M .. x0+127+M, centeredGradient per slot), the same taps and order.  Each step
+//     they write the row's warp constants and u into a 2-row LDS C ring, and to HBM too
+//     when the warp may need further passes (store_c);
+//   * one consumer runs the k_iterate_roll<false, 2, 2> pipeline (roll_advance: the same
+//     arithmetic), taking each input row's constants and u from the C ring one step after
+//     the producers wrote it, and only p from HBM.
+// One LDS-only barrier per step orders the window row writes before the gathers and each
+// C ring row before its read (2 C ring rows: a row is overwritten two steps after it was
+// written, after the consumer's read at the step between).  The consumer's step is the
+// longer one; the producers' wait at the barrier is issue time for the other blocks'
+// wavefronts on the SIMD.  Against k_warp_ring + the pass, the constants (12 B/px stored
+// and loaded, unless store_c) and one u load (8 B/px) stay on chip, and the gather's LDS
+// latency hides behind the consumer's arithmetic.
+struct WarpIterArgs {
+  RollArgs ra;           // pass geometry (bands of 124 output px) and planes
+  const float *I0, *I1;  // level images
+  int store_c;           // also store I1wx / I1wy / rho (ra.it.I1wx, ...) for later passes
+};
+
+constexpr int kWiRows = 16;   // window ring rows
+constexpr int kWiBW = 128;    // band width (px): 64 consumer lanes x 2 px
+template <int M>
+constexpr int wi_ww() { return kWiBW + 2 * M; }
+
+// window row r enters the ring: slot 64p + lane, and (producer 0, lanes < 2M) 128 + lane
+template <int M>
+__device__ __forceinline__ void wi_ring_put(float *__restrict__ ring, const WarpRowI &v, int r,
+                                            int p, int lane) {
+  constexpr int WW = wi_ww<M>();
+  float *dst = ring + (r & (kWiRows - 1)) * (3 * WW);
+  const int k0 = 64 * p + lane;
+  dst[k0] = v.c0;
+  dst[WW + k0] = 0.5f * (v.r0 - v.l0);
+  dst[2 * WW + k0] = 0.5f * (v.s0 - v.n0);
+  if (p == 0 && lane < 2 * M) {
+    dst[kWiBW + lane] = v.c1;
+    dst[WW + kWiBW + lane] = 0.5f * (v.r1 - v.l1);
+    dst[2 * WW + kWiBW + lane] = 0.5f * (v.s1 - v.n1);
+  }
+}
+
+// Producer lane geometry: column xc (the lane's px, clamped into the image), window
+// column of slot 0 (xw0), C ring index ci, and whether the px is a stored output px.
+struct WiLane {
+  int xc, xw0, ci;
+  unsigned xcb;
+  bool outc;
+};
+
+template <int M>
+__device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__restrict__ cring,
+                                             const WarpRowI &cur, WarpRowI &ahead,
+                                             const WarpRingArgs &wa, const WarpIterArgs &w,
+                                             int g, int p, int lane, const WiLane &P,
+                                             const unsigned (&xs)[2][3], int ys, int ye,
+                                             unsigned nb, unsigned rowb) {
+  constexpr int WW = wi_ww<M>();
+  // loads for row g + kWarpAhead: window row g + kWarpAhead + M and its flow row
+  warp_ring_load(ahead, wa, nb, rowb, g + kWarpAhead + M, xs);
+  warp_flow_load(ahead, wa, nb, rowb, g + kWarpAhead, P.xcb);
+  __builtin_amdgcn_sched_barrier(0);
+  wi_ring_put<M>(ring, cur, g + M, p, lane);
+  lds_barrier();
+  // rows past the image bottom repeat row H-1 (the pass clamps its input rows)
+  const int gy = imin(g, wa.H - 1);
+  const float wx = (float)P.xc + cur.u1;
+  const float wy = (float)gy + cur.u2;
+  const int fx = tap_floor(wx);
+  const int fy = tap_floor(wy);
+  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
+  const bool inwin = fx - 1 >= P.xw0 && fx + 2 < P.xw0 + WW && fy - 1 >= gy - M && fy + 2 <= gy + M;
+  if (inwin) {
+    warp_gather_fn(
+        [&](int cy, int cx) {
+          const float *q = ring + (cy & (kWiRows - 1)) * (3 * WW) + (cx - P.xw0);
+          return Tap3{q[0], q[WW], q[2 * WW]};
+        },
+        wx, wy, fx, fy, sum, sumx, sumy, wsum);
+  } else {
+    warp_gather_fn(
+        [&](int cy, int cx) {
+          const int rx = imin(imax(cx, 0), wa.W - 1), ry = imin(imax(cy, 0), wa.H - 1);
+          const float *row = wa.I1 + (size_t)ry * wa.P;
+          const float gx = 0.5f * (row[imin(rx + 1, wa.W - 1)] - row[imax(rx - 1, 0)]);
+          const float gyv = 0.5f * (wa.I1[(size_t)imin(ry + 1, wa.H - 1) * wa.P + rx] -
+                                    wa.I1[(size_t)imax(ry - 1, 0) * wa.P + rx]);
+          return Tap3{row[rx], gx, gyv};
+        },
+        wx, wy, fx, fy, sum, sumx, sumy, wsum);
+  }
+  const float coeff = 1.0f / wsum;
+  const float I1wv = sum * coeff;
+  const float I1wxv = sumx * coeff;
+  const float I1wyv = sumy * coeff;
+  const float rh = I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0;
+  float *c = cring + (g & 1) * (5 * kWiBW) + P.ci;
+  c[0] = I1wxv;
+  c[kWiBW] = I1wyv;
+  c[2 * kWiBW] = rh;
+  c[3 * kWiBW] = cur.u1;
+  c[4 * kWiBW] = cur.u2;
+  if (w.store_c) {
+    const unsigned vo = P.outc && g >= ys && g < ye ? (unsigned)g * rowb + P.xcb : kOOB;
+    bstore<kWarpStoreAux>(wa.I1wx, nb, vo, 0, I1wxv);
+    bstore<kWarpStoreAux>(wa.I1wy, nb, vo, 0, I1wyv);
+    bstore<kWarpStoreAux>(wa.rho, nb, vo, 0, rh);
+  }
+}
+
+struct WiP {   // the consumer's HBM input of one row: p at its 2 px
+  float p11[2], p12[2], p21[2], p22[2];
+};
+
+__device__ __forceinline__ void wi_p_load(WiP &v, const IterArgs &a, unsigned nb, unsigned soff,
+                                          unsigned voff) {
+  bload<2>(v.p11, a.p11s, nb, voff, soff);
+  bload<2>(v.p12, a.p12s, nb, voff, soff);
+  bload<2>(v.p21, a.p21s, nb, voff, soff);
+  bload<2>(v.p22, a.p22s, nb, voff, soff);
+}
+
+__device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, 2> &S,
+                                             const float *__restrict__ cring, const WiP &cur,
+                                             WiP &ahead, const IterArgs &a, int r,
+                                             const RollLane &L, int lane, unsigned nb,
+                                             unsigned rowb, double &acc) {
+  wi_p_load(ahead, a, nb, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vload);
+  __builtin_amdgcn_sched_barrier(0);
+  lds_barrier();   // C ring row r was written at the previous step
+  RollIn<false, 2> in;
+  const float *c = cring + (r & 1) * (5 * kWiBW) + 2 * lane;
+  in.wx[0] = c[0]; in.wx[1] = c[1];
+  in.wy[0] = c[kWiBW]; in.wy[1] = c[kWiBW + 1];
+  in.rh[0] = c[2 * kWiBW]; in.rh[1] = c[2 * kWiBW + 1];
+  in.u1[0] = c[3 * kWiBW]; in.u1[1] = c[3 * kWiBW + 1];
+  in.u2[0] = c[4 * kWiBW]; in.u2[1] = c[4 * kWiBW + 1];
+  in.u3[0] = in.u3[1] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    in.p11[j] = cur.p11[j]; in.p12[j] = cur.p12[j];
+    in.p21[j] = cur.p21[j]; in.p22[j] = cur.p22[j];
+    in.p31[j] = in.p32[j] = 0.0f;
+  }
+  roll_advance<false, 2, 2>(S, in, a, r, L, nb, rowb, acc);
+}
+
+template <int M>
+__global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
+  constexpr int K = 2, PX = 2, HALO = roll_halo<2, 2>(), WW = wi_ww<M>();
+  static_assert(2 * M + 2 <= kWiRows, "window ring too small for the margin");
+  static_assert(2 * M <= 64, "second window slot per lane");
+  static_assert(kRollAhead == 2 && kWarpAhead == 2, "the step loops are unrolled by 3");
+  __shared__ float ring[kWiRows * 3 * WW];
+  __shared__ float cring[2 * 5 * kWiBW];
+  const RollArgs &ra = w.ra;
+  const IterArgs &a = ra.it;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
+  if (wid >= ra.waves) return;   // whole blocks
+  // wave 0 consumer, 1-2 producers (measured: a consumer on wave 1 or 2 of some blocks, or
+  // a raised s_setprio for it, is slower)
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int band = wid % ra.bands, seg = wid / ra.bands;
+  const int X0 = band * (kWiBW - 2 * HALO) - HALO;   // the band's first px
+  const unsigned nb = 4u * (unsigned)a.P * (unsigned)a.H;
+  const unsigned rowb = 4u * (unsigned)a.P;
+  const int ys = seg * ra.seg_rows, ye = imin(ys + ra.seg_rows, a.H);
+  const int r0 = imax(ys - K, 0);
+  // consumer steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K; the producers run one row ahead
+  // and 3 (thirds + 1) steps, the consumer 1 + 3 thirds + 2 barriers
+  const int thirds = (ye + K - r0 + 2) / 3;
+  if (wv == 0) {
+    RollLane L;
+    L.X = X0 + PX * lane;
+    L.vload = 4u * imin(imax(L.X, 0), a.P - PX);
+    L.out = PX * lane >= HALO && PX * lane < kWiBW - HALO && L.X < a.W;
+    L.vst = 4u * (unsigned)imax(L.X, 0);
+    L.ys = ys;
+    L.ye = ye;
+    RollPipe<false, K, PX> S;
+#pragma unroll
+    for (int n = 0; n <= K; ++n)
+#pragma unroll
+      for (int j = 0; j < PX; ++j) {
+        S.U1c[n][j] = S.U2c[n][j] = S.U3c[n][j] = S.U1p[n][j] = S.U2p[n][j] = S.U3p[n][j] = 0.0f;
+        S.P11c[n][j] = S.P12c[n][j] = S.P21c[n][j] = S.P22c[n][j] = S.P31c[n][j] = S.P32c[n][j] = 0.0f;
+        S.P11p[n][j] = S.P12p[n][j] = S.P21p[n][j] = S.P22p[n][j] = S.P31p[n][j] = S.P32p[n][j] = 0.0f;
+      }
+#pragma unroll
+    for (int n = 0; n < K; ++n)
+#pragma unroll
+      for (int j = 0; j < PX; ++j) S.CX[n][j] = S.CY[n][j] = S.CR[n][j] = 0.0f;
+    // as many dropped stores after each prologue load as a step issues (k_iterate_roll)
+    auto dummy_stores = [&]() {
+      float z[PX] = {0.0f, 0.0f};
+      bstorev<PX>(a.u1d, nb, kOOB, z);
+      bstorev<PX>(a.u2d, nb, kOOB, z);
+      bstorev<PX>(a.p11d, nb, kOOB, z);
+      bstorev<PX>(a.p12d, nb, kOOB, z);
+      bstorev<PX>(a.p21d, nb, kOOB, z);
+      bstorev<PX>(a.p22d, nb, kOOB, z);
+    };
+    WiP A, B, C;
+    wi_p_load(A, a, nb, (unsigned)r0 * rowb, L.vload);
+    dummy_stores();
+    wi_p_load(B, a, nb, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
+    dummy_stores();
+    lds_barrier();   // the producers' first step (row r0)
+    double acc = 0.0;
+    for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
+      wi_cons_step(S, cring, A, C, a, r, L, lane, nb, rowb, acc);
+      wi_cons_step(S, cring, B, A, a, r + 1, L, lane, nb, rowb, acc);
+      wi_cons_step(S, cring, C, B, a, r + 2, L, lane, nb, rowb, acc);
+    }
+    lds_barrier();   // the producers' last two steps
+    lds_barrier();
+    if (a.calc_err) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+      if (lane == 0) a.partials[wid] = acc;
+    }
+  } else {
+    const int p = wv - 1;
+    WarpRingArgs wa;
+    wa.I0 = w.I0;
+    wa.I1 = w.I1;
+    wa.u1 = a.u1s;
+    wa.u2 = a.u2s;
+    wa.I1wx = const_cast<float *>(a.I1wx);
+    wa.I1wy = const_cast<float *>(a.I1wy);
+    wa.rho = const_cast<float *>(a.rho);
+    wa.W = a.W;
+    wa.H = a.H;
+    wa.P = a.P;
+    WiLane P;
+    P.xw0 = X0 - M;
+    P.ci = 64 * p + lane;
+    const int px = X0 + P.ci;
+    P.xc = imin(imax(px, 0), a.W - 1);
+    P.xcb = 4u * (unsigned)P.xc;
+    P.outc = P.ci >= HALO && P.ci < kWiBW - HALO && px >= 0 && px < a.W;
+    // the lane's window slots (clamped column, its clamped x-1 and x+1): 64p + lane, and
+    // 128 + lane for producer 0's lanes < 2M (other lanes re-read the first slot)
+    unsigned xs[2][3];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int slot = k == 1 && p == 0 && lane < 2 * M ? kWiBW + lane : P.ci;
+      const int cc = imin(imax(P.xw0 + slot, 0), a.W - 1);
+      xs[k][0] = 4u * cc;
+      xs[k][1] = 4u * imax(cc - 1, 0);
+      xs[k][2] = 4u * imin(cc + 1, a.W - 1);
+    }
+    // ring prologue: window rows r0 - M .. r0 + M - 1, loads issued M rows at a time
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      WarpRowI t[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) warp_ring_load(t[i], wa, nb, rowb, r0 - M + b * M + i, xs);
+#pragma unroll
+      for (int i = 0; i < M; ++i) wi_ring_put<M>(ring, t[i], r0 - M + b * M + i, p, lane);
+    }
+    WarpRowI A, B, C;
+    warp_ring_load(A, wa, nb, rowb, r0 + M, xs);
+    warp_flow_load(A, wa, nb, rowb, r0, P.xcb);
+    warp_ring_load(B, wa, nb, rowb, r0 + 1 + M, xs);
+    warp_flow_load(B, wa, nb, rowb, r0 + 1, P.xcb);
+    for (int h = 0, g = r0; h <= thirds; ++h, g += 3) {
+      wi_prod_step<M>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
+    }
+  }
+}
+
 // K7: fixed-order sum of the per-block partials (one block).
 __global__ void k_reduce(const double *__restrict__ partials, int n, double *__restrict__ out) {
   __shared__ double s[kBlock];

@@ -65,8 +65,11 @@ def main():
     # kernel classes as bench.py / tvl1_stats report them: every iteration pass
     # (k_iterate_roll + k_iterate_tb of the hybrid) and every warpBackward
     classes = {}
+    # (k_warp_iter, warpBackward fused with a warp's first pass, is an iteration pass)
     for cls, prefix in (("iterate", "k_iterate"), ("warp", "k_warp")):
-        ks = [k for k in out if k.startswith(prefix)]
+        ks = [k for k in out if k.startswith(prefix) or (cls == "iterate" and k.startswith("k_warp_iter"))]
+        if cls == "warp":
+            ks = [k for k in ks if not k.startswith("k_warp_iter")]
         if not ks:
             continue
         n = sum(out[k]["dispatches"] for k in ks)
