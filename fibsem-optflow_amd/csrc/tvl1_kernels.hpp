@@ -907,17 +907,11 @@ __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float
   return y > 0 ? yhi : ylo;
 }
 
-// estimateU at one px (x, y): the TH step from the warp constants and u^{n-1}, then
-// u^n = v + theta * div(p^{n-1}).  pl = p*1 at x-1, pu = p*2 at y-1.  Shared by every
-// iteration kernel, so they all run exactly this sequence of IEEE float operations.
+// estimateU's TH step at one px: v = u^{n-1} + d from the warp constants (pointwise).
 template <bool G>
-__device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rhoc, float u1o,
-                                              float u2o, float u3o, float p11, float p11l,
-                                              float p12, float p12u, float p21, float p21l,
-                                              float p22, float p22u, float p31, float p31l,
-                                              float p32, float p32u, int x, int y,
-                                              const IterArgs &a, float &n1, float &n2,
-                                              float &n3) {
+__device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, float u1o, float u2o,
+                                      float u3o, const IterArgs &a, float &v1, float &v2,
+                                      float &v3) {
   const float Ix2 = I1wxv * I1wxv;
   const float Iy2 = I1wyv * I1wyv;
   const float gradv = Ix2 + Iy2;
@@ -939,17 +933,44 @@ __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rh
   d1 = lo ? a.l_t * I1wxv : d1;
   d2 = lo ? a.l_t * I1wyv : d2;
   d3 = lo ? a.l_t * a.gamma : d3;
-  const float v1 = u1o + d1;
-  const float v2 = u2o + d2;
+  v1 = u1o + d1;
+  v2 = u2o + d2;
+  v3 = G ? u3o + d3 : 0.0f;
+}
+
+// estimateU's second half at one px: u^n = v + theta * div(p^{n-1}).  pl = p*1 at x-1,
+// pu = p*2 at y-1.
+template <bool G>
+__device__ __forceinline__ void u_from_v(float v1, float v2, float v3, float p11, float p11l,
+                                         float p12, float p12u, float p21, float p21l,
+                                         float p22, float p22u, float p31, float p31l,
+                                         float p32, float p32u, int x, int y,
+                                         const IterArgs &a, float &n1, float &n2, float &n3) {
   const float div1 = divergence(p11, p11l, p12, p12u, x, y);
   const float div2 = divergence(p21, p21l, p22, p22u, x, y);
   n1 = v1 + a.theta * div1;
   n2 = v2 + a.theta * div2;
   if (G) {
-    const float v3 = u3o + d3;
     const float div3 = divergence(p31, p31l, p32, p32u, x, y);
     n3 = v3 + a.theta * div3;
   }
+}
+
+// estimateU at one px (x, y): the TH step from the warp constants and u^{n-1}, then
+// u^n = v + theta * div(p^{n-1}).  Shared by every iteration kernel, so they all run
+// exactly this sequence of IEEE float operations.
+template <bool G>
+__device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rhoc, float u1o,
+                                              float u2o, float u3o, float p11, float p11l,
+                                              float p12, float p12u, float p21, float p21l,
+                                              float p22, float p22u, float p31, float p31l,
+                                              float p32, float p32u, int x, int y,
+                                              const IterArgs &a, float &n1, float &n2,
+                                              float &n3) {
+  float v1, v2, v3;
+  th_px<G>(I1wxv, I1wyv, rhoc, u1o, u2o, u3o, a, v1, v2, v3);
+  u_from_v<G>(v1, v2, v3, p11, p11l, p12, p12u, p21, p21l, p22, p22u, p31, p31l, p32, p32u, x,
+              y, a, n1, n2, n3);
 }
 
 // estimateU for the PX px of this lane on row y.  up* = p12/p22/p32 of row y-1.
@@ -1401,7 +1422,9 @@ __device__ __forceinline__ float right_of(const float (&v)[PX], int j) {
 // in flight with counted waits.  Stages run every step: before a segment's first rows
 // reach them and past the image bottom they compute values no stored cell depends on (see
 // the dependency list above; the border forms select, never combine).
-template <bool G, int K, int PX>
+// VIN: in.u1 / u2 / u3 hold stage 1's v = u^0 + TH step (th_px, computed by the caller)
+// instead of u^0
+template <bool G, int K, int PX, bool VIN = false>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                              const IterArgs &a, int r, const RollLane &L,
                                              unsigned nb, unsigned rowb, double &acc);
@@ -1421,10 +1444,11 @@ __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G,
 
 // The compute and stores of one step: input row r (in `in`) enters stage 0 and every
 // stage advances one row.
-template <bool G, int K, int PX>
+template <bool G, int K, int PX, bool VIN>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                              const IterArgs &a, int r, const RollLane &L,
                                              unsigned nb, unsigned rowb, double &acc) {
+  static_assert(!VIN || K >= 2, "stage 1's u^0 (replaced by v) is the K = 1 residual's input");
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     // shift every stage one row down
@@ -1457,13 +1481,20 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
 #pragma unroll
     for (int j = 0; j < PX; ++j) {
       float n1, n2, n3 = 0.0f;
-      estimate_u_px<G>(S.CX[n - 1][j], S.CY[n - 1][j], S.CR[n - 1][j], S.U1p[n - 1][j],
-                       S.U2p[n - 1][j], S.U3p[n - 1][j], S.P11c[n - 1][j],
-                       left_of<PX>(S.P11c[n - 1], j), S.P12c[n - 1][j], S.P12p[n - 1][j],
-                       S.P21c[n - 1][j], left_of<PX>(S.P21c[n - 1], j), S.P22c[n - 1][j],
-                       S.P22p[n - 1][j], S.P31c[n - 1][j],
-                       G ? left_of<PX>(S.P31c[n - 1], j) : 0.0f, S.P32c[n - 1][j],
-                       S.P32p[n - 1][j], L.X + j, yU, a, n1, n2, n3);
+      if (VIN && n == 1)
+        u_from_v<G>(S.U1p[0][j], S.U2p[0][j], S.U3p[0][j], S.P11c[0][j],
+                    left_of<PX>(S.P11c[0], j), S.P12c[0][j], S.P12p[0][j], S.P21c[0][j],
+                    left_of<PX>(S.P21c[0], j), S.P22c[0][j], S.P22p[0][j], S.P31c[0][j],
+                    G ? left_of<PX>(S.P31c[0], j) : 0.0f, S.P32c[0][j], S.P32p[0][j], L.X + j,
+                    yU, a, n1, n2, n3);
+      else
+        estimate_u_px<G>(S.CX[n - 1][j], S.CY[n - 1][j], S.CR[n - 1][j], S.U1p[n - 1][j],
+                         S.U2p[n - 1][j], S.U3p[n - 1][j], S.P11c[n - 1][j],
+                         left_of<PX>(S.P11c[n - 1], j), S.P12c[n - 1][j], S.P12p[n - 1][j],
+                         S.P21c[n - 1][j], left_of<PX>(S.P21c[n - 1], j), S.P22c[n - 1][j],
+                         S.P22p[n - 1][j], S.P31c[n - 1][j],
+                         G ? left_of<PX>(S.P31c[n - 1], j) : 0.0f, S.P32c[n - 1][j],
+                         S.P32p[n - 1][j], L.X + j, yU, a, n1, n2, n3);
       if (n == K && a.calc_err) {
         const float f1 = (S.U1p[n - 1][j] - n1) * (S.U1p[n - 1][j] - n1);
         const float f2 = (S.U2p[n - 1][j] - n2) * (S.U2p[n - 1][j] - n2);
@@ -1805,10 +1836,11 @@ __global__ __launch_bounds__(64) void k_warp_pass(WarpPassArgs w) {
 //   * two producers run k_warp_ring's streaming warpBackward for the band's 128 columns
 //     of one row per step (64 each): an LDS ring of I1 window rows r-M .. r+M (slots
 //     x0-M .. x0+127+M, centeredGradient per slot), the same taps and order.  Each step
-//     they write the row's warp constants and u into a 2-row LDS C ring, and to HBM too
-//     when the warp may need further passes (store_c);
+//     they write the row's warp constants and v = u + TH step of the first iteration
+//     (pointwise, th_px) into a 2-row LDS C ring, and the constants to HBM too when the
+//     warp may need further passes (store_c);
 //   * one consumer runs the k_iterate_roll<false, 2, 2> pipeline (roll_advance: the same
-//     arithmetic), taking each input row's constants and u from the C ring one step after
+//     arithmetic), taking each input row's constants and v from the C ring one step after
 //     the producers wrote it, and only p from HBM.
 // One LDS-only barrier per step orders the window row writes before the gathers and each
 // C ring row before its read (2 C ring rows: a row is overwritten two steps after it was
@@ -1899,12 +1931,16 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
   const float rh = I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0;
+  // the first iteration's TH step is pointwise: the producer does it (the consumer sets
+  // the block's pace), and the C ring carries v = u^0 + d instead of u^0
+  float v1, v2, v3;
+  th_px<false>(I1wxv, I1wyv, rh, cur.u1, cur.u2, 0.0f, w.ra.it, v1, v2, v3);
   float *c = cring + (g & 1) * (5 * kWiBW) + P.ci;
   c[0] = I1wxv;
   c[kWiBW] = I1wyv;
   c[2 * kWiBW] = rh;
-  c[3 * kWiBW] = cur.u1;
-  c[4 * kWiBW] = cur.u2;
+  c[3 * kWiBW] = v1;
+  c[4 * kWiBW] = v2;
   if (w.store_c) {
     const unsigned vo = P.outc && g >= ys && g < ye ? (unsigned)g * rowb + P.xcb : kOOB;
     bstore<kWarpStoreAux>(wa.I1wx, nb, vo, 0, I1wxv);
@@ -1938,7 +1974,7 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, 2> &S,
   in.wx[0] = c[0]; in.wx[1] = c[1];
   in.wy[0] = c[kWiBW]; in.wy[1] = c[kWiBW + 1];
   in.rh[0] = c[2 * kWiBW]; in.rh[1] = c[2 * kWiBW + 1];
-  in.u1[0] = c[3 * kWiBW]; in.u1[1] = c[3 * kWiBW + 1];
+  in.u1[0] = c[3 * kWiBW]; in.u1[1] = c[3 * kWiBW + 1];   // v (roll_advance<.., VIN>)
   in.u2[0] = c[4 * kWiBW]; in.u2[1] = c[4 * kWiBW + 1];
   in.u3[0] = in.u3[1] = 0.0f;
 #pragma unroll
@@ -1947,7 +1983,7 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, 2> &S,
     in.p21[j] = cur.p21[j]; in.p22[j] = cur.p22[j];
     in.p31[j] = in.p32[j] = 0.0f;
   }
-  roll_advance<false, 2, 2>(S, in, a, r, L, nb, rowb, acc);
+  roll_advance<false, 2, 2, true>(S, in, a, r, L, nb, rowb, acc);
 }
 
 template <int M>
