@@ -392,6 +392,9 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
 
   const float l_t = (float)(prm.lambda * prm.theta);
   const float taut = (float)(prm.tau / prm.theta);
+  // The projection's shared-reciprocal division (dual_px) needs ng = 1 + taut*|grad u| >= 1;
+  // other parameters take the one-iteration kernel with plain IEEE divisions.
+  const bool exact_div = !(taut >= 0.0f && taut <= FLT_MAX);
   const float theta_f = (float)prm.theta;
   const float gamma_f = (float)prm.gamma;
   const float upmul = (float)(1.0 / prm.scale_step);
@@ -572,7 +575,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       }
       // warpBackward fused into the warp's first pass (2 iterations ending in the first
       // check) when that pass would stream through k_iterate_roll anyway
-      const bool fuse = c->fuse_first && !gam && !have_gather && roll_short &&
+      const bool fuse = c->fuse_first && !gam && !exact_div && !have_gather && roll_short &&
                         prm.epsilon > 0 && prm.iterations >= 2 &&
                         (c->fuse_first == 1 || (long)lw * lh >= c->fuse_min);
       bool fused_nostore = false;   // k_warp_iter ran without storing the constants
@@ -588,7 +591,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         int k = 0;
         bool calc_end = false;
         double prev_sim = prevError;
-        const int kmax = c->iter_mode == 1 ? 1 : (roll_all || roll_short) ? kRollMax : kTbMax;
+        const int kmax = c->iter_mode == 1 || exact_div ? 1 : (roll_all || roll_short) ? kRollMax : kTbMax;
         while (k < kmax && n + k < prm.iterations) {
           const bool calcError = (prm.epsilon > 0) && ((n + k) & 1) && (prev_sim < scaledEps);
           ++k;
@@ -683,8 +686,12 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           hbm = (double)w.ra.bands * 64.0 * rows * 4.0 * ((p_zero ? 3 : 7) + (64.0 + 2 * M) / 64.0) +
                 Nl * 4.0 * 9.0;
           alg_extra = Nl * 40.0;   // 40 B/px per warp
-        } else if (c->iter_mode == 1) {
-          if (gam)
+        } else if (c->iter_mode == 1 || exact_div) {
+          if (gam && exact_div)
+            hipLaunchKernelGGL((k_iterate<true, true>), dim3(nblk), dim3(kBlock), 0, st, a);
+          else if (exact_div)
+            hipLaunchKernelGGL((k_iterate<false, true>), dim3(nblk), dim3(kBlock), 0, st, a);
+          else if (gam)
             hipLaunchKernelGGL(k_iterate<true>, dim3(nblk), dim3(kBlock), 0, st, a);
           else
             hipLaunchKernelGGL(k_iterate<false>, dim3(nblk), dim3(kBlock), 0, st, a);

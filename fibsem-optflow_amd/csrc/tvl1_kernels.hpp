@@ -1000,10 +1000,56 @@ __device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up
   }
 }
 
-__device__ __forceinline__ float hypot_f(float a, float b) { return sqrtf(a * a + b * b); }
+// Correctly rounded sqrt of x >= 0 (or +inf): the compiler's IEEE sqrtf sequence
+// (v_sqrt_f32 on x scaled by 2^32 below 2^-96, the two one-ulp neighbours tested with fma
+// residuals, scaled back by 2^-16) without its final class test, which returns x itself
+// for +-0 and +inf -- the sequence already gives exactly those (+0: the candidates are
+// NaN and a denormal whose residual is +0; +inf: NaN residuals).  -0 cannot reach it.
+__device__ __forceinline__ float sqrt_nn(float x) {
+  const bool small = x < 0x1p-96f;
+  const float xs = small ? x * 0x1p32f : x;
+  const float s = __builtin_amdgcn_sqrtf(xs);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rm = __builtin_fmaf(-sm, s, xs);
+  const float rp = __builtin_fmaf(-sp, s, xs);
+  float r = rm <= 0.0f ? sm : s;
+  r = rp > 0.0f ? sp : r;
+  return small ? r * 0x1p-16f : r;
+}
+
+__device__ __forceinline__ float hypot_f(float a, float b) { return sqrt_nn(a * a + b * b); }
+
+// Correctly rounded a / d for the projection's d = ng = 1 + taut * |grad u| >= 1 (taut >= 0):
+// the compiler's IEEE division sequence (div_scale, refined reciprocal, two fma
+// corrections, div_fmas, div_fixup) minus the denominator's div_scale, which returns d
+// unchanged unless d is denormal, 1/d is, or exp(a) - exp(d) >= 96 -- none can happen:
+// |p| <= 1 (the projection keeps it there) gives |a| = |p + taut*du| <= 1 + taut*|grad u| = d.
+// The refined reciprocal is shared by the two quotients with the same d.
+struct Recip {
+  float d, y;
+};
+__device__ __forceinline__ Recip recip_of(float d) {
+  const float r = __builtin_amdgcn_rcpf(d);
+  const float e = __builtin_fmaf(-d, r, 1.0f);
+  return Recip{d, __builtin_fmaf(e, r, r)};
+}
+__device__ __forceinline__ float div_by(float a, const Recip &R) {
+  bool scaled;
+  const float n = __builtin_amdgcn_div_scalef(a, R.d, true, &scaled);
+  const float q0 = n * R.y;
+  const float r0 = __builtin_fmaf(-R.d, q0, n);
+  const float q1 = __builtin_fmaf(r0, R.y, q0);
+  const float r1 = __builtin_fmaf(-R.d, q1, n);
+  const float q = __builtin_amdgcn_div_fmasf(r1, R.y, q1, scaled);
+  return __builtin_amdgcn_div_fixupf(q, R.d, a);
+}
 
 // estimateDualVariables for one (u, p*1, p*2) component at one px:
 // p' = (p + taut * du) / ng, du from u at (x+1) and (y+1) (clamped at the image edge).
+// EXACT: plain IEEE divisions, for taut < 0 or non-finite (k_iterate<G, true>; the host
+// routes such parameters there), where ng >= 1 does not hold.
+template <bool EXACT = false>
 __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_right,
                                         bool has_down, float taut, float pa, float pb, float &oa,
                                         float &ob) {
@@ -1013,12 +1059,18 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
   const float uy = down - uc;
   const float g = hypot_f(ux, uy);
   const float ng = 1.0f + taut * g;
-  oa = (pa + taut * ux) / ng;
-  ob = (pb + taut * uy) / ng;
+  if (EXACT) {
+    oa = (pa + taut * ux) / ng;
+    ob = (pb + taut * uy) / ng;
+  } else {
+    const Recip R = recip_of(ng);
+    oa = div_by(pa + taut * ux, R);
+    ob = div_by(pb + taut * uy, R);
+  }
 }
 
 // One projection component for the PX px of this lane.
-template <int PX>
+template <int PX, bool EXACT = false>
 __device__ __forceinline__ void dual_component(const float (&uc)[PX], const float (&un)[PX],
                                                bool has_down, int X0, int W, float taut,
                                                const float (&pa)[PX], const float (&pb)[PX],
@@ -1029,10 +1081,11 @@ __device__ __forceinline__ void dual_component(const float (&uc)[PX], const floa
   for (int k = 0; k < PX - 1; ++k) ur[k] = uc[k + 1];
 #pragma unroll
   for (int k = 0; k < PX; ++k)
-    dual_px(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k], oa[k], ob[k]);
+    dual_px<EXACT>(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k], oa[k],
+                   ob[k]);
 }
 
-template <bool G>
+template <bool G, bool EXACT = false>
 __global__ __launch_bounds__(kBlock) void k_iterate(IterArgs a) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
@@ -1073,9 +1126,10 @@ __global__ __launch_bounds__(kBlock) void k_iterate(IterArgs a) {
         for (int k = 0; k < 4; ++k) { n1[k] = c1[k]; n2[k] = c2[k]; n3[k] = c3[k]; }
       }
       float q11[4], q12[4], q21[4], q22[4], q31[4], q32[4];
-      dual_component(c1, n1, has_down, X0, a.W, a.taut, cur.p11, cur.p12, q11, q12);
-      dual_component(c2, n2, has_down, X0, a.W, a.taut, cur.p21, cur.p22, q21, q22);
-      if (G) dual_component(c3, n3, has_down, X0, a.W, a.taut, cur.p31, cur.p32, q31, q32);
+      dual_component<4, EXACT>(c1, n1, has_down, X0, a.W, a.taut, cur.p11, cur.p12, q11, q12);
+      dual_component<4, EXACT>(c2, n2, has_down, X0, a.W, a.taut, cur.p21, cur.p22, q21, q22);
+      if (G)
+        dual_component<4, EXACT>(c3, n3, has_down, X0, a.W, a.taut, cur.p31, cur.p32, q31, q32);
       if (writer) {
         const size_t off = (size_t)y * a.P + xa;
         st4(a.u1d, off, c1);

@@ -57,6 +57,21 @@ def test_engine_matches_oracle(engine, W, H, seed, kw):
         f"not bit-exact: max|du|={np.abs(u-ur).max()} max|dv|={np.abs(v-vr).max()}"
 
 
+@pytest.mark.parametrize("tau,theta", [(-0.05, 0.3), (0.25, -0.3)])
+def test_negative_taut_takes_exact_division_path(engine, tau, theta):
+    """tau/theta < 0 breaks ng >= 1, which the projection's shared-reciprocal division
+    relies on: the engine must route such parameters to plain IEEE divisions."""
+    I0, I1 = synth.gen_pair(70, 50, seed=11)
+    p = capi.make_params(nscales=3, warps=2, iterations=12, tau=tau, theta=theta)
+    engine.set_params(p)
+    u, v, _, wi = engine.calc_host(I0, I1)
+    ur, vr, _, wr = capi.oracle_calc(I0, I1, p)
+    np.testing.assert_array_equal(wi, wr)
+    fin = np.isfinite(ur) & np.isfinite(vr)
+    assert np.array_equal(fin, np.isfinite(u) & np.isfinite(v))
+    assert bits_equal(u[fin], ur[fin]) and bits_equal(v[fin], vr[fin])
+
+
 def test_identity_pair_gives_zero_flow(engine):
     I0, _ = synth.gen_pair(80, 60, seed=3)
     engine.set_params(capi.make_params(nscales=4, warps=3))
