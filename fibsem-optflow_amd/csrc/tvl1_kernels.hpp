@@ -898,13 +898,13 @@ __device__ __forceinline__ void load_row(Row<G, PX> &r, const IterArgs &a, size_
 // selected (the x == 0, y > 0 form associates differently from the interior one).
 __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float p2u, int x,
                                             int y) {
-  const float interior = (p1 - p1l) + (p2 - p2u);
-  const float col0 = p1 + p2 - p2u;      // x == 0, y > 0
-  const float row0 = p1 - p1l + p2;      // y == 0, x > 0
-  const float corner = p1 + p2;          // x == 0, y == 0
-  const float ylo = x > 0 ? row0 : corner;
-  const float yhi = x > 0 ? interior : col0;
-  return y > 0 ? yhi : ylo;
+  // interior (p1 - p1l) + (p2 - p2u) and row 0 (p1 - p1l) + p2 are one form with p2u := 0
+  // at y = 0 (p2 - +0 == p2 exactly, signed zeros included); column 0 (p1 + p2) - p2u and
+  // the corner p1 + p2 likewise
+  const float p2u0 = y > 0 ? p2u : 0.0f;
+  const float rest = (p1 - p1l) + (p2 - p2u0);
+  const float col0 = (p1 + p2) - p2u0;
+  return x > 0 ? rest : col0;
 }
 
 // estimateU's TH step at one px: v = u^{n-1} + d from the warp constants (pointwise).
@@ -1005,20 +1005,32 @@ __device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up
 // residuals, scaled back by 2^-16) without its final class test, which returns x itself
 // for +-0 and +inf -- the sequence already gives exactly those (+0: the candidates are
 // NaN and a denormal whose residual is +0; +inf: NaN residuals).  -0 cannot reach it.
-__device__ __forceinline__ float sqrt_nn(float x) {
-  const bool small = x < 0x1p-96f;
-  const float xs = small ? x * 0x1p32f : x;
+__device__ __forceinline__ float sqrt_rn_core(float xs) {
   const float s = __builtin_amdgcn_sqrtf(xs);
   const float sm = __uint_as_float(__float_as_uint(s) - 1u);
   const float sp = __uint_as_float(__float_as_uint(s) + 1u);
   const float rm = __builtin_fmaf(-sm, s, xs);
   const float rp = __builtin_fmaf(-sp, s, xs);
-  float r = rm <= 0.0f ? sm : s;
-  r = rp > 0.0f ? sp : r;
+  const float r = rm <= 0.0f ? sm : s;
+  return rp > 0.0f ? sp : r;
+}
+// BR: lanes below 2^-96 (rare: both differences under 2^-48) take the scaled form in a
+// branch the wavefront skips when no lane needs it -- faster in the looped k_iterate_tb,
+// slower in the unrolled pipelines, which select instead.
+template <bool BR>
+__device__ __forceinline__ float sqrt_nn(float x) {
+  if (BR) {
+    float r = sqrt_rn_core(x);
+    if (x < 0x1p-96f) r = sqrt_rn_core(x * 0x1p32f) * 0x1p-16f;
+    return r;
+  }
+  const bool small = x < 0x1p-96f;
+  const float r = sqrt_rn_core(small ? x * 0x1p32f : x);
   return small ? r * 0x1p-16f : r;
 }
 
-__device__ __forceinline__ float hypot_f(float a, float b) { return sqrt_nn(a * a + b * b); }
+template <bool BR = false>
+__device__ __forceinline__ float hypot_f(float a, float b) { return sqrt_nn<BR>(a * a + b * b); }
 
 // Correctly rounded a / d for the projection's d = ng = 1 + taut * |grad u| >= 1 (taut >= 0):
 // the compiler's IEEE division sequence (div_scale, refined reciprocal, two fma
@@ -1049,7 +1061,7 @@ __device__ __forceinline__ float div_by(float a, const Recip &R) {
 // p' = (p + taut * du) / ng, du from u at (x+1) and (y+1) (clamped at the image edge).
 // EXACT: plain IEEE divisions, for taut < 0 or non-finite (k_iterate<G, true>; the host
 // routes such parameters there), where ng >= 1 does not hold.
-template <bool EXACT = false>
+template <bool EXACT = false, bool BR = false>
 __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_right,
                                         bool has_down, float taut, float pa, float pb, float &oa,
                                         float &ob) {
@@ -1057,7 +1069,7 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
   const float down = has_down ? ud : uc;
   const float ux = right - uc;
   const float uy = down - uc;
-  const float g = hypot_f(ux, uy);
+  const float g = hypot_f<BR>(ux, uy);
   const float ng = 1.0f + taut * g;
   if (EXACT) {
     oa = (pa + taut * ux) / ng;
@@ -1081,8 +1093,8 @@ __device__ __forceinline__ void dual_component(const float (&uc)[PX], const floa
   for (int k = 0; k < PX - 1; ++k) ur[k] = uc[k + 1];
 #pragma unroll
   for (int k = 0; k < PX; ++k)
-    dual_px<EXACT>(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k], oa[k],
-                   ob[k]);
+    dual_px<EXACT, true>(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k],
+                         oa[k], ob[k]);
 }
 
 template <bool G, bool EXACT = false>
