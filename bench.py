@@ -65,6 +65,13 @@ def parse():
     ap.add_argument("--iterations", type=int, default=300)
     ap.add_argument("--epsilon", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fast-math", action="store_true",
+                    help="headline run in fast-math mode (tvl1_params.fast_math = 1: the "
+                         "reference build's CUDA_FAST_MATH semantics; tolerance parity, not "
+                         "bit-identical). Default: IEEE (bit-identical to oracle/), with a "
+                         "secondary fast-math measurement reported under \"fast_math\"")
+    ap.add_argument("--no-fast-math-line", action="store_true",
+                    help="skip the secondary fast-math measurement")
     ap.add_argument("--cpu-sample", default="3072x2048")
     ap.add_argument("--inflight", type=int, default=2,
                     help="slice pairs solved concurrently per GPU (one ctx + stream + host "
@@ -124,7 +131,8 @@ def run_stack(args, rank, world, local_rank, dist):
     W, H, Z = args.width, args.height, args.slices
     strides = [int(t) for t in args.strides.split(",")]
     params = capi.make_params(nscales=args.nscales, warps=args.warps,
-                              iterations=args.iterations, epsilon=args.epsilon)
+                              iterations=args.iterations, epsilon=args.epsilon,
+                              fast_math=int(args.fast_math))
     dev = torch.device("cuda", local_rank)
     gen = DeviceStack(W, H, dev)
     items = []
@@ -219,6 +227,7 @@ def run_stack(args, rank, world, local_rank, dist):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
+        "math": "fast (CUDA_FAST_MATH semantics)" if args.fast_math else "IEEE (bit-identical to oracle/)",
         "data": "synthetic (slices generated on the device)",
         "config": {
             "workload": (f"{name}: {npairs} pairs (z, z+s), s in {strides}, of a {Z}-slice "
@@ -258,7 +267,8 @@ def main():
 
     W, H = args.width, args.height
     params = capi.make_params(nscales=args.nscales, warps=args.warps,
-                              iterations=args.iterations, epsilon=args.epsilon)
+                              iterations=args.iterations, epsilon=args.epsilon,
+                              fast_math=int(args.fast_math))
     # each rank gets its own slice pair(s) of the synthetic stack (z = rank*F + j + 1 vs base)
     F = max(1, args.inflight)
     dev = torch.device("cuda", local_rank)
@@ -290,25 +300,31 @@ def main():
             return [solve(slots[0])]
         return list(pool.map(solve, slots))
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    stats = []
-    for _ in range(args.steps):
-        stats.extend(step())
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(warmup, steps):
+        """W untimed warmup steps, then exactly K timed steps bracketed by a barrier and a
+        device sync on both sides; the max over ranks."""
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        stats = []
+        for _ in range(steps):
+            stats.extend(step())
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, stats
+
+    elapsed, stats = timed(args.warmup, args.steps)
     I0h, I1h = slots[0]["I0h"], slots[0]["I1h"]
     # one extra solve alone on the GPU (not timed): clean per-kernel durations, no
     # interleaving with the other in-flight pair
@@ -318,6 +334,29 @@ def main():
     single_pair_ms = 1e3 * (time.perf_counter() - t_iso)
     if F == 1 or args.no_kernel_timing:
         iso = None
+
+    # secondary measurement in the other math mode (same pairs, same K): the IEEE run is
+    # the headline unless --fast-math; its flow is the reference for the EPE figures
+    alt = None
+    if not args.no_fast_math_line:
+        u_ref, v_ref = slots[0]["u"].clone(), slots[0]["v"].clone()
+        alt_params = capi.make_params(nscales=args.nscales, warps=args.warps,
+                                      iterations=args.iterations, epsilon=args.epsilon,
+                                      fast_math=0 if args.fast_math else 1)
+        for sl in slots:
+            sl["eng"].set_params(alt_params)
+            sl["eng"].set_profiling(False)
+        alt_elapsed, alt_stats = timed(1, args.steps)
+        solve(slots[0])
+        torch.cuda.synchronize(dev)
+        e = torch.sqrt((slots[0]["u"] - u_ref) ** 2 + (slots[0]["v"] - v_ref) ** 2)
+        alt = {"math": "IEEE" if args.fast_math else "fast (CUDA_FAST_MATH semantics)",
+               "value": round(world * args.steps * F / alt_elapsed, 4),
+               "ms_per_step": round(1e3 * alt_elapsed / args.steps, 3),
+               "iterations_per_pair": alt_stats[0]["iterations_total"],
+               "same_iterations": alt_stats[0]["iterations_total"] == stats[0]["iterations_total"],
+               "mean_epe_vs_headline_px": float(e.mean()),
+               "max_epe_vs_headline_px": float(e.max())}
 
     # aggregate per-kernel timing of this rank (rank 0 reports its own kernel roofline)
     k_ms = sum(s["kernel_ms"][0] for s in stats)
@@ -379,6 +418,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
+        "math": "fast (CUDA_FAST_MATH semantics)" if args.fast_math else "IEEE (bit-identical to oracle/)",
         "data": "synthetic",
         "config": {
             "workload": (("C2" if (W, H, args.nscales, args.warps) == (6144, 4096, 5, 30)
@@ -409,6 +449,7 @@ def main():
              "other_kernels": round(cls_ms[2], 2),
              "host_sync_and_gaps": round(ms_per_step - sum(cls_ms), 2)}),
         "cpu_baseline": None,
+        "fast_math" if not args.fast_math else "ieee_math": alt,
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(I0h, I1h, params, args.cpu_sample)

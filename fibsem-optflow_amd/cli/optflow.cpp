@@ -109,6 +109,7 @@ tvl1_params generate_TV_args(const Value &im, const Value &args) {
   p.gamma = D("gamma", 0.0);
   p.use_initial_flow = im.get("useInitialFlow", args.get("useInitialFlow", false).asBool()).asBool();
   p.median_filtering = I("medianFiltering", 1);
+  p.fast_math = I("fastMath", 0);
   return p;
 }
 
@@ -550,6 +551,7 @@ static int from_file(Value &args, bool plan_only) {
           pl["tv"]["scaleStep"] = tp.scale_step;
           pl["tv"]["gamma"] = tp.gamma;
           pl["tv"]["medianFiltering"] = tp.median_filtering;
+          pl["tv"]["fastMath"] = tp.fast_math;
           for (auto &key : rois.memberNames())
             pl["files"].append(im["output"].asString() +
                                ((key == "top" || key == "bottom") ? "_" + key : std::string()));

@@ -169,6 +169,8 @@ static tvl1_status check_params(tvl1_ctx *c, const tvl1_params *p) {
     return set_err(c, TVL1_EINVAL, "scaleStep must be in (0, 1]");
   if (p->median_filtering > 1 && p->median_filtering != 3 && p->median_filtering != 5)
     return set_err(c, TVL1_EINVAL, "medianFiltering must be 1 (off), 3 or 5");
+  if (p->fast_math != 0 && p->fast_math != 1)
+    return set_err(c, TVL1_EINVAL, "fastMath must be 0 or 1 (got %d)", p->fast_math);
   return TVL1_OK;
 }
 
@@ -395,6 +397,8 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   // The projection's shared-reciprocal division (dual_px) needs ng = 1 + taut*|grad u| >= 1;
   // other parameters take the one-iteration kernel with plain IEEE divisions.
   const bool exact_div = !(taut >= 0.0f && taut <= FLT_MAX);
+  // fast-math kernels (FM template argument) for the gamma = 0 iteration passes
+  const bool fm = prm.fast_math != 0 && !gam;
   const float theta_f = (float)prm.theta;
   const float gamma_f = (float)prm.gamma;
   const float upmul = (float)(1.0 / prm.scale_step);
@@ -639,8 +643,12 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
                            c->partials_cap);
-          if (M == 4)
+          if (M == 4 && fm)
+            hipLaunchKernelGGL((k_warp_iter<4, true>), dim3(w.ra.waves), dim3(192), 0, st, w);
+          else if (M == 4)
             hipLaunchKernelGGL(k_warp_iter<4>, dim3(w.ra.waves), dim3(192), 0, st, w);
+          else if (fm)
+            hipLaunchKernelGGL((k_warp_iter<6, true>), dim3(w.ra.waves), dim3(192), 0, st, w);
           else
             hipLaunchKernelGGL(k_warp_iter<6>, dim3(w.ra.waves), dim3(192), 0, st, w);
           // compulsory: p, u, I0 and the I1 window (x 1 + 2M/128) per band column and row;
@@ -718,6 +726,9 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   if (gam)                                                                                     \
     hipLaunchKernelGGL((k_iterate_roll<true, K, PX>), dim3((ra.waves + 3) / 4), dim3(256),     \
                        c->roll_lds, st, ra);                                                   \
+  else if (fm)                                                                                 \
+    hipLaunchKernelGGL((k_iterate_roll<false, K, PX, true>), dim3((ra.waves + 3) / 4),         \
+                       dim3(256), c->roll_lds, st, ra);                                        \
   else                                                                                         \
     hipLaunchKernelGGL((k_iterate_roll<false, K, PX>), dim3((ra.waves + 3) / 4), dim3(256),    \
                        c->roll_lds, st, ra);
@@ -765,6 +776,9 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
 #define TB_LAUNCH(RH, NG, PX)                                                                  \
   if (gam)                                                                                     \
     hipLaunchKernelGGL((k_iterate_tb<true, RH, NG, PX>), dim3(blocks),                         \
+                       dim3((64 / PX) * RH / NG), 0, st, t);                                   \
+  else if (fm)                                                                                 \
+    hipLaunchKernelGGL((k_iterate_tb<false, RH, NG, PX, true>), dim3(blocks),                  \
                        dim3((64 / PX) * RH / NG), 0, st, t);                                   \
   else                                                                                         \
     hipLaunchKernelGGL((k_iterate_tb<false, RH, NG, PX>), dim3(blocks),                        \
@@ -899,6 +913,7 @@ void tvl1_params_default(tvl1_params *p) {
   p->gamma = 0.0;
   p->use_initial_flow = 0;
   p->median_filtering = 1;
+  p->fast_math = 0;
 }
 
 int32_t tvl1_abi_version(void) { return TVL1_ABI_VERSION; }

@@ -277,13 +277,45 @@ __device__ __forceinline__ float cubic_out(float x) {
 struct Tap3 {
   float x, y, z;
 };
-template <class TapF>
+// FM (fast-math mode, see th_px): the polynomial and the accumulation contracted to fma.
+__device__ __forceinline__ float cubic_in_fm(float x) {
+  x = fabsf(x);
+  return __builtin_fmaf(x * x, __builtin_fmaf(1.5f, x, -2.5f), 1.0f);
+}
+__device__ __forceinline__ float cubic_out_fm(float x) {
+  x = fabsf(x);
+  return __builtin_fmaf(x, __builtin_fmaf(x, __builtin_fmaf(-0.5f, x, 2.5f), -4.0f), 2.0f);
+}
+template <bool FM = false, class TapF>
 __device__ __forceinline__ void warp_gather_fn(TapF tap, float wx, float wy, int fx, int fy,
                                                float &sum, float &sumx, float &sumy, float &wsum) {
   // (float)(fx + k) == (float)fx + k exactly: |fx| <= 2^24 (tap_floor), and both round
   // the same integer once
   const float fxf = (float)fx, fyf = (float)fy;
   float kx[4], ky[4];
+  if (FM) {
+    kx[0] = cubic_out_fm(wx - (fxf - 1.0f));
+    kx[1] = cubic_in_fm(wx - fxf);
+    kx[2] = cubic_in_fm(wx - (fxf + 1.0f));
+    kx[3] = cubic_out_fm(wx - (fxf + 2.0f));
+    ky[0] = cubic_out_fm(wy - (fyf - 1.0f));
+    ky[1] = cubic_in_fm(wy - fyf);
+    ky[2] = cubic_in_fm(wy - (fyf + 1.0f));
+    ky[3] = cubic_out_fm(wy - (fyf + 2.0f));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float w = kx[i] * ky[j];
+        const Tap3 g = tap(fy - 1 + j, fx - 1 + i);
+        sum = __builtin_fmaf(w, g.x, sum);
+        sumx = __builtin_fmaf(w, g.y, sumx);
+        sumy = __builtin_fmaf(w, g.z, sumy);
+        wsum = wsum + w;
+      }
+    }
+    return;
+  }
   kx[0] = cubic_out(wx - (fxf - 1.0f));
   kx[1] = cubic_in(wx - fxf);
   kx[2] = cubic_in(wx - (fxf + 1.0f));
@@ -907,23 +939,36 @@ __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float
   return x > 0 ? rest : col0;
 }
 
+// Fast-math mode (tvl1_params.fast_math; FM template argument): the reference's own
+// OpenCV build flags (CUDA_FAST_MATH: nvcc -use_fast_math = approximate division and
+// sqrt, a*b + c contracted to fma; singularity/optflow.def:33-34) restated for CDNA4:
+// a / b -> a * v_rcp_f32(b), sqrt -> v_sqrt_f32 (both 1 ulp), and the products feeding a
+// sum are fused as nvcc would contract them.  Not bit-identical to oracle/: it is held to
+// the north-star tolerance (mean EPE <= 1e-3 px, same per-warp iteration counts) in
+// tests/test_gpu_parity.py.
+__device__ __forceinline__ float fm_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
 // estimateU's TH step at one px: v = u^{n-1} + d from the warp constants (pointwise).
-template <bool G>
+template <bool G, bool FM = false>
 __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, float u1o, float u2o,
                                       float u3o, const IterArgs &a, float &v1, float &v2,
                                       float &v3) {
   const float Ix2 = I1wxv * I1wxv;
   const float Iy2 = I1wyv * I1wyv;
-  const float gradv = Ix2 + Iy2;
+  const float gradv = FM ? fm_fma(I1wyv, I1wyv, Ix2) : Ix2 + Iy2;
   // gamma*u3 inside the parentheses (with gamma = 0 either association gives
   // the same bits, signed zeros included)
-  const float rho = rhoc + (I1wxv * u1o + I1wyv * u2o + a.gamma * (G ? u3o : 0.0f));
+  const float rho =
+      FM ? rhoc + (G ? fm_fma(a.gamma, u3o, fm_fma(I1wyv, u2o, I1wxv * u1o))
+                     : fm_fma(I1wyv, u2o, I1wxv * u1o))
+         : rhoc + (I1wxv * u1o + I1wyv * u2o + a.gamma * (G ? u3o : 0.0f));
   // TH operator, branch-free: the three candidate steps are computed with the
   // reference's exact expressions and the applicable one selected.
   const bool lo = rho < -a.l_t * gradv;
   const bool hi = rho > a.l_t * gradv;
   const bool mid = gradv > kFltEps;
-  const float fi = -rho / gradv;     // only selected when gradv > FLT_EPSILON
+  // only selected when gradv > FLT_EPSILON
+  const float fi = FM ? -rho * __builtin_amdgcn_rcpf(gradv) : -rho / gradv;
   float d1 = mid ? fi * I1wxv : 0.0f;
   float d2 = mid ? fi * I1wyv : 0.0f;
   float d3 = mid ? fi * a.gamma : 0.0f;
@@ -940,7 +985,7 @@ __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, floa
 
 // estimateU's second half at one px: u^n = v + theta * div(p^{n-1}).  pl = p*1 at x-1,
 // pu = p*2 at y-1.
-template <bool G>
+template <bool G, bool FM = false>
 __device__ __forceinline__ void u_from_v(float v1, float v2, float v3, float p11, float p11l,
                                          float p12, float p12u, float p21, float p21l,
                                          float p22, float p22u, float p31, float p31l,
@@ -948,18 +993,18 @@ __device__ __forceinline__ void u_from_v(float v1, float v2, float v3, float p11
                                          const IterArgs &a, float &n1, float &n2, float &n3) {
   const float div1 = divergence(p11, p11l, p12, p12u, x, y);
   const float div2 = divergence(p21, p21l, p22, p22u, x, y);
-  n1 = v1 + a.theta * div1;
-  n2 = v2 + a.theta * div2;
+  n1 = FM ? fm_fma(a.theta, div1, v1) : v1 + a.theta * div1;
+  n2 = FM ? fm_fma(a.theta, div2, v2) : v2 + a.theta * div2;
   if (G) {
     const float div3 = divergence(p31, p31l, p32, p32u, x, y);
-    n3 = v3 + a.theta * div3;
+    n3 = FM ? fm_fma(a.theta, div3, v3) : v3 + a.theta * div3;
   }
 }
 
 // estimateU at one px (x, y): the TH step from the warp constants and u^{n-1}, then
 // u^n = v + theta * div(p^{n-1}).  Shared by every iteration kernel, so they all run
 // exactly this sequence of IEEE float operations.
-template <bool G>
+template <bool G, bool FM = false>
 __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rhoc, float u1o,
                                               float u2o, float u3o, float p11, float p11l,
                                               float p12, float p12u, float p21, float p21l,
@@ -968,13 +1013,13 @@ __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rh
                                               const IterArgs &a, float &n1, float &n2,
                                               float &n3) {
   float v1, v2, v3;
-  th_px<G>(I1wxv, I1wyv, rhoc, u1o, u2o, u3o, a, v1, v2, v3);
-  u_from_v<G>(v1, v2, v3, p11, p11l, p12, p12u, p21, p21l, p22, p22u, p31, p31l, p32, p32u, x,
+  th_px<G, FM>(I1wxv, I1wyv, rhoc, u1o, u2o, u3o, a, v1, v2, v3);
+  u_from_v<G, FM>(v1, v2, v3, p11, p11l, p12, p12u, p21, p21l, p22, p22u, p31, p31l, p32, p32u, x,
               y, a, n1, n2, n3);
 }
 
 // estimateU for the PX px of this lane on row y.  up* = p12/p22/p32 of row y-1.
-template <bool G, int PX = 4>
+template <bool G, int PX = 4, bool FM = false>
 __device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up12)[PX],
                                            const float (&up22)[PX], const float (&up32)[PX],
                                            int X0, int y, const IterArgs &a, float (&n1)[PX],
@@ -994,7 +1039,7 @@ __device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up
     const float u3o = G ? r.u3[k] : 0.0f;
     const float p31 = G ? r.p31[k] : 0.0f, p31l = G ? l31[k] : 0.0f;
     const float p32 = G ? r.p32[k] : 0.0f;
-    estimate_u_px<G>(r.wx[k], r.wy[k], r.rh[k], r.u1[k], r.u2[k], u3o, r.p11[k], l11[k],
+    estimate_u_px<G, FM>(r.wx[k], r.wy[k], r.rh[k], r.u1[k], r.u2[k], u3o, r.p11[k], l11[k],
                      r.p12[k], up12[k], r.p21[k], l21[k], r.p22[k], up22[k], p31, p31l, p32,
                      up32[k], X0 + k, y, a, n1[k], n2[k], n3[k]);
   }
@@ -1061,7 +1106,7 @@ __device__ __forceinline__ float div_by(float a, const Recip &R) {
 // p' = (p + taut * du) / ng, du from u at (x+1) and (y+1) (clamped at the image edge).
 // EXACT: plain IEEE divisions, for taut < 0 or non-finite (k_iterate<G, true>; the host
 // routes such parameters there), where ng >= 1 does not hold.
-template <bool EXACT = false, bool BR = false>
+template <bool EXACT = false, bool BR = false, bool FM = false>
 __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_right,
                                         bool has_down, float taut, float pa, float pb, float &oa,
                                         float &ob) {
@@ -1069,6 +1114,13 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
   const float down = has_down ? ud : uc;
   const float ux = right - uc;
   const float uy = down - uc;
+  if (FM && !EXACT) {
+    const float g = __builtin_amdgcn_sqrtf(fm_fma(uy, uy, ux * ux));
+    const float r = __builtin_amdgcn_rcpf(fm_fma(taut, g, 1.0f));
+    oa = fm_fma(taut, ux, pa) * r;
+    ob = fm_fma(taut, uy, pb) * r;
+    return;
+  }
   const float g = hypot_f<BR>(ux, uy);
   const float ng = 1.0f + taut * g;
   if (EXACT) {
@@ -1082,7 +1134,7 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
 }
 
 // One projection component for the PX px of this lane.
-template <int PX, bool EXACT = false>
+template <int PX, bool EXACT = false, bool FM = false>
 __device__ __forceinline__ void dual_component(const float (&uc)[PX], const float (&un)[PX],
                                                bool has_down, int X0, int W, float taut,
                                                const float (&pa)[PX], const float (&pb)[PX],
@@ -1093,7 +1145,7 @@ __device__ __forceinline__ void dual_component(const float (&uc)[PX], const floa
   for (int k = 0; k < PX - 1; ++k) ur[k] = uc[k + 1];
 #pragma unroll
   for (int k = 0; k < PX; ++k)
-    dual_px<EXACT, true>(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k],
+    dual_px<EXACT, true, FM>(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k],
                          oa[k], ob[k]);
 }
 
@@ -1211,7 +1263,7 @@ struct TBArgs {
 // Pass body of the blocked kernel: stage the vertically read planes, run the pass's
 // iterations on register-resident state, store the exact interior and the residual
 // partial of the last iteration.  lds = NPL planes of RH x LPR vectors of PX floats.
-template <bool G, int RH, int NG, int PX>
+template <bool G, int RH, int NG, int PX, bool FM>
 __device__ __forceinline__ void tb_iterate_store(const TBArgs &t,
                                                  typename VecT<PX>::type *__restrict__ lds,
                                                  Row<G, PX> (&r)[NG], const int (&Y)[NG], int X,
@@ -1256,7 +1308,7 @@ __device__ __forceinline__ void tb_iterate_store(const TBArgs &t,
       if (G) unpack(up32, L(4, rowu));
       else zerov<PX>(up32);
       float n1[PX], n2[PX], n3[PX];
-      estimate_u<G, PX>(r[g], up12, up22, up32, X, Y[g], a, n1, n2, n3);
+      estimate_u<G, PX, FM>(r[g], up12, up22, up32, X, Y[g], a, n1, n2, n3);
       if (last && a.calc_err && out_ok[g]) {
 #pragma unroll
         for (int k = 0; k < PX; ++k) {
@@ -1288,11 +1340,11 @@ __device__ __forceinline__ void tb_iterate_store(const TBArgs &t,
       unpack(d1, L(2, rowd));
       unpack(d2, L(3, rowd));
       float q11[PX], q12[PX], q21[PX], q22[PX], q31[PX], q32[PX];
-      dual_component(r[g].u1, d1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12);
-      dual_component(r[g].u2, d2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22);
+      dual_component<PX, false, FM>(r[g].u1, d1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12);
+      dual_component<PX, false, FM>(r[g].u2, d2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22);
       if (G) {
         unpack(d3, L(5, rowd));
-        dual_component(r[g].u3, d3, has_down, X, a.W, a.taut, r[g].p31, r[g].p32, q31, q32);
+        dual_component<PX, false, FM>(r[g].u3, d3, has_down, X, a.W, a.taut, r[g].p31, r[g].p32, q31, q32);
       }
 #pragma unroll
       for (int k = 0; k < PX; ++k) {
@@ -1348,7 +1400,7 @@ __device__ __forceinline__ void tb_iterate_store(const TBArgs &t,
   }
 }
 
-template <bool G, int RH, int NG, int PX = 4>
+template <bool G, int RH, int NG, int PX = 4, bool FM = false>
 __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterate_tb(TBArgs t) {
   constexpr int LPR = 64 / PX;
   constexpr int HALF = RH / NG;
@@ -1373,7 +1425,7 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
     const int ya = imin(imax(Y[g], 0), a.H - 1);
     load_row<G, PX>(r[g], a, (size_t)ya * a.P + xa);
   }
-  tb_iterate_store<G, RH, NG, PX>(t, lds, r, Y, X, c4, rr);
+  tb_iterate_store<G, RH, NG, PX, FM>(t, lds, r, Y, X, c4, rr);
 }
 
 // ---------------------------------------------------------------- K6+K8 wavefront pipeline
@@ -1490,12 +1542,12 @@ __device__ __forceinline__ float right_of(const float (&v)[PX], int j) {
 // the dependency list above; the border forms select, never combine).
 // VIN: in.u1 / u2 / u3 hold stage 1's v = u^0 + TH step (th_px, computed by the caller)
 // instead of u^0
-template <bool G, int K, int PX, bool VIN = false>
+template <bool G, int K, int PX, bool VIN = false, bool FM = false>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                              const IterArgs &a, int r, const RollLane &L,
                                              unsigned nb, unsigned rowb, double &acc);
 
-template <bool G, int K, int PX>
+template <bool G, int K, int PX, bool FM>
 __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                           RollIn<G, PX> &ahead, const IterArgs &a, int r,
                                           const RollLane &L, unsigned nb, unsigned rowb,
@@ -1505,12 +1557,12 @@ __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G,
   // roll_ahead steps later then leaves the younger stores and loads in flight (vmcnt
   // counts in issue order)
   __builtin_amdgcn_sched_barrier(0);
-  roll_advance<G, K, PX>(S, in, a, r, L, nb, rowb, acc);
+  roll_advance<G, K, PX, false, FM>(S, in, a, r, L, nb, rowb, acc);
 }
 
 // The compute and stores of one step: input row r (in `in`) enters stage 0 and every
 // stage advances one row.
-template <bool G, int K, int PX, bool VIN>
+template <bool G, int K, int PX, bool VIN, bool FM>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                              const IterArgs &a, int r, const RollLane &L,
                                              unsigned nb, unsigned rowb, double &acc) {
@@ -1548,13 +1600,13 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
     for (int j = 0; j < PX; ++j) {
       float n1, n2, n3 = 0.0f;
       if (VIN && n == 1)
-        u_from_v<G>(S.U1p[0][j], S.U2p[0][j], S.U3p[0][j], S.P11c[0][j],
+        u_from_v<G, FM>(S.U1p[0][j], S.U2p[0][j], S.U3p[0][j], S.P11c[0][j],
                     left_of<PX>(S.P11c[0], j), S.P12c[0][j], S.P12p[0][j], S.P21c[0][j],
                     left_of<PX>(S.P21c[0], j), S.P22c[0][j], S.P22p[0][j], S.P31c[0][j],
                     G ? left_of<PX>(S.P31c[0], j) : 0.0f, S.P32c[0][j], S.P32p[0][j], L.X + j,
                     yU, a, n1, n2, n3);
       else
-        estimate_u_px<G>(S.CX[n - 1][j], S.CY[n - 1][j], S.CR[n - 1][j], S.U1p[n - 1][j],
+        estimate_u_px<G, FM>(S.CX[n - 1][j], S.CY[n - 1][j], S.CR[n - 1][j], S.U1p[n - 1][j],
                          S.U2p[n - 1][j], S.U3p[n - 1][j], S.P11c[n - 1][j],
                          left_of<PX>(S.P11c[n - 1], j), S.P12c[n - 1][j], S.P12p[n - 1][j],
                          S.P21c[n - 1][j], left_of<PX>(S.P21c[n - 1], j), S.P22c[n - 1][j],
@@ -1580,12 +1632,14 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
 #pragma unroll
     for (int j = 0; j < PX; ++j) {
       const bool has_right = L.X + j + 1 < a.W;
-      dual_px(S.U1p[n][j], right_of<PX>(S.U1p[n], j), S.U1c[n][j], has_right, has_down, a.taut,
-              S.P11p[n - 1][j], S.P12p[n - 1][j], S.P11c[n][j], S.P12c[n][j]);
-      dual_px(S.U2p[n][j], right_of<PX>(S.U2p[n], j), S.U2c[n][j], has_right, has_down, a.taut,
-              S.P21p[n - 1][j], S.P22p[n - 1][j], S.P21c[n][j], S.P22c[n][j]);
+      dual_px<false, false, FM>(S.U1p[n][j], right_of<PX>(S.U1p[n], j), S.U1c[n][j], has_right,
+                                has_down, a.taut, S.P11p[n - 1][j], S.P12p[n - 1][j],
+                                S.P11c[n][j], S.P12c[n][j]);
+      dual_px<false, false, FM>(S.U2p[n][j], right_of<PX>(S.U2p[n], j), S.U2c[n][j], has_right,
+                                has_down, a.taut, S.P21p[n - 1][j], S.P22p[n - 1][j],
+                                S.P21c[n][j], S.P22c[n][j]);
       if (G)
-        dual_px(S.U3p[n][j], right_of<PX>(S.U3p[n], j), S.U3c[n][j], has_right, has_down,
+        dual_px<false, false, FM>(S.U3p[n][j], right_of<PX>(S.U3p[n], j), S.U3c[n][j], has_right, has_down,
                 a.taut, S.P31p[n - 1][j], S.P32p[n - 1][j], S.P31c[n][j], S.P32c[n][j]);
     }
     if (n == K) {
@@ -1606,7 +1660,7 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
 template <int K, int PX>
 constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
 
-template <bool G, int K, int PX>
+template <bool G, int K, int PX, bool FM = false>
 __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
   constexpr int HALO = roll_halo<K, PX>();
   constexpr int BW = 64 * PX;            // band width (px)
@@ -1671,8 +1725,8 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
     dummy_stores();
     const int halves = (L.ye + K - r0 + 1) / 2;
     for (int h = 0, r = r0; h < halves; ++h, r += 2) {
-      roll_step<G, K, PX>(S, A, B, a, r, L, nb, rowb, acc);
-      roll_step<G, K, PX>(S, B, A, a, r + 1, L, nb, rowb, acc);
+      roll_step<G, K, PX, FM>(S, A, B, a, r, L, nb, rowb, acc);
+      roll_step<G, K, PX, FM>(S, B, A, a, r + 1, L, nb, rowb, acc);
     }
   } else {   // 3-row ring, steps unrolled by 3
     static_assert(roll_ahead<PX>() == 2, "the step loop below is unrolled for a 3-row ring");
@@ -1684,9 +1738,9 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
     // steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K (rows >= H drain the pipeline)
     const int thirds = (L.ye + K - r0 + 2) / 3;
     for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
-      roll_step<G, K, PX>(S, A, C, a, r, L, nb, rowb, acc);
-      roll_step<G, K, PX>(S, B, A, a, r + 1, L, nb, rowb, acc);
-      roll_step<G, K, PX>(S, C, B, a, r + 2, L, nb, rowb, acc);
+      roll_step<G, K, PX, FM>(S, A, C, a, r, L, nb, rowb, acc);
+      roll_step<G, K, PX, FM>(S, B, A, a, r + 1, L, nb, rowb, acc);
+      roll_step<G, K, PX, FM>(S, C, B, a, r + 2, L, nb, rowb, acc);
     }
   }
   if (a.calc_err) {
@@ -1951,7 +2005,7 @@ struct WiLane {
   bool outc;
 };
 
-template <int M>
+template <int M, bool FM>
 __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__restrict__ cring,
                                              const WarpRowI &cur, WarpRowI &ahead,
                                              const WarpRingArgs &wa, const WarpIterArgs &w,
@@ -1974,14 +2028,14 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
   float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
   const bool inwin = fx - 1 >= P.xw0 && fx + 2 < P.xw0 + WW && fy - 1 >= gy - M && fy + 2 <= gy + M;
   if (inwin) {
-    warp_gather_fn(
+    warp_gather_fn<FM>(
         [&](int cy, int cx) {
           const float *q = ring + (cy & (kWiRows - 1)) * (3 * WW) + (cx - P.xw0);
           return Tap3{q[0], q[WW], q[2 * WW]};
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
   } else {
-    warp_gather_fn(
+    warp_gather_fn<FM>(
         [&](int cy, int cx) {
           const int rx = imin(imax(cx, 0), wa.W - 1), ry = imin(imax(cy, 0), wa.H - 1);
           const float *row = wa.I1 + (size_t)ry * wa.P;
@@ -1992,15 +2046,16 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
   }
-  const float coeff = 1.0f / wsum;
+  const float coeff = FM ? __builtin_amdgcn_rcpf(wsum) : 1.0f / wsum;
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
-  const float rh = I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0;
+  const float rh = FM ? __builtin_fmaf(-I1wyv, cur.u2, __builtin_fmaf(-I1wxv, cur.u1, I1wv)) - cur.i0
+                      : I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0;
   // the first iteration's TH step is pointwise: the producer does it (the consumer sets
   // the block's pace), and the C ring carries v = u^0 + d instead of u^0
   float v1, v2, v3;
-  th_px<false>(I1wxv, I1wyv, rh, cur.u1, cur.u2, 0.0f, w.ra.it, v1, v2, v3);
+  th_px<false, FM>(I1wxv, I1wyv, rh, cur.u1, cur.u2, 0.0f, w.ra.it, v1, v2, v3);
   float *c = cring + (g & 1) * (5 * kWiBW) + P.ci;
   c[0] = I1wxv;
   c[kWiBW] = I1wyv;
@@ -2027,6 +2082,7 @@ __device__ __forceinline__ void wi_p_load(WiP &v, const IterArgs &a, unsigned nb
   bload<2>(v.p22, a.p22s, nb, voff, soff);
 }
 
+template <bool FM>
 __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, 2> &S,
                                              const float *__restrict__ cring, const WiP &cur,
                                              WiP &ahead, const IterArgs &a, int r,
@@ -2049,10 +2105,10 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, 2> &S,
     in.p21[j] = cur.p21[j]; in.p22[j] = cur.p22[j];
     in.p31[j] = in.p32[j] = 0.0f;
   }
-  roll_advance<false, 2, 2, true>(S, in, a, r, L, nb, rowb, acc);
+  roll_advance<false, 2, 2, true, FM>(S, in, a, r, L, nb, rowb, acc);
 }
 
-template <int M>
+template <int M, bool FM = false>
 __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
   constexpr int K = 2, PX = 2, HALO = roll_halo<2, 2>(), WW = wi_ww<M>();
   static_assert(2 * M + 2 <= kWiRows, "window ring too small for the margin");
@@ -2116,9 +2172,9 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
     lds_barrier();   // the producers' first step (row r0)
     double acc = 0.0;
     for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
-      wi_cons_step(S, cring, A, C, a, r, L, lane, nb, rowb, acc);
-      wi_cons_step(S, cring, B, A, a, r + 1, L, lane, nb, rowb, acc);
-      wi_cons_step(S, cring, C, B, a, r + 2, L, lane, nb, rowb, acc);
+      wi_cons_step<FM>(S, cring, A, C, a, r, L, lane, nb, rowb, acc);
+      wi_cons_step<FM>(S, cring, B, A, a, r + 1, L, lane, nb, rowb, acc);
+      wi_cons_step<FM>(S, cring, C, B, a, r + 2, L, lane, nb, rowb, acc);
     }
     lds_barrier();   // the producers' last two steps
     lds_barrier();
@@ -2173,9 +2229,9 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
     warp_ring_load(B, wa, nb, rowb, r0 + 1 + M, xs);
     warp_flow_load(B, wa, nb, rowb, r0 + 1, P.xcb);
     for (int h = 0, g = r0; h <= thirds; ++h, g += 3) {
-      wi_prod_step<M>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
-      wi_prod_step<M>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
-      wi_prod_step<M>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
     }
   }
 }

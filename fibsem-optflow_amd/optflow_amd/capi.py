@@ -19,6 +19,7 @@ ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
 ORACLE_SO = REPO_ROOT / "oracle" / "liboracle_tvl1.so"
 
 TVL1_MAX_LEVELS = 32
+ABI_VERSION = 2          # TVL1_ABI_VERSION of include/tvl1.h
 STATUS = {0: "TVL1_OK", 1: "TVL1_EINVAL", 2: "TVL1_ESIZE", 3: "TVL1_EHIP",
           4: "TVL1_ENOMEM", 5: "TVL1_ENODEV"}
 
@@ -36,6 +37,7 @@ class TVL1Params(C.Structure):
         ("gamma", C.c_double),
         ("use_initial_flow", C.c_int32),
         ("median_filtering", C.c_int32),
+        ("fast_math", C.c_int32),
     ]
 
 
@@ -61,13 +63,13 @@ class TVL1Stats(C.Structure):
 # generate_TV_args defaults, /root/reference/src/optflow.cpp:503-512
 DEFAULTS = dict(tau=0.25, lambda_=0.05, theta=0.3, nscales=10, warps=5, epsilon=0.01,
                 iterations=300, scale_step=0.8, gamma=0.0, use_initial_flow=0,
-                median_filtering=1)
+                median_filtering=1, fast_math=0)
 
 # JSON key -> struct field (JSON keys are the reference's, optflow.cpp:503-512)
 JSON_KEYS = {"tau": "tau", "lambda": "lambda_", "theta": "theta", "nscales": "nscales",
              "warps": "warps", "epsilon": "epsilon", "iterations": "iterations",
              "scaleStep": "scale_step", "gamma": "gamma", "useInitialFlow": "use_initial_flow",
-             "medianFiltering": "median_filtering"}
+             "medianFiltering": "median_filtering", "fastMath": "fast_math"}
 
 
 def make_params(**kw) -> TVL1Params:
@@ -139,7 +141,8 @@ def load_engine() -> C.CDLL:
     """The product: libtvl1_hip.so (HIP kernels for gfx950 + C-ABI).  Raises
     if it was not built — there is no CPU fallback."""
     # TVL1_ENGINE_SO: another build of the same engine (A/B runs of tools/ab_lib.sh)
-    lib = Library(Path(os.environ.get("TVL1_ENGINE_SO", ENGINE_SO))).lib
+    path = Path(os.environ.get("TVL1_ENGINE_SO", ENGINE_SO))
+    lib = Library(path).lib
     lib.tvl1_params_default.argtypes = [C.POINTER(TVL1Params)]
     lib.tvl1_params_default.restype = None
     lib.tvl1_create.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.POINTER(TVL1Params)]
@@ -169,6 +172,8 @@ def load_engine() -> C.CDLL:
     lib.tvl1_last_error.restype = C.c_char_p
     lib.tvl1_abi_version.restype = C.c_int32
     lib.tvl1_device_count.restype = C.c_int32
+    if lib.tvl1_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{path}: ABI version {lib.tvl1_abi_version()}, binding expects {ABI_VERSION}")
     return lib
 
 

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TVL1_ABI_VERSION 1
+#define TVL1_ABI_VERSION 2
 #define TVL1_MAX_LEVELS 32
 
 typedef enum tvl1_status {
@@ -73,6 +73,11 @@ typedef struct tvl1_params {
   double gamma;        /* 0.0   optflow.cpp:511 */
   int32_t use_initial_flow; /* read at optflow.cpp:512 but NOT passed to create() (:518): ignored, as in the reference */
   int32_t median_filtering; /* build-only: 1 = off (reference behaviour); 3 or 5 = median of u,v before each warp */
+  int32_t fast_math;   /* build-only: 0 = IEEE float32, bit-identical to oracle/ (default);
+                          1 = the reference build's CUDA_FAST_MATH semantics (singularity/optflow.def:33-34):
+                          approximate division and sqrt, fused multiply-add.  Held to the north-star
+                          tolerance (mean EPE <= 1e-3 px vs oracle/), not to bit identity.  gamma != 0
+                          solves stay IEEE. */
 } tvl1_params;
 
 /* Per-call statistics.  Valid after tvl1_calc returns (host-side counters). */
