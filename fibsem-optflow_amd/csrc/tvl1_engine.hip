@@ -91,7 +91,8 @@ struct tvl1_ctx {
   long fuse_min = 5000000;   // smaller levels: k_warp_ring + the pass (as fast, and their
                              // warps mostly run past the first check)
   int fuse_slots[8] = {};    // resident k_warp_pass<M> wavefronts per device
-  int witer_slots[8] = {};   // resident k_warp_iter<M> blocks per device
+  int witer_slots[8][2] = {};   // resident k_warp_iter<M, -, BW> blocks per device [M][BW == 64]
+  int witer_bw = 128;           // TVL1_WITER_BW: k_warp_iter band width (128: 2 producers, 64: 1)
   int fuse_store = 0;        // TVL1_FUSE_STORE=1: k_warp_iter always stores the constants
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
@@ -633,9 +634,11 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           w.store_c = c->fuse_store || wp == 0 || last_warp_n != 2;
           fused_nostore = !w.store_c;
           const int M = c->warp_margin == 4 ? 4 : 6;
-          w.ra.bands = (lw + 123) / 124;
+          const int BW = c->witer_bw;
+          w.ra.bands = (lw + BW - 5) / (BW - 4);
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                          : roll_segment(w.ra.bands, lh, 2 + M, c->witer_slots[M]);
+                                          : roll_segment(w.ra.bands, lh, 2 + M,
+                                                         c->witer_slots[M][BW == 64]);
           w.ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           w.ra.waves = w.ra.bands * segs;
@@ -643,22 +646,29 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
                            c->partials_cap);
-          if (M == 4 && fm)
-            hipLaunchKernelGGL((k_warp_iter<4, true>), dim3(w.ra.waves), dim3(192), 0, st, w);
-          else if (M == 4)
-            hipLaunchKernelGGL(k_warp_iter<4>, dim3(w.ra.waves), dim3(192), 0, st, w);
-          else if (fm)
-            hipLaunchKernelGGL((k_warp_iter<6, true>), dim3(w.ra.waves), dim3(192), 0, st, w);
-          else
-            hipLaunchKernelGGL(k_warp_iter<6>, dim3(w.ra.waves), dim3(192), 0, st, w);
-          // compulsory: p, u, I0 and the I1 window (x 1 + 2M/128) per band column and row;
+#define WITER_LAUNCH(MM, BB)                                                                   \
+  if (fm)                                                                                      \
+    hipLaunchKernelGGL((k_warp_iter<MM, true, BB>), dim3(w.ra.waves), dim3(64 + BB), 0, st, w); \
+  else                                                                                         \
+    hipLaunchKernelGGL((k_warp_iter<MM, false, BB>), dim3(w.ra.waves), dim3(64 + BB), 0, st, w);
+          if (M == 4 && BW == 64) {
+            WITER_LAUNCH(4, 64)
+          } else if (M == 4) {
+            WITER_LAUNCH(4, 128)
+          } else if (BW == 64) {
+            WITER_LAUNCH(6, 64)
+          } else {
+            WITER_LAUNCH(6, 128)
+          }
+#undef WITER_LAUNCH
+          // compulsory: p, u, I0 and the I1 window (x 1 + 2M/BW) per band column and row;
           // u, p (+ the constants) stored
           double rows = 0.0;
           for (int sg = 0; sg < segs; ++sg) {
             const int ys = sg * seg, ye = std::min(ys + seg, lh);
             rows += std::min(ye - 1 + 2, lh - 1) - std::max(ys - 2, 0) + 1;
           }
-          hbm = (double)w.ra.bands * 128.0 * rows * 4.0 * ((p_zero ? 3 : 7) + (128.0 + 2 * M) / 128.0) +
+          hbm = (double)w.ra.bands * BW * rows * 4.0 * ((p_zero ? 3 : 7) + (double)(BW + 2 * M) / BW) +
                 Nl * 4.0 * (6.0 + (w.store_c ? 3.0 : 0.0));
           alg_extra = Nl * 40.0;   // 40 B/px per warp
         } else if (fuse && n == 0 && k == 2 && calc_end) {
@@ -962,6 +972,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_WARP_MARGIN")) c->warp_margin = atoi(m);
   if (const char *m = getenv("TVL1_WARP_NW")) c->warp_nw = atoi(m);
   if (const char *m = getenv("TVL1_FUSE_STORE")) c->fuse_store = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_WITER_BW")) c->witer_bw = atoi(m) == 64 ? 64 : 128;
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse_first = atoi(m) == 1 ? 1 : atoi(m) == 2 ? 2 : 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // tests: force the 64-bit-addressed kernels
@@ -1017,8 +1028,10 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
 #undef RING_SLOTS
     c->fuse_slots[4] = blocks_of((const void *)k_warp_pass<4>, 64);
     c->fuse_slots[6] = blocks_of((const void *)k_warp_pass<6>, 64);
-    c->witer_slots[4] = blocks_of((const void *)k_warp_iter<4>, 192);
-    c->witer_slots[6] = blocks_of((const void *)k_warp_iter<6>, 192);
+    c->witer_slots[4][0] = blocks_of((const void *)k_warp_iter<4>, 192);
+    c->witer_slots[6][0] = blocks_of((const void *)k_warp_iter<6>, 192);
+    c->witer_slots[4][1] = blocks_of((const void *)k_warp_iter<4, false, 64>, 128);
+    c->witer_slots[6][1] = blocks_of((const void *)k_warp_iter<6, false, 64>, 128);
     (void)hipGetLastError();
   }
   *out = c;

@@ -1976,24 +1976,25 @@ struct WarpIterArgs {
 };
 
 constexpr int kWiRows = 16;   // window ring rows
-constexpr int kWiBW = 128;    // band width (px): 64 consumer lanes x 2 px
-template <int M>
-constexpr int wi_ww() { return kWiBW + 2 * M; }
+// band width BW (px): 128 = 64 consumer lanes x 2 px + 2 producers (default), or 64 =
+// 64 lanes x 1 px + 1 producer (consumer and producer steps of similar length)
+template <int M, int BW>
+constexpr int wi_ww() { return BW + 2 * M; }
 
 // window row r enters the ring: slot 64p + lane, and (producer 0, lanes < 2M) 128 + lane
-template <int M>
+template <int M, int BW>
 __device__ __forceinline__ void wi_ring_put(float *__restrict__ ring, const WarpRowI &v, int r,
                                             int p, int lane) {
-  constexpr int WW = wi_ww<M>();
+  constexpr int WW = wi_ww<M, BW>();
   float *dst = ring + (r & (kWiRows - 1)) * (3 * WW);
   const int k0 = 64 * p + lane;
   dst[k0] = v.c0;
   dst[WW + k0] = 0.5f * (v.r0 - v.l0);
   dst[2 * WW + k0] = 0.5f * (v.s0 - v.n0);
   if (p == 0 && lane < 2 * M) {
-    dst[kWiBW + lane] = v.c1;
-    dst[WW + kWiBW + lane] = 0.5f * (v.r1 - v.l1);
-    dst[2 * WW + kWiBW + lane] = 0.5f * (v.s1 - v.n1);
+    dst[BW + lane] = v.c1;
+    dst[WW + BW + lane] = 0.5f * (v.r1 - v.l1);
+    dst[2 * WW + BW + lane] = 0.5f * (v.s1 - v.n1);
   }
 }
 
@@ -2005,19 +2006,19 @@ struct WiLane {
   bool outc;
 };
 
-template <int M, bool FM>
+template <int M, bool FM, int BW>
 __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__restrict__ cring,
                                              const WarpRowI &cur, WarpRowI &ahead,
                                              const WarpRingArgs &wa, const WarpIterArgs &w,
                                              int g, int p, int lane, const WiLane &P,
                                              const unsigned (&xs)[2][3], int ys, int ye,
                                              unsigned nb, unsigned rowb) {
-  constexpr int WW = wi_ww<M>();
+  constexpr int WW = wi_ww<M, BW>();
   // loads for row g + kWarpAhead: window row g + kWarpAhead + M and its flow row
   warp_ring_load(ahead, wa, nb, rowb, g + kWarpAhead + M, xs);
   warp_flow_load(ahead, wa, nb, rowb, g + kWarpAhead, P.xcb);
   __builtin_amdgcn_sched_barrier(0);
-  wi_ring_put<M>(ring, cur, g + M, p, lane);
+  wi_ring_put<M, BW>(ring, cur, g + M, p, lane);
   lds_barrier();
   // rows past the image bottom repeat row H-1 (the pass clamps its input rows)
   const int gy = imin(g, wa.H - 1);
@@ -2056,12 +2057,12 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
   // the block's pace), and the C ring carries v = u^0 + d instead of u^0
   float v1, v2, v3;
   th_px<false, FM>(I1wxv, I1wyv, rh, cur.u1, cur.u2, 0.0f, w.ra.it, v1, v2, v3);
-  float *c = cring + (g & 1) * (5 * kWiBW) + P.ci;
+  float *c = cring + (g & 1) * (5 * BW) + P.ci;
   c[0] = I1wxv;
-  c[kWiBW] = I1wyv;
-  c[2 * kWiBW] = rh;
-  c[3 * kWiBW] = v1;
-  c[4 * kWiBW] = v2;
+  c[BW] = I1wyv;
+  c[2 * BW] = rh;
+  c[3 * BW] = v1;
+  c[4 * BW] = v2;
   if (w.store_c) {
     const unsigned vo = P.outc && g >= ys && g < ye ? (unsigned)g * rowb + P.xcb : kOOB;
     bstore<kWarpStoreAux>(wa.I1wx, nb, vo, 0, I1wxv);
@@ -2070,52 +2071,56 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
   }
 }
 
-struct WiP {   // the consumer's HBM input of one row: p at its 2 px
-  float p11[2], p12[2], p21[2], p22[2];
+template <int PX>
+struct WiP {   // the consumer's HBM input of one row: p at its PX px
+  float p11[PX], p12[PX], p21[PX], p22[PX];
 };
 
-__device__ __forceinline__ void wi_p_load(WiP &v, const IterArgs &a, unsigned nb, unsigned soff,
+template <int PX>
+__device__ __forceinline__ void wi_p_load(WiP<PX> &v, const IterArgs &a, unsigned nb, unsigned soff,
                                           unsigned voff) {
-  bload<2>(v.p11, a.p11s, nb, voff, soff);
-  bload<2>(v.p12, a.p12s, nb, voff, soff);
-  bload<2>(v.p21, a.p21s, nb, voff, soff);
-  bload<2>(v.p22, a.p22s, nb, voff, soff);
+  bload<PX>(v.p11, a.p11s, nb, voff, soff);
+  bload<PX>(v.p12, a.p12s, nb, voff, soff);
+  bload<PX>(v.p21, a.p21s, nb, voff, soff);
+  bload<PX>(v.p22, a.p22s, nb, voff, soff);
 }
 
-template <bool FM>
-__device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, 2> &S,
-                                             const float *__restrict__ cring, const WiP &cur,
-                                             WiP &ahead, const IterArgs &a, int r,
+template <bool FM, int PX>
+__device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
+                                             const float *__restrict__ cring, const WiP<PX> &cur,
+                                             WiP<PX> &ahead, const IterArgs &a, int r,
                                              const RollLane &L, int lane, unsigned nb,
                                              unsigned rowb, double &acc) {
   wi_p_load(ahead, a, nb, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vload);
   __builtin_amdgcn_sched_barrier(0);
   lds_barrier();   // C ring row r was written at the previous step
-  RollIn<false, 2> in;
-  const float *c = cring + (r & 1) * (5 * kWiBW) + 2 * lane;
-  in.wx[0] = c[0]; in.wx[1] = c[1];
-  in.wy[0] = c[kWiBW]; in.wy[1] = c[kWiBW + 1];
-  in.rh[0] = c[2 * kWiBW]; in.rh[1] = c[2 * kWiBW + 1];
-  in.u1[0] = c[3 * kWiBW]; in.u1[1] = c[3 * kWiBW + 1];   // v (roll_advance<.., VIN>)
-  in.u2[0] = c[4 * kWiBW]; in.u2[1] = c[4 * kWiBW + 1];
-  in.u3[0] = in.u3[1] = 0.0f;
+  constexpr int BW = 64 * PX;
+  RollIn<false, PX> in;
+  const float *c = cring + (r & 1) * (5 * BW) + PX * lane;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < PX; ++j) {
+    in.wx[j] = c[j];
+    in.wy[j] = c[BW + j];
+    in.rh[j] = c[2 * BW + j];
+    in.u1[j] = c[3 * BW + j];   // v (roll_advance<.., VIN>)
+    in.u2[j] = c[4 * BW + j];
+    in.u3[j] = 0.0f;
     in.p11[j] = cur.p11[j]; in.p12[j] = cur.p12[j];
     in.p21[j] = cur.p21[j]; in.p22[j] = cur.p22[j];
     in.p31[j] = in.p32[j] = 0.0f;
   }
-  roll_advance<false, 2, 2, true, FM>(S, in, a, r, L, nb, rowb, acc);
+  roll_advance<false, 2, PX, true, FM>(S, in, a, r, L, nb, rowb, acc);
 }
 
-template <int M, bool FM = false>
-__global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
-  constexpr int K = 2, PX = 2, HALO = roll_halo<2, 2>(), WW = wi_ww<M>();
+template <int M, bool FM = false, int BW = 128>
+__global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
+  constexpr int K = 2, PX = BW / 64, HALO = roll_halo<2, PX>(), WW = wi_ww<M, BW>();
+  static_assert(BW == 64 || BW == 128, "one producer per 64 columns, PX = 1 or 2");
   static_assert(2 * M + 2 <= kWiRows, "window ring too small for the margin");
   static_assert(2 * M <= 64, "second window slot per lane");
   static_assert(kRollAhead == 2 && kWarpAhead == 2, "the step loops are unrolled by 3");
   __shared__ float ring[kWiRows * 3 * WW];
-  __shared__ float cring[2 * 5 * kWiBW];
+  __shared__ float cring[2 * 5 * BW];
   const RollArgs &ra = w.ra;
   const IterArgs &a = ra.it;
   const int lane = threadIdx.x & 63;
@@ -2125,7 +2130,7 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
   // a raised s_setprio for it, is slower)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int band = wid % ra.bands, seg = wid / ra.bands;
-  const int X0 = band * (kWiBW - 2 * HALO) - HALO;   // the band's first px
+  const int X0 = band * (BW - 2 * HALO) - HALO;   // the band's first px
   const unsigned nb = 4u * (unsigned)a.P * (unsigned)a.H;
   const unsigned rowb = 4u * (unsigned)a.P;
   const int ys = seg * ra.seg_rows, ye = imin(ys + ra.seg_rows, a.H);
@@ -2137,7 +2142,7 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
     RollLane L;
     L.X = X0 + PX * lane;
     L.vload = 4u * imin(imax(L.X, 0), a.P - PX);
-    L.out = PX * lane >= HALO && PX * lane < kWiBW - HALO && L.X < a.W;
+    L.out = PX * lane >= HALO && PX * lane < BW - HALO && L.X < a.W;
     L.vst = 4u * (unsigned)imax(L.X, 0);
     L.ys = ys;
     L.ye = ye;
@@ -2156,7 +2161,9 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
       for (int j = 0; j < PX; ++j) S.CX[n][j] = S.CY[n][j] = S.CR[n][j] = 0.0f;
     // as many dropped stores after each prologue load as a step issues (k_iterate_roll)
     auto dummy_stores = [&]() {
-      float z[PX] = {0.0f, 0.0f};
+      float z[PX];
+#pragma unroll
+      for (int j = 0; j < PX; ++j) z[j] = 0.0f;
       bstorev<PX>(a.u1d, nb, kOOB, z);
       bstorev<PX>(a.u2d, nb, kOOB, z);
       bstorev<PX>(a.p11d, nb, kOOB, z);
@@ -2164,7 +2171,7 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
       bstorev<PX>(a.p21d, nb, kOOB, z);
       bstorev<PX>(a.p22d, nb, kOOB, z);
     };
-    WiP A, B, C;
+    WiP<PX> A, B, C;
     wi_p_load(A, a, nb, (unsigned)r0 * rowb, L.vload);
     dummy_stores();
     wi_p_load(B, a, nb, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
@@ -2172,9 +2179,9 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
     lds_barrier();   // the producers' first step (row r0)
     double acc = 0.0;
     for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
-      wi_cons_step<FM>(S, cring, A, C, a, r, L, lane, nb, rowb, acc);
-      wi_cons_step<FM>(S, cring, B, A, a, r + 1, L, lane, nb, rowb, acc);
-      wi_cons_step<FM>(S, cring, C, B, a, r + 2, L, lane, nb, rowb, acc);
+      wi_cons_step<FM, PX>(S, cring, A, C, a, r, L, lane, nb, rowb, acc);
+      wi_cons_step<FM, PX>(S, cring, B, A, a, r + 1, L, lane, nb, rowb, acc);
+      wi_cons_step<FM, PX>(S, cring, C, B, a, r + 2, L, lane, nb, rowb, acc);
     }
     lds_barrier();   // the producers' last two steps
     lds_barrier();
@@ -2202,13 +2209,13 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
     const int px = X0 + P.ci;
     P.xc = imin(imax(px, 0), a.W - 1);
     P.xcb = 4u * (unsigned)P.xc;
-    P.outc = P.ci >= HALO && P.ci < kWiBW - HALO && px >= 0 && px < a.W;
+    P.outc = P.ci >= HALO && P.ci < BW - HALO && px >= 0 && px < a.W;
     // the lane's window slots (clamped column, its clamped x-1 and x+1): 64p + lane, and
     // 128 + lane for producer 0's lanes < 2M (other lanes re-read the first slot)
     unsigned xs[2][3];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const int slot = k == 1 && p == 0 && lane < 2 * M ? kWiBW + lane : P.ci;
+      const int slot = k == 1 && p == 0 && lane < 2 * M ? BW + lane : P.ci;
       const int cc = imin(imax(P.xw0 + slot, 0), a.W - 1);
       xs[k][0] = 4u * cc;
       xs[k][1] = 4u * imax(cc - 1, 0);
@@ -2221,7 +2228,7 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
 #pragma unroll
       for (int i = 0; i < M; ++i) warp_ring_load(t[i], wa, nb, rowb, r0 - M + b * M + i, xs);
 #pragma unroll
-      for (int i = 0; i < M; ++i) wi_ring_put<M>(ring, t[i], r0 - M + b * M + i, p, lane);
+      for (int i = 0; i < M; ++i) wi_ring_put<M, BW>(ring, t[i], r0 - M + b * M + i, p, lane);
     }
     WarpRowI A, B, C;
     warp_ring_load(A, wa, nb, rowb, r0 + M, xs);
@@ -2229,9 +2236,9 @@ __global__ __launch_bounds__(192) void k_warp_iter(WarpIterArgs w) {
     warp_ring_load(B, wa, nb, rowb, r0 + 1 + M, xs);
     warp_flow_load(B, wa, nb, rowb, r0 + 1, P.xcb);
     for (int h = 0, g = r0; h <= thirds; ++h, g += 3) {
-      wi_prod_step<M, FM>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
-      wi_prod_step<M, FM>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
-      wi_prod_step<M, FM>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM, BW>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM, BW>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM, BW>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
     }
   }
 }

@@ -22,7 +22,7 @@ FAR_SHARE_TOL = 1e-3
 
 KNOBS = ("TVL1_ITER_MODE", "TVL1_ROLL_SEG", "TVL1_ROLL_PX", "TVL1_ROLL_PX_SHORT",
          "TVL1_ROLL_PX4_MIN", "TVL1_TB_CFG", "TVL1_TB_CFG_LONG", "TVL1_WARP_MODE",
-         "TVL1_FUSE", "TVL1_FUSE_MIN", "TVL1_FUSE_STORE", "TVL1_WARP_MARGIN", "TVL1_BUF_LIMIT")
+         "TVL1_FUSE", "TVL1_FUSE_MIN", "TVL1_WITER_BW", "TVL1_FUSE_STORE", "TVL1_WARP_MARGIN", "TVL1_BUF_LIMIT")
 
 
 def _solve(monkeypatch, env, W, H, seed, kw):
@@ -49,7 +49,7 @@ CASES = [
 ]
 # every fast kernel: hybrid default, fused warp + first pass on small levels, 4 px/lane
 # rolling passes, rolling-only, each blocked-region shape
-ENVS = ["", "TVL1_FUSE_MIN=0,TVL1_ROLL_PX4_MIN=0", "TVL1_FUSE_MIN=0,TVL1_WARP_MARGIN=4",
+ENVS = ["", "TVL1_FUSE_MIN=0,TVL1_ROLL_PX4_MIN=0", "TVL1_FUSE_MIN=0,TVL1_WARP_MARGIN=4", "TVL1_FUSE_MIN=0,TVL1_WITER_BW=64",
         "TVL1_ITER_MODE=2", "TVL1_ITER_MODE=0,TVL1_TB_CFG=0", "TVL1_ITER_MODE=0,TVL1_TB_CFG=1",
         "TVL1_ITER_MODE=0,TVL1_TB_CFG=2"]
 

@@ -113,10 +113,11 @@ MODES = ["TVL1_ITER_MODE=0", "TVL1_ITER_MODE=1", "TVL1_ITER_MODE=2", "TVL1_ITER_
          "TVL1_ROLL_PX4_MIN=0,TVL1_ITER_MODE=2", "TVL1_ROLL_PX_SHORT=2",
          "TVL1_FUSE_MIN=0", "TVL1_FUSE_MIN=0,TVL1_FUSE_STORE=1", "TVL1_FUSE_MIN=0,TVL1_ROLL_SEG=8",
          "TVL1_FUSE_MIN=0,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8", "TVL1_FUSE=0",
-         "TVL1_FUSE_MIN=0,TVL1_ROLL_PX4_MIN=0"]
+         "TVL1_FUSE_MIN=0,TVL1_ROLL_PX4_MIN=0", "TVL1_FUSE_MIN=0,TVL1_WITER_BW=64",
+         "TVL1_FUSE_MIN=0,TVL1_WITER_BW=64,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8"]
 KNOBS = ("TVL1_ITER_MODE", "TVL1_ROLL_SEG", "TVL1_ROLL_PX", "TVL1_ROLL_PX_SHORT", "TVL1_ROLL_PX4_MIN", "TVL1_ROLL_LDS", "TVL1_TB_CFG",
          "TVL1_TB_CFG_LONG", "TVL1_WARP_MODE",
-         "TVL1_SPECULATE", "TVL1_WARP_TH", "TVL1_WARP_MARGIN", "TVL1_WARP_LDS", "TVL1_WARP_NW", "TVL1_FUSE", "TVL1_FUSE_STORE", "TVL1_FUSE_MIN",
+         "TVL1_SPECULATE", "TVL1_WARP_TH", "TVL1_WARP_MARGIN", "TVL1_WARP_LDS", "TVL1_WARP_NW", "TVL1_FUSE", "TVL1_FUSE_STORE", "TVL1_FUSE_MIN", "TVL1_WITER_BW",
          "TVL1_ROLL_FILL", "TVL1_WARP_FILL", "TVL1_BUF_LIMIT")
 
 
@@ -161,7 +162,8 @@ def test_engine_reproduces_golden(engine, path):
                                  "TVL1_WARP_MODE=4", "TVL1_WARP_MODE=4,TVL1_WARP_MARGIN=4",
                                  "TVL1_FUSE=1", "TVL1_FUSE=1,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8",
                                  "TVL1_WARP_MODE=3,TVL1_WARP_MARGIN=4", "TVL1_FUSE_MIN=0",
-                                 "TVL1_FUSE_MIN=0,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8"])
+                                 "TVL1_FUSE_MIN=0,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8",
+                                 "TVL1_FUSE_MIN=0,TVL1_WITER_BW=64"])
 def test_large_flow_uses_global_gather_fallback(built, monkeypatch, env):
     """A ~7 px shift puts taps outside the warp kernels' LDS windows (margin 4-6 px):
     the global-memory fallback must give the same bits."""
