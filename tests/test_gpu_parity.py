@@ -186,3 +186,17 @@ def test_large_flow_uses_global_gather_fallback(built, monkeypatch, env):
     assert float(np.abs(ur).max()) > 5.0   # the case really leaves the window
     np.testing.assert_array_equal(wi, wr)
     assert bits_equal(u, ur) and bits_equal(v, vr)
+
+
+def test_benchmark_pair_bit_exact(engine):
+    """The bench workload itself (BASELINE configs[1], C2): one 6144x4096 synthetic pair,
+    5 scales, 30 warps -- the same bits and the same 880-odd iterations as the oracle."""
+    I0, I1 = synth.gen_pair(6144, 4096, seed=0x5EED, z=1)
+    p = capi.make_params(nscales=5, warps=30)
+    engine.set_params(p)
+    u, v, st, wi = engine.calc_host(I0, I1)
+    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    assert st["levels"] == sr["levels"] == 5
+    np.testing.assert_array_equal(wi, wr)
+    assert bits_equal(u, ur) and bits_equal(v, vr)
+    print(f"C2 pair: {int(wi.sum())} iterations, bit-exact vs oracle")
