@@ -391,7 +391,11 @@ def main():
                 "compulsory_bytes_per_launch": round(k_hbm / k_launch),
                 "compulsory_GBs": round(k_hbm / (k_ms * 1e-3) / 1e9, 1),
                 "compulsory_frac": round(k_hbm / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "kernel_busy_share": round(k_ms / wall_ms, 4)}
+                "kernel_busy_share": round(k_ms / wall_ms, 4),
+                # what actually limits these passes (profiles/r1/valu_util_*):
+                # VALU issue of the exact IEEE division / sqrt sequences, except the
+                # 2-iteration passes, which stream at 3.7-4.5 TB/s
+                "measured_bound": "valu (IEEE div/sqrt sequences; 2-iteration passes hbm)"}
 
     roof = None
     if k_ms > 0:
