@@ -70,6 +70,13 @@ def parse():
                          "reference build's CUDA_FAST_MATH semantics; tolerance parity, not "
                          "bit-identical). Default: IEEE (bit-identical to oracle/), with a "
                          "secondary fast-math measurement reported under \"fast_math\"")
+    ap.add_argument("--profile", type=int, default=0, choices=(0, 1),
+                    help="1 = OpenCV's CPU DualTVL1OpticalFlow schedule (SURVEY 8(f) N3; "
+                         "BASELINE configs[0]), with --inner / --outer iterations")
+    ap.add_argument("--inner", type=int, default=30)
+    ap.add_argument("--outer", type=int, default=10)
+    ap.add_argument("--lambda", dest="lam", type=float, default=0.05)
+    ap.add_argument("--median", type=int, default=1)
     ap.add_argument("--no-fast-math-line", action="store_true",
                     help="skip the secondary fast-math measurement")
     ap.add_argument("--cpu-sample", default="3072x2048")
@@ -268,7 +275,11 @@ def main():
     W, H = args.width, args.height
     params = capi.make_params(nscales=args.nscales, warps=args.warps,
                               iterations=args.iterations, epsilon=args.epsilon,
-                              fast_math=int(args.fast_math))
+                              fast_math=int(args.fast_math), profile=args.profile,
+                              inner_iterations=args.inner, outer_iterations=args.outer,
+                              lambda_=args.lam, median_filtering=args.median)
+    if args.profile == 1:
+        args.no_fast_math_line = True   # fast_math does not apply to profile 1
     # each rank gets its own slice pair(s) of the synthetic stack (z = rank*F + j + 1 vs base)
     F = max(1, args.inflight)
     dev = torch.device("cuda", local_rank)
@@ -342,7 +353,8 @@ def main():
         u_ref, v_ref = slots[0]["u"].clone(), slots[0]["v"].clone()
         alt_params = capi.make_params(nscales=args.nscales, warps=args.warps,
                                       iterations=args.iterations, epsilon=args.epsilon,
-                                      fast_math=0 if args.fast_math else 1)
+                                      fast_math=0 if args.fast_math else 1,
+                                      lambda_=args.lam, median_filtering=args.median)
         for sl in slots:
             sl["eng"].set_params(alt_params)
             sl["eng"].set_profiling(False)
@@ -425,10 +437,15 @@ def main():
         "math": "fast (CUDA_FAST_MATH semantics)" if args.fast_math else "IEEE (bit-identical to oracle/)",
         "data": "synthetic",
         "config": {
-            "workload": (("C2" if (W, H, args.nscales, args.warps) == (6144, 4096, 5, 30)
-                          else "pair") + f": one {W}x{H} u8 slice pair per GPU per step, nscales "
-                         f"{args.nscales}, warps {args.warps}, iterations {args.iterations}, "
-                         f"epsilon {args.epsilon} (reference defaults otherwise)"),
+            "workload": ((("C2" if (W, H, args.nscales, args.warps) == (6144, 4096, 5, 30)
+                           else "pair") + f": one {W}x{H} u8 slice pair per GPU per step, nscales "
+                          f"{args.nscales}, warps {args.warps}, iterations {args.iterations}, "
+                          f"epsilon {args.epsilon} (reference defaults otherwise)")
+                         if args.profile == 0 else
+                         (f"profile 1 (CPU DualTVL1OpticalFlow schedule): one {W}x{H} u8 pair "
+                          f"per GPU per step, nscales {args.nscales}, warps {args.warps}, "
+                          f"inner {args.inner} x outer {args.outer}, lambda {args.lam}, median "
+                          f"{args.median}, epsilon {args.epsilon}")),
             "pair": f"{W}x{H}",
             "parallelism": f"pairs sharded over {world} GPU(s), no data-path collective",
             "pairs_in_flight_per_gpu": F,

@@ -110,6 +110,10 @@ tvl1_params generate_TV_args(const Value &im, const Value &args) {
   p.use_initial_flow = im.get("useInitialFlow", args.get("useInitialFlow", false).asBool()).asBool();
   p.median_filtering = I("medianFiltering", 1);
   p.fast_math = I("fastMath", 0);
+  // build-only: OpenCV's CPU DualTVL1OpticalFlow schedule
+  p.profile = I("profile", 0);
+  p.inner_iterations = I("innerIterations", 30);
+  p.outer_iterations = I("outerIterations", 10);
   return p;
 }
 
@@ -552,6 +556,9 @@ static int from_file(Value &args, bool plan_only) {
           pl["tv"]["gamma"] = tp.gamma;
           pl["tv"]["medianFiltering"] = tp.median_filtering;
           pl["tv"]["fastMath"] = tp.fast_math;
+          pl["tv"]["profile"] = tp.profile;
+          pl["tv"]["innerIterations"] = tp.inner_iterations;
+          pl["tv"]["outerIterations"] = tp.outer_iterations;
           for (auto &key : rois.memberNames())
             pl["files"].append(im["output"].asString() +
                                ((key == "top" || key == "bottom") ? "_" + key : std::string()));

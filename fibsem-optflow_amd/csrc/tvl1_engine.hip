@@ -172,6 +172,11 @@ static tvl1_status check_params(tvl1_ctx *c, const tvl1_params *p) {
     return set_err(c, TVL1_EINVAL, "medianFiltering must be 1 (off), 3 or 5");
   if (p->fast_math != 0 && p->fast_math != 1)
     return set_err(c, TVL1_EINVAL, "fastMath must be 0 or 1 (got %d)", p->fast_math);
+  if (p->profile != 0 && p->profile != 1)
+    return set_err(c, TVL1_EINVAL, "profile must be 0 (CUDA OpticalFlowDual_TVL1) or 1 (CPU DualTVL1) (got %d)",
+                   p->profile);
+  if (p->inner_iterations < 0 || p->outer_iterations < 0)
+    return set_err(c, TVL1_EINVAL, "innerIterations / outerIterations must be >= 0");
   return TVL1_OK;
 }
 
@@ -354,10 +359,156 @@ static double survey_bytes(const Geometry &g, int warps, const int64_t *iters) {
 // spare constants buffer, the next ping-pong u set, the gradient of a level whose
 // gathers are done) and is redone at the next check.  Results are bit-identical
 // either way; the GPU just never idles while the host reads a residual.
+// resize(): an exact 2x downscale of INTER_LINEAR takes the INTER_AREA fast path
+static int area_fast_of(double sx, double sy) {
+  const int ix = (int)std::lrint(sx), iy = (int)std::lrint(sy);
+  return std::fabs(sx - ix) < DBL_EPSILON && std::fabs(sy - iy) < DBL_EPSILON && ix == 2 && iy == 2;
+}
+
+// Profile 1 (tvl1_params.profile): the schedule of OpenCV's CPU
+// cv::DualTVL1OpticalFlow::calc / procOneScale, restated in oracle/tvl1_oracle_dualtvl1.c.
+// Per warp: remap (k_remap_cubic), then up to outerIterations rounds, each starting with
+// medianFiltering, of up to innerIterations primal-dual iterations, every one of which
+// evaluates the residual (one k_iterate launch + k_reduce + one host read each).  This is
+// a compatibility mode, not the benchmark path: it keeps OpenCV's per-iteration check.
+static tvl1_status solve_dualtvl1(tvl1_ctx *c, const uint8_t *I0, size_t pitch0,
+                                  const uint8_t *I1, size_t pitch1, int W, int H, float *u,
+                                  float *v, size_t fpitch, tvl1_stats *stats, hipStream_t st) {
+  const tvl1_params &prm = c->prm;
+  const Geometry &g = c->geo;
+  const int L = g.L;
+  const bool gam = g.gamma;
+  const bool median = prm.median_filtering > 1;
+  hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 2), kBlk2, 0, st, I0, pitch0, I1, pitch1,
+                     c->I0s[0], c->I1s[0], W, H, g.ps[0]);
+  const double dscale = 1. / prm.scale_step;
+  const int afast = area_fast_of(dscale, dscale);
+  for (int s = 1; s < L; ++s)
+    hipLaunchKernelGGL(k_resize_hp, grid2(g.ws[s], g.hs[s], 2), kBlk2, 0, st, c->I0s[s - 1],
+                       c->I1s[s - 1], nullptr, g.ws[s - 1], g.hs[s - 1], g.ps[s - 1], c->I0s[s],
+                       c->I1s[s], nullptr, g.ws[s], g.hs[s], g.ps[s], dscale, dscale, afast, 0,
+                       1.0f);
+  HIP_TRY(c, hipGetLastError());
+  int ui = 0, pi = 0;
+  {
+    const size_t n = (size_t)g.ps[L - 1] * g.hs[L - 1] * sizeof(float);
+    for (int k = 0; k < (gam ? 3 : 2); ++k) HIP_TRY(c, hipMemsetAsync(c->U[ui][k], 0, n, st));
+  }
+  const float l_t = (float)(prm.lambda * prm.theta);
+  const float taut = (float)(prm.tau / prm.theta);
+  const bool exact_div = !(taut >= 0.0f && taut <= FLT_MAX);
+  const float upmul = (float)(1.0 / prm.scale_step);
+  int64_t level_iters[TVL1_MAX_LEVELS] = {};
+  for (int s = L - 1; s >= 0; --s) {
+    const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
+    const float scaledEps = (float)(prm.epsilon * prm.epsilon * (double)(lw * lh));
+    hipLaunchKernelGGL(k_gradient, grid2(lw, lh), kBlk2, 0, st, c->I1s[s], lw, lh, P, c->G);
+    IterArgs a{};
+    a.W = lw;
+    a.H = lh;
+    a.P = P;
+    a.segs = (lw + kSegPx - 1) / kSegPx;
+    a.strip_rows = kStripRows;
+    a.l_t = l_t;
+    a.theta = (float)prm.theta;
+    a.gamma = (float)prm.gamma;
+    a.taut = taut;
+    a.partials = c->partials;
+    a.calc_err = 1;
+    a.I1wx = c->C[0][0];
+    a.I1wy = c->C[0][1];
+    a.rho = c->C[0][2];
+    const int nblk = iterate_blocks(lw, lh);
+    bool p_zero = true;
+    for (int wp = 0; wp < prm.warps; ++wp) {
+      hipLaunchKernelGGL(k_remap_cubic, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G,
+                         c->U[ui][0], c->U[ui][1], lw, lh, P, c->C[0][0], c->C[0][1],
+                         c->C[0][2]);
+      float error = FLT_MAX;
+      int n = 0;
+      for (int no = 0; error > scaledEps && no < prm.outer_iterations; ++no) {
+        if (median) {
+          hipLaunchKernelGGL(k_median, grid2(lw, lh, 2), kBlk2, 0, st, c->U[ui][0], c->U[ui][1],
+                             lw, lh, P, prm.median_filtering, c->U[ui ^ 1][0], c->U[ui ^ 1][1]);
+          if (gam)
+            HIP_TRY(c, hipMemcpyAsync(c->U[ui ^ 1][2], c->U[ui][2], (size_t)P * lh * sizeof(float),
+                                      hipMemcpyDeviceToDevice, st));
+          ui ^= 1;
+        }
+        for (int ni = 0; error > scaledEps && ni < prm.inner_iterations; ++ni) {
+          a.u1s = c->U[ui][0]; a.u2s = c->U[ui][1]; a.u3s = c->U[ui][2];
+          a.u1d = c->U[ui ^ 1][0]; a.u2d = c->U[ui ^ 1][1]; a.u3d = c->U[ui ^ 1][2];
+          a.p11s = c->Pd[pi][0]; a.p12s = c->Pd[pi][1]; a.p21s = c->Pd[pi][2];
+          a.p22s = c->Pd[pi][3]; a.p31s = c->Pd[pi][4]; a.p32s = c->Pd[pi][5];
+          a.p11d = c->Pd[pi ^ 1][0]; a.p12d = c->Pd[pi ^ 1][1]; a.p21d = c->Pd[pi ^ 1][2];
+          a.p22d = c->Pd[pi ^ 1][3]; a.p31d = c->Pd[pi ^ 1][4]; a.p32d = c->Pd[pi ^ 1][5];
+          a.p_zero = p_zero ? 1 : 0;
+          if (gam && exact_div)
+            hipLaunchKernelGGL((k_iterate<true, true, true>), dim3(nblk), dim3(kBlock), 0, st, a);
+          else if (exact_div)
+            hipLaunchKernelGGL((k_iterate<false, true, true>), dim3(nblk), dim3(kBlock), 0, st, a);
+          else if (gam)
+            hipLaunchKernelGGL((k_iterate<true, false, true>), dim3(nblk), dim3(kBlock), 0, st, a);
+          else
+            hipLaunchKernelGGL((k_iterate<false, false, true>), dim3(nblk), dim3(kBlock), 0, st, a);
+          hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, nblk,
+                             c->pinned_dev);
+          HIP_TRY(c, hipEventRecord(c->ev_check, st));
+          HIP_TRY(c, hipEventSynchronize(c->ev_check));
+          error = (float)*c->pinned;
+          p_zero = false;
+          ui ^= 1;
+          pi ^= 1;
+          ++n;
+        }
+      }
+      level_iters[s] += n;
+      if (stats && stats->warp_iterations && s * prm.warps + wp < stats->warp_iterations_capacity)
+        stats->warp_iterations[s * prm.warps + wp] = n;
+    }
+    HIP_TRY(c, hipGetLastError());
+    if (s == 0) break;
+    // resize(u, .., I0s[s-1].size()), then multiply u1, u2 (not u3) by 1/scaleStep
+    const int dw = g.ws[s - 1], dh = g.hs[s - 1];
+    const double sxu = 1. / ((double)dw / lw), syu = 1. / ((double)dh / lh);
+    hipLaunchKernelGGL(k_resize_hp, grid2(dw, dh, gam ? 3 : 2), kBlk2, 0, st, c->U[ui][0],
+                       c->U[ui][1], c->U[ui][2], lw, lh, P, c->U[ui ^ 1][0], c->U[ui ^ 1][1],
+                       c->U[ui ^ 1][2], dw, dh, g.ps[s - 1], sxu, syu, area_fast_of(sxu, syu), 2,
+                       upmul);
+    ui ^= 1;
+  }
+  hipLaunchKernelGGL(k_output, grid2(W, H), kBlk2, 0, st, c->U[ui][0], c->U[ui][1], W, H,
+                     g.ps[0], u, v, fpitch);
+  HIP_TRY(c, hipGetLastError());
+  if (stats) {
+    stats->levels = L;
+    int64_t tot = 0;
+    for (int s = 0; s < TVL1_MAX_LEVELS; ++s) {
+      stats->level_width[s] = s < L ? g.ws[s] : 0;
+      stats->level_height[s] = s < L ? g.hs[s] : 0;
+      stats->level_iterations[s] = s < L ? level_iters[s] : 0;
+      tot += s < L ? level_iters[s] : 0;
+    }
+    stats->iterations_total = tot;
+    stats->checks_total = tot;
+    stats->speculation_misses = 0;
+    stats->algorithmic_bytes = survey_bytes(g, prm.warps, level_iters);
+    for (int k = 0; k < 4; ++k) {
+      stats->kernel_ms[k] = 0.0;
+      stats->kernel_launches[k] = 0;
+      stats->kernel_bytes[k] = 0.0;
+      stats->kernel_hbm_bytes[k] = 0.0;
+    }
+  }
+  return TVL1_OK;
+}
+
 static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8_t *I1,
                          size_t pitch1, int W, int H, float *u, float *v, size_t fpitch,
                          tvl1_stats *stats, hipStream_t st) {
   const tvl1_params &prm = c->prm;
+  if (prm.profile == 1)
+    return solve_dualtvl1(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch, stats, st);
   const Geometry &g = c->geo;
   const int L = g.L;
   const bool gam = g.gamma;
@@ -924,6 +1075,9 @@ void tvl1_params_default(tvl1_params *p) {
   p->use_initial_flow = 0;
   p->median_filtering = 1;
   p->fast_math = 0;
+  p->profile = 0;
+  p->inner_iterations = 30;   // cv::DualTVL1OpticalFlow defaults (profile 1)
+  p->outer_iterations = 10;
 }
 
 int32_t tvl1_abi_version(void) { return TVL1_ABI_VERSION; }

@@ -191,6 +191,125 @@ __global__ void k_gradient(const float *__restrict__ I, int W, int H, int P,
   G[(size_t)y * P + x] = make_float4(c, gx, gy, 0.0f);
 }
 
+// ---------------------------------------------------------------- profile 1
+// OpenCV's CPU cv::DualTVL1OpticalFlow schedule (tvl1_params.profile = 1; restated in
+// oracle/tvl1_oracle_dualtvl1.c, whose file:line-free notes list what is recalled).
+//
+// cv::resize INTER_LINEAR on CV_32F: half-pixel source coordinate (double, cast to
+// float), x clamped to the edge columns (f := 0, the last column a single tap), the two
+// rows clamped but their weights kept; or the exact-2x INTER_AREA fast path.  Planes by
+// blockIdx.z (< nmul of them are then multiplied by mul: cv::multiply(u, 1/scaleStep)).
+__global__ void k_resize_hp(const float *__restrict__ s0, const float *__restrict__ s1,
+                            const float *__restrict__ s2, int sw, int sh, int sp,
+                            float *__restrict__ d0, float *__restrict__ d1,
+                            float *__restrict__ d2, int dw, int dh, int dp, double scale_x,
+                            double scale_y, int area_fast, int nmul, float mul) {
+  const int dx = blockIdx.x * 64 + threadIdx.x;
+  const int dy = blockIdx.y * 4 + threadIdx.y;
+  if (dx >= dw || dy >= dh) return;
+  const int c = blockIdx.z;
+  const float *src = c == 0 ? s0 : (c == 1 ? s1 : s2);
+  float *dst = c == 0 ? d0 : (c == 1 ? d1 : d2);
+  float r;
+  if (sw == dw && sh == dh) {
+    r = src[(size_t)dy * sp + dx];
+  } else if (area_fast) {
+    const float *S = src + (size_t)(2 * dy) * sp + 2 * dx;
+    r = (S[0] + S[1] + S[sp] + S[sp + 1]) * 0.25f;
+  } else {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    const float b0 = 1.f - fy, b1 = fy;
+    const int r0 = imin(imax(sy, 0), sh - 1), r1 = imin(imax(sy + 1, 0), sh - 1);
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) fx = 0.f, sx = 0;
+    const bool single = sx + 1 >= sw;
+    if (sx >= sw - 1) fx = 0.f, sx = sw - 1;
+    const float a0 = 1.f - fx, a1 = fx;
+    const float *S0 = src + (size_t)r0 * sp, *S1 = src + (size_t)r1 * sp;
+    const float t0 = single ? S0[sx] * 1.0f : S0[sx] * a0 + S0[sx + 1] * a1;
+    const float t1 = single ? S1[sx] * 1.0f : S1[sx] * a0 + S1[sx + 1] * a1;
+    r = t0 * b0 + t1 * b1;
+  }
+  dst[(size_t)dy * dp + dx] = c < nmul ? r * mul : r;
+}
+
+// remap(I1 / I1x / I1y, x + u1, y + u2, INTER_CUBIC, BORDER_CONSTANT 0) + calcGradRho:
+// the map rounded to 1/32 px (cvRound), the Keys a = -0.75 weights of interpolateCubic at
+// the two 1/32 fractions (the float table entries, recomputed with the same operations),
+// 4x4 taps from G = (I1, I1x, I1y); a tap outside the image adds nothing.
+__device__ __forceinline__ void cubic_tab_entry(int i, float (&t)[4]) {
+  const float A = -0.75f;
+  const float x = (float)i * (1.f / 32);
+  t[0] = ((A * (x + 1) - 5 * A) * (x + 1) + 8 * A) * (x + 1) - 4 * A;
+  t[1] = ((A + 2) * x - (A + 3)) * x * x + 1;
+  t[2] = ((A + 2) * (1 - x) - (A + 3)) * (1 - x) * (1 - x) + 1;
+  t[3] = 1.f - t[0] - t[1] - t[2];
+}
+__device__ __forceinline__ int round_map(float v) {
+  if (!(v > -2147483648.f && v < 2147483648.f)) return (int)0x80000000u;
+  return (int)rintf(v);
+}
+__global__ void k_remap_cubic(const float *__restrict__ I0, const float4 *__restrict__ G,
+                              const float *__restrict__ u1, const float *__restrict__ u2,
+                              int W, int H, int P, float *__restrict__ I1wx,
+                              float *__restrict__ I1wy, float *__restrict__ rho) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const size_t i = (size_t)y * P + x;
+  const float u1v = u1[i], u2v = u2[i];
+  const float X = (float)x + u1v, Y = (float)y + u2v;
+  const int ix = round_map(X * 32.f), iy = round_map(Y * 32.f);
+  const int sx = imin(imax(ix >> 5, -32768), 32767) - 1;
+  const int sy = imin(imax(iy >> 5, -32768), 32767) - 1;
+  float ty[4], tx[4];
+  cubic_tab_entry(iy & 31, ty);
+  cubic_tab_entry(ix & 31, tx);
+  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f;
+  if ((unsigned)sx < (unsigned)imax(W - 3, 0) && (unsigned)sy < (unsigned)imax(H - 3, 0)) {
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      const float4 *r = G + (size_t)(sy + k1) * P + sx;
+      const float w0 = ty[k1] * tx[0], w1 = ty[k1] * tx[1], w2 = ty[k1] * tx[2],
+                  w3 = ty[k1] * tx[3];
+      const float4 g0 = r[0], g1 = r[1], g2 = r[2], g3 = r[3];
+      const float a = g0.x * w0 + g1.x * w1 + g2.x * w2 + g3.x * w3;
+      const float b = g0.y * w0 + g1.y * w1 + g2.y * w2 + g3.y * w3;
+      const float c = g0.z * w0 + g1.z * w1 + g2.z * w2 + g3.z * w3;
+      if (k1 == 0) {
+        sum = a; sumx = b; sumy = c;
+      } else {
+        sum += a; sumx += b; sumy += c;
+      }
+    }
+  } else if (!(sx >= W || sx + 4 <= 0 || sy >= H || sy + 4 <= 0)) {
+    sum = sumx = sumy = 0.0f * 1.0f;
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      const int yi = sy + k1;
+      if (yi < 0 || yi >= H) continue;
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) {
+        const int xj = sx + k2;
+        if (xj < 0 || xj >= W) continue;
+        const float w = ty[k1] * tx[k2];
+        const float4 g = G[(size_t)yi * P + xj];
+        sum += (g.x - 0.0f) * w;
+        sumx += (g.y - 0.0f) * w;
+        sumy += (g.z - 0.0f) * w;
+      }
+    }
+  }
+  // calcGradRho (grad = I1wx^2 + I1wy^2 is recomputed by the iteration kernels)
+  I1wx[i] = sumx;
+  I1wy[i] = sumy;
+  rho[i] = sum - sumx * u1v - sumy * u2v - I0[i];
+}
+
 // ---------------------------------------------------------------- K5 warp
 __device__ __forceinline__ float cubic(float x) {
   x = fabsf(x);
@@ -949,7 +1068,8 @@ __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float
 __device__ __forceinline__ float fm_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
 // estimateU's TH step at one px: v = u^{n-1} + d from the warp constants (pointwise).
-template <bool G, bool FM = false>
+// CPUP: profile 1 (OpenCV's CPU estimateV): rho = rho_c + (I1wx*u1 + I1wy*u2) [+ gamma*u3]
+template <bool G, bool FM = false, bool CPUP = false>
 __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, float u1o, float u2o,
                                       float u3o, const IterArgs &a, float &v1, float &v2,
                                       float &v3) {
@@ -959,9 +1079,11 @@ __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, floa
   // gamma*u3 inside the parentheses (with gamma = 0 either association gives
   // the same bits, signed zeros included)
   const float rho =
-      FM ? rhoc + (G ? fm_fma(a.gamma, u3o, fm_fma(I1wyv, u2o, I1wxv * u1o))
-                     : fm_fma(I1wyv, u2o, I1wxv * u1o))
-         : rhoc + (I1wxv * u1o + I1wyv * u2o + a.gamma * (G ? u3o : 0.0f));
+      CPUP ? (G ? rhoc + (I1wxv * u1o + I1wyv * u2o) + a.gamma * u3o
+                : rhoc + (I1wxv * u1o + I1wyv * u2o))
+      : FM ? rhoc + (G ? fm_fma(a.gamma, u3o, fm_fma(I1wyv, u2o, I1wxv * u1o))
+                       : fm_fma(I1wyv, u2o, I1wxv * u1o))
+           : rhoc + (I1wxv * u1o + I1wyv * u2o + a.gamma * (G ? u3o : 0.0f));
   // TH operator, branch-free: the three candidate steps are computed with the
   // reference's exact expressions and the applicable one selected.
   const bool lo = rho < -a.l_t * gradv;
@@ -1004,7 +1126,7 @@ __device__ __forceinline__ void u_from_v(float v1, float v2, float v3, float p11
 // estimateU at one px (x, y): the TH step from the warp constants and u^{n-1}, then
 // u^n = v + theta * div(p^{n-1}).  Shared by every iteration kernel, so they all run
 // exactly this sequence of IEEE float operations.
-template <bool G, bool FM = false>
+template <bool G, bool FM = false, bool CPUP = false>
 __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rhoc, float u1o,
                                               float u2o, float u3o, float p11, float p11l,
                                               float p12, float p12u, float p21, float p21l,
@@ -1013,13 +1135,13 @@ __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rh
                                               const IterArgs &a, float &n1, float &n2,
                                               float &n3) {
   float v1, v2, v3;
-  th_px<G, FM>(I1wxv, I1wyv, rhoc, u1o, u2o, u3o, a, v1, v2, v3);
+  th_px<G, FM, CPUP>(I1wxv, I1wyv, rhoc, u1o, u2o, u3o, a, v1, v2, v3);
   u_from_v<G, FM>(v1, v2, v3, p11, p11l, p12, p12u, p21, p21l, p22, p22u, p31, p31l, p32, p32u, x,
               y, a, n1, n2, n3);
 }
 
 // estimateU for the PX px of this lane on row y.  up* = p12/p22/p32 of row y-1.
-template <bool G, int PX = 4, bool FM = false>
+template <bool G, int PX = 4, bool FM = false, bool CPUP = false>
 __device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up12)[PX],
                                            const float (&up22)[PX], const float (&up32)[PX],
                                            int X0, int y, const IterArgs &a, float (&n1)[PX],
@@ -1039,7 +1161,7 @@ __device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up
     const float u3o = G ? r.u3[k] : 0.0f;
     const float p31 = G ? r.p31[k] : 0.0f, p31l = G ? l31[k] : 0.0f;
     const float p32 = G ? r.p32[k] : 0.0f;
-    estimate_u_px<G, FM>(r.wx[k], r.wy[k], r.rh[k], r.u1[k], r.u2[k], u3o, r.p11[k], l11[k],
+    estimate_u_px<G, FM, CPUP>(r.wx[k], r.wy[k], r.rh[k], r.u1[k], r.u2[k], u3o, r.p11[k], l11[k],
                      r.p12[k], up12[k], r.p21[k], l21[k], r.p22[k], up22[k], p31, p31l, p32,
                      up32[k], X0 + k, y, a, n1[k], n2[k], n3[k]);
   }
@@ -1106,7 +1228,8 @@ __device__ __forceinline__ float div_by(float a, const Recip &R) {
 // p' = (p + taut * du) / ng, du from u at (x+1) and (y+1) (clamped at the image edge).
 // EXACT: plain IEEE divisions, for taut < 0 or non-finite (k_iterate<G, true>; the host
 // routes such parameters there), where ng >= 1 does not hold.
-template <bool EXACT = false, bool BR = false, bool FM = false>
+// CPUP: profile 1, |grad u| as glibc hypotf: (float) sqrt((double) a*a + (double) b*b)
+template <bool EXACT = false, bool BR = false, bool FM = false, bool CPUP = false>
 __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_right,
                                         bool has_down, float taut, float pa, float pb, float &oa,
                                         float &ob) {
@@ -1121,7 +1244,8 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
     ob = fm_fma(taut, uy, pb) * r;
     return;
   }
-  const float g = hypot_f<BR>(ux, uy);
+  const float g = CPUP ? (float)__builtin_sqrt((double)ux * ux + (double)uy * uy)
+                       : hypot_f<BR>(ux, uy);
   const float ng = 1.0f + taut * g;
   if (EXACT) {
     oa = (pa + taut * ux) / ng;
@@ -1134,7 +1258,7 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
 }
 
 // One projection component for the PX px of this lane.
-template <int PX, bool EXACT = false, bool FM = false>
+template <int PX, bool EXACT = false, bool FM = false, bool CPUP = false>
 __device__ __forceinline__ void dual_component(const float (&uc)[PX], const float (&un)[PX],
                                                bool has_down, int X0, int W, float taut,
                                                const float (&pa)[PX], const float (&pb)[PX],
@@ -1145,11 +1269,11 @@ __device__ __forceinline__ void dual_component(const float (&uc)[PX], const floa
   for (int k = 0; k < PX - 1; ++k) ur[k] = uc[k + 1];
 #pragma unroll
   for (int k = 0; k < PX; ++k)
-    dual_px<EXACT, true, FM>(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k],
+    dual_px<EXACT, true, FM, CPUP>(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k],
                          oa[k], ob[k]);
 }
 
-template <bool G, bool EXACT = false>
+template <bool G, bool EXACT = false, bool CPUP = false>
 __global__ __launch_bounds__(kBlock) void k_iterate(IterArgs a) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
@@ -1176,7 +1300,7 @@ __global__ __launch_bounds__(kBlock) void k_iterate(IterArgs a) {
     Row<G> cur;
     load_row<G>(cur, a, (size_t)y0 * a.P + xa);
     float c1[4], c2[4], c3[4];
-    estimate_u<G>(cur, up12, up22, up32, X0, y0, a, c1, c2, c3);
+    estimate_u<G, 4, false, CPUP>(cur, up12, up22, up32, X0, y0, a, c1, c2, c3);
 
     for (int y = y0; y < y1; ++y) {
       const bool has_down = y + 1 < a.H;
@@ -1184,16 +1308,16 @@ __global__ __launch_bounds__(kBlock) void k_iterate(IterArgs a) {
       float n1[4], n2[4], n3[4];
       if (has_down) {
         load_row<G>(nxt, a, (size_t)(y + 1) * a.P + xa);
-        estimate_u<G>(nxt, cur.p12, cur.p22, cur.p32, X0, y + 1, a, n1, n2, n3);
+        estimate_u<G, 4, false, CPUP>(nxt, cur.p12, cur.p22, cur.p32, X0, y + 1, a, n1, n2, n3);
       } else {  // last image row: forward difference in y is 0 (clamp)
 #pragma unroll
         for (int k = 0; k < 4; ++k) { n1[k] = c1[k]; n2[k] = c2[k]; n3[k] = c3[k]; }
       }
       float q11[4], q12[4], q21[4], q22[4], q31[4], q32[4];
-      dual_component<4, EXACT>(c1, n1, has_down, X0, a.W, a.taut, cur.p11, cur.p12, q11, q12);
-      dual_component<4, EXACT>(c2, n2, has_down, X0, a.W, a.taut, cur.p21, cur.p22, q21, q22);
+      dual_component<4, EXACT, false, CPUP>(c1, n1, has_down, X0, a.W, a.taut, cur.p11, cur.p12, q11, q12);
+      dual_component<4, EXACT, false, CPUP>(c2, n2, has_down, X0, a.W, a.taut, cur.p21, cur.p22, q21, q22);
       if (G)
-        dual_component<4, EXACT>(c3, n3, has_down, X0, a.W, a.taut, cur.p31, cur.p32, q31, q32);
+        dual_component<4, EXACT, false, CPUP>(c3, n3, has_down, X0, a.W, a.taut, cur.p31, cur.p32, q31, q32);
       if (writer) {
         const size_t off = (size_t)y * a.P + xa;
         st4(a.u1d, off, c1);

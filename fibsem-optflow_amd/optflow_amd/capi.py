@@ -19,7 +19,7 @@ ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
 ORACLE_SO = REPO_ROOT / "oracle" / "liboracle_tvl1.so"
 
 TVL1_MAX_LEVELS = 32
-ABI_VERSION = 2          # TVL1_ABI_VERSION of include/tvl1.h
+ABI_VERSION = 3          # TVL1_ABI_VERSION of include/tvl1.h
 STATUS = {0: "TVL1_OK", 1: "TVL1_EINVAL", 2: "TVL1_ESIZE", 3: "TVL1_EHIP",
           4: "TVL1_ENOMEM", 5: "TVL1_ENODEV"}
 
@@ -38,6 +38,9 @@ class TVL1Params(C.Structure):
         ("use_initial_flow", C.c_int32),
         ("median_filtering", C.c_int32),
         ("fast_math", C.c_int32),
+        ("profile", C.c_int32),
+        ("inner_iterations", C.c_int32),
+        ("outer_iterations", C.c_int32),
     ]
 
 
@@ -63,13 +66,16 @@ class TVL1Stats(C.Structure):
 # generate_TV_args defaults, /root/reference/src/optflow.cpp:503-512
 DEFAULTS = dict(tau=0.25, lambda_=0.05, theta=0.3, nscales=10, warps=5, epsilon=0.01,
                 iterations=300, scale_step=0.8, gamma=0.0, use_initial_flow=0,
-                median_filtering=1, fast_math=0)
+                median_filtering=1, fast_math=0, profile=0, inner_iterations=30,
+                outer_iterations=10)
 
 # JSON key -> struct field (JSON keys are the reference's, optflow.cpp:503-512)
 JSON_KEYS = {"tau": "tau", "lambda": "lambda_", "theta": "theta", "nscales": "nscales",
              "warps": "warps", "epsilon": "epsilon", "iterations": "iterations",
              "scaleStep": "scale_step", "gamma": "gamma", "useInitialFlow": "use_initial_flow",
-             "medianFiltering": "median_filtering", "fastMath": "fast_math"}
+             "medianFiltering": "median_filtering", "fastMath": "fast_math",
+             "profile": "profile", "innerIterations": "inner_iterations",
+             "outerIterations": "outer_iterations"}
 
 
 def make_params(**kw) -> TVL1Params:

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TVL1_ABI_VERSION 2
+#define TVL1_ABI_VERSION 3
 #define TVL1_MAX_LEVELS 32
 
 typedef enum tvl1_status {
@@ -78,6 +78,14 @@ typedef struct tvl1_params {
                           approximate division and sqrt, fused multiply-add.  Held to the north-star
                           tolerance (mean EPE <= 1e-3 px vs oracle/), not to bit identity.  gamma != 0
                           solves stay IEEE. */
+  int32_t profile;     /* build-only: 0 = cv::cuda::OpticalFlowDual_TVL1,
+                          the reference's path (default); 1 = the schedule of OpenCV's CPU
+                          cv::DualTVL1OpticalFlow: half-pixel pyramid/upsample, remap INTER_CUBIC
+                          (a = -0.75, 1/32 px map, BORDER_CONSTANT), outer iterations each starting
+                          with medianFiltering, inner iterations each checking the residual.
+                          `iterations` is unused there; fast_math is ignored. */
+  int32_t inner_iterations; /* profile 1: innerIterations (cv::DualTVL1OpticalFlow default 30) */
+  int32_t outer_iterations; /* profile 1: outerIterations (default 10) */
 } tvl1_params;
 
 /* Per-call statistics.  Valid after tvl1_calc returns (host-side counters). */

@@ -336,7 +336,7 @@ void orc_postprocess(float *u, float *v, size_t flow_pitch, const uint8_t *I1, s
 }
 
 /* SURVEY 8(d) byte model, per level with executed iteration counts. */
-static double survey_bytes(int L, const int *ws, const int *hs, int warps,
+double orc_survey_bytes(int L, const int *ws, const int *hs, int warps,
                            const int64_t *iters) {
   double B = 0.0;
   for (int l = 0; l < L; ++l) {
@@ -359,6 +359,9 @@ int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
                   const uint8_t *I1, size_t pitch1, int w, int h, float *u, float *v,
                   size_t flow_pitch, tvl1_stats *stats) {
   if (!prm || !I0 || !I1 || !u || !v) return TVL1_EINVAL;
+  if (prm->profile == 1)
+    return orc_tvl1_calc_dualtvl1(prm, I0, pitch0, I1, pitch1, w, h, u, v, flow_pitch, stats);
+  if (prm->profile != 0) return TVL1_EINVAL;
   if (prm->nscales <= 0 || prm->warps < 0 || prm->iterations < 0) return TVL1_EINVAL;
   if (w <= 0 || h <= 0) return TVL1_ESIZE;
   if (pitch0 < (size_t)w || pitch1 < (size_t)w || flow_pitch < sizeof(float) * (size_t)w)
@@ -494,7 +497,7 @@ int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
     }
     stats->iterations_total = tot;
     stats->checks_total = checks;
-    stats->algorithmic_bytes = survey_bytes(L, ws, hs, prm->warps, level_iters);
+    stats->algorithmic_bytes = orc_survey_bytes(L, ws, hs, prm->warps, level_iters);
   }
 
   for (int s = 0; s < L; ++s) {

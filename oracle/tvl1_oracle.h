@@ -59,6 +59,23 @@ void orc_estimate_dual(const float *u1, const float *u2, const float *u3, float 
 /* build-only median filter (cv::medianBlur semantics, BORDER_REPLICATE, k = 3 or 5) */
 void orc_median(const float *src, int w, int h, int k, float *dst);
 
+/* ---- profile 1: OpenCV's CPU cv::DualTVL1OpticalFlow schedule ---- */
+
+/* cv::resize INTER_LINEAR on CV_32F (half-pixel centres, separable float weights);
+ * scale = source px per destination px (double, as resize derives it); area_fast =
+ * the exact-2x INTER_AREA fast path resize switches to */
+void orc_resize_hp(const float *src, int sw, int sh, float *dst, int dw, int dh,
+                   double scale_x, double scale_y, int area_fast);
+
+/* remap(I1 / I1x / I1y, x + u1, y + u2, INTER_CUBIC, BORDER_CONSTANT 0) + calcGradRho */
+void orc_remap_cubic(const float *I0, const float *I1, const float *I1x, const float *I1y,
+                     const float *u1, const float *u2, int w, int h, float *I1wx,
+                     float *I1wy, float *grad, float *rho_c);
+
+int orc_tvl1_calc_dualtvl1(const tvl1_params *params, const uint8_t *I0, size_t pitch0,
+                           const uint8_t *I1, size_t pitch1, int w, int h, float *u, float *v,
+                           size_t flow_pitch, tvl1_stats *stats);
+
 /* ---- whole solve: same contract as tvl1_calc_host (include/tvl1.h) ---- */
 int orc_tvl1_calc(const tvl1_params *params, const uint8_t *I0, size_t pitch0,
                   const uint8_t *I1, size_t pitch1, int w, int h, float *u, float *v,

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol(built):
 
 def test_abi_version_and_defaults(built):
     lib = capi.load_engine()
-    assert lib.tvl1_abi_version() == 2
+    assert lib.tvl1_abi_version() == 3
     p = capi.TVL1Params()
     lib.tvl1_params_default(C.byref(p))
     # generate_TV_args defaults, /root/reference/src/optflow.cpp:503-512
@@ -52,14 +52,14 @@ def test_struct_layout_matches_header(built, tmp_path):
         '#include <stdio.h>\n#include <stddef.h>\n#include "tvl1.h"\n'
         "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu\\n\","
         "sizeof(tvl1_params), sizeof(tvl1_stats), offsetof(tvl1_params, epsilon),"
-        "offsetof(tvl1_params, fast_math), offsetof(tvl1_stats, warp_iterations),"
+        "offsetof(tvl1_params, outer_iterations), offsetof(tvl1_stats, warp_iterations),"
         "offsetof(tvl1_stats, kernel_ms), offsetof(tvl1_stats, kernel_hbm_bytes));return 0;}\n")
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-I", str(HEADER.parent), str(src), "-o", str(exe)], check=True)
     got = [int(t) for t in subprocess.run([str(exe)], capture_output=True, text=True,
                                           check=True).stdout.split()]
     P, S = capi.TVL1Params, capi.TVL1Stats
-    assert got == [C.sizeof(P), C.sizeof(S), P.epsilon.offset, P.fast_math.offset,
+    assert got == [C.sizeof(P), C.sizeof(S), P.epsilon.offset, P.outer_iterations.offset,
                    S.warp_iterations.offset, S.kernel_ms.offset, S.kernel_hbm_bytes.offset]
 
 
@@ -72,6 +72,9 @@ def test_create_rejects_bad_params_and_missing_gpu(built):
     bad = capi.make_params(fast_math=2)
     assert lib.tvl1_create(C.byref(ctx), 0, C.byref(bad)) == 1        # TVL1_EINVAL
     assert b"fastMath" in lib.tvl1_last_error(None)
+    bad = capi.make_params(profile=2)
+    assert lib.tvl1_create(C.byref(ctx), 0, C.byref(bad)) == 1        # TVL1_EINVAL
+    assert b"profile" in lib.tvl1_last_error(None)
     if lib.tvl1_device_count() == 0:
         good = capi.make_params()
         assert lib.tvl1_create(C.byref(ctx), 0, C.byref(good)) == 5   # TVL1_ENODEV

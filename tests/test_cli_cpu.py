@@ -71,7 +71,8 @@ def test_defaults_and_precedence(tmp_path, slices):
     # TV args: per-image -> global -> default (optflow.cpp:503-512)
     assert a["tv"] == {"tau": 0.3, "lambda": 0.05, "theta": 0.3, "nscales": 5, "warps": 5,
                        "epsilon": 0.01, "iterations": 300, "scaleStep": 0.8, "gamma": 0.0,
-                       "medianFiltering": 1, "fastMath": 0}
+                       "medianFiltering": 1, "fastMath": 0, "profile": 0,
+                       "innerIterations": 30, "outerIterations": 10}
     assert b["tv"]["tau"] == 0.2 and b["tv"]["warps"] == 7 and b["tv"]["nscales"] == 5
     assert b["output"] == f"{tmp_path}/b_1.00" and b["size0"] == [83, 61]
     # no ROI -> "default" full frame (optflow.cpp:147-154); per-image rois honoured

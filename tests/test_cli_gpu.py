@@ -130,3 +130,21 @@ def test_two_workers_match_one(tmp_path, built):
                  "images": imgs}, tmp_path, name=f"{tag}.json")
         outs.append({p.name: p.read_bytes() for p in sorted(d.glob("*.tiff"))})
     assert len(outs[0]) == 8 and outs[0] == outs[1]
+
+
+def test_dualtvl1_profile_via_json(tmp_path, pair):
+    """BASELINE configs[0]'s "DualTVL1 CPU" schedule through the CLI's JSON surface
+    (build-only keys profile / innerIterations / outerIterations)."""
+    I0, I1 = pair
+    cfg = {"output_dir": str(tmp_path), "scale": 1, "output_type": "flow", "profile": 1,
+           "nscales": 4, "warps": 3, "lambda": 0.15, "medianFiltering": 5,
+           "innerIterations": 10, "outerIterations": 3,
+           "images": [{"p": str(tmp_path / "p.png"), "q": str(tmp_path / "q.png"),
+                       "output_name": "pq", "rois": {"custom": [0, 0, 150, 110]}}]}
+    run_cli(cfg, tmp_path)
+    params = capi.make_params(profile=1, nscales=4, warps=3, lambda_=0.15, median_filtering=5,
+                              inner_iterations=10, outer_iterations=3)
+    u, v = oracle_post(I0, I1, params, 0)
+    out = sorted(tmp_path.glob("pq*_x.tiff"))
+    assert out, list(tmp_path.iterdir())
+    assert np.array_equal(tif(out[0]).view(np.uint32), u.view(np.uint32))

@@ -200,3 +200,40 @@ def test_benchmark_pair_bit_exact(engine):
     np.testing.assert_array_equal(wi, wr)
     assert bits_equal(u, ur) and bits_equal(v, vr)
     print(f"C2 pair: {int(wi.sum())} iterations, bit-exact vs oracle")
+
+
+# Profile 1: OpenCV's CPU DualTVL1OpticalFlow schedule, bit-identical to
+# its restatement (oracle/tvl1_oracle_dualtvl1.c; parity with OpenCV itself unpinned).
+P1_CASES = [
+    (64, 48, 41, dict(nscales=4, warps=3)),
+    (17, 16, 42, dict(nscales=3, warps=2)),
+    (250, 131, 43, dict(nscales=5, warps=5, lambda_=0.15, median_filtering=5)),  # CPU defaults
+    (96, 64, 44, dict(nscales=4, warps=3, gamma=0.2, median_filtering=5)),
+    (96, 64, 45, dict(nscales=4, warps=3, median_filtering=3)),
+    (120, 90, 46, dict(nscales=3, warps=2, epsilon=0.0, inner_iterations=3, outer_iterations=2)),
+    (128, 96, 47, dict(nscales=4, warps=2, scale_step=0.5)),                     # 2x area path
+    (70, 50, 48, dict(nscales=3, warps=2, tau=-0.05, inner_iterations=4, outer_iterations=2)),
+]
+
+
+@pytest.mark.parametrize("W,H,seed,kw", P1_CASES)
+def test_dualtvl1_profile_matches_oracle(engine, W, H, seed, kw):
+    I0, I1 = synth.gen_pair(W, H, seed=seed)
+    p = capi.make_params(profile=1, **kw)
+    engine.set_params(p)
+    u, v, st, wi = engine.calc_host(I0, I1)
+    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    assert st["levels"] == sr["levels"]
+    np.testing.assert_array_equal(wi, wr)
+    fin = np.isfinite(ur) & np.isfinite(vr)
+    assert np.array_equal(fin, np.isfinite(u) & np.isfinite(v))
+    assert bits_equal(u[fin], ur[fin]) and bits_equal(v[fin], vr[fin]), \
+        f"max|du|={np.abs(u - ur)[fin].max()} max|dv|={np.abs(v - vr)[fin].max()}"
+
+
+def test_dualtvl1_profile_identity(engine):
+    I0, _ = synth.gen_pair(80, 60, seed=3)
+    engine.set_params(capi.make_params(profile=1, nscales=4, warps=3))
+    u, v, st, wi = engine.calc_host(I0, I0)
+    assert np.all(u == 0) and np.all(v == 0)
+    assert np.all(wi == 1)
