@@ -50,6 +50,7 @@ def _traffic():
 
 
 TRAFFIC = _traffic()
+RED_CPU = False   # reductions on CPU tensors (gloo rehearsal, BENCH_DIST_BACKEND=gloo)
 METRIC = "slice-pairs/sec (6k×4k, 5 scales, 30 warps) at 1/2/4/8 GPUs; % HBM roofline"
 
 
@@ -207,7 +208,7 @@ def run_stack(args, rank, world, local_rank, dist):
     if errors:
         raise RuntimeError("; ".join(errors))
     mine = torch.tensor([float(sum(done)), float(sum(iters)), elapsed], dtype=torch.float64,
-                        device=dev)
+                        device="cpu" if RED_CPU else dev)
     if dist:
         tot = mine[:2].clone()
         dist.all_reduce(tot)
@@ -261,12 +262,23 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dist = None
+    # nccl (= RCCL) by default; BENCH_DIST_BACKEND=gloo rehearses the N > 1 path on fewer
+    # GPUs than ranks (ranks share devices round-robin; the collectives here are only the
+    # barrier and the max / sum of a few scalars, never on the data path)
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(local_rank)
+    global RED_CPU
+    RED_CPU = backend == "gloo"
     if args.workload == "stack":
         return run_stack(args, rank, world, local_rank, dist)
 
@@ -330,7 +342,7 @@ def main():
         torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t0
         if dist:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if RED_CPU else dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         return elapsed, stats
