@@ -86,7 +86,9 @@ def parse():
                          "thread each); a step = one batch of this many pairs")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip per-kernel HIP events (roofline fields become null)")
-    ap.add_argument("--workload", choices=("pair", "stack"), default="pair",
+    ap.add_argument("--batch", type=int, default=64,
+                    help="strips: pairs per tvl1_calc_batch call")
+    ap.add_argument("--workload", choices=("pair", "stack", "strips"), default="pair",
                     help="pair: BASELINE configs[1] (C2, the headline); stack: adjacent / "
                          "strided pairs of a synthetic stack (C3: --slices 256; C4: --slices "
                          "4096 on 8 GPUs; C5: --strides 1,4,16), slices made on the device")
@@ -251,6 +253,99 @@ def run_stack(args, rank, world, local_rank, dist):
     print(json.dumps(out), flush=True)
 
 
+def run_strips(args, rank, world, local_rank, dist):
+    """The production workload: per slice pair, two ROI strips of the
+    half-scale slice (gen_cross_file_list.py top/bottom 100 rows at scale 0.5 -> 3072x100),
+    nscales 10 (-> 9 levels), warps 5, the reference's other defaults.  A step = --inflight
+    batches of --batch strip pairs, each batch one tvl1_calc_batch call on its own ctx +
+    stream + host thread.  value = strip solves/s; slice pairs/s = value / 2."""
+    import numpy as np
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from optflow_amd import capi, synth
+
+    W, H, B, F = args.width, args.height, args.batch, max(1, args.inflight)
+    params = capi.make_params(nscales=args.nscales, warps=args.warps,
+                              iterations=args.iterations, epsilon=args.epsilon)
+    dev = torch.device("cuda", local_rank)
+    slots = []
+    for j in range(F):
+        I0s, I1s = [], []
+        for b in range(B):
+            a, c = synth.gen_pair(W, H, seed=0x5EED + 977 * (rank * F + j) + b, z=1 + b % 7)
+            I0s.append(a)
+            I1s.append(c)
+        eng = capi.Engine(params, device=local_rank)
+        slots.append(dict(eng=eng, I0=torch.from_numpy(np.stack(I0s)).to(dev),
+                          I1=torch.from_numpy(np.stack(I1s)).to(dev),
+                          u=torch.empty((B, H, W), dtype=torch.float32, device=dev),
+                          v=torch.empty((B, H, W), dtype=torch.float32, device=dev)))
+    torch.cuda.synchronize(dev)
+
+    def solve(sl):
+        st = sl["eng"].calc_batch_device(B, sl["I0"].data_ptr(), W, W * H, sl["I1"].data_ptr(),
+                                         W, W * H, W, H, sl["u"].data_ptr(), sl["v"].data_ptr(),
+                                         4 * W, 4 * W * H, stream=sl["eng"].stream)
+        torch.cuda.synchronize(dev)
+        return st
+
+    pool = ThreadPoolExecutor(max_workers=F)
+
+    def step():
+        return list(pool.map(solve, slots))
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(args.steps):
+        for st in step():
+            iters += sum(s["iterations_total"] for s in st)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if RED_CPU else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.destroy_process_group()
+    if rank != 0:
+        return
+    solves = world * args.steps * F * B
+    value = solves / elapsed
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        a, c = synth.gen_pair(W, H, seed=0x5EED, z=1)
+        lib = capi.load_oracle()
+        t1 = time.perf_counter()
+        n_rep = 4
+        for _ in range(n_rep):
+            capi.oracle_calc(a, c, params, warp_iters=False)
+        dt = (time.perf_counter() - t1) / n_rep
+        cpu = {"value": round(1.0 / dt, 3), "unit": "strip solves/s",
+               "cores": int(lib.orc_num_threads()), "kind": "port",
+               "sample": f"oracle/ CPU restatement, {n_rep} solves of one {W}x{H} strip pair"}
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "strip solves/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "math": "IEEE (bit-identical to oracle/)", "data": "synthetic",
+        "config": {"workload": (f"production ROI strips (SURVEY 3.2): {W}x{H} pairs, nscales "
+                                f"{args.nscales}, warps {args.warps}, epsilon {args.epsilon}; "
+                                f"2 strips per slice pair"),
+                   "slice_pairs_per_s": round(value / 2, 2),
+                   "batch": B, "batches_in_flight_per_gpu": F,
+                   "iterations_per_strip": round(iters / (args.steps * F * B), 1)},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
     import numpy as np
@@ -281,6 +376,8 @@ def main():
     RED_CPU = backend == "gloo"
     if args.workload == "stack":
         return run_stack(args, rank, world, local_rank, dist)
+    if args.workload == "strips":
+        return run_strips(args, rank, world, local_rank, dist)
 
     from optflow_amd import capi, synth
 

@@ -1,0 +1,231 @@
+// tvl1_batch.hpp — batched kernels of the MI355X TV-L1 engine: one launch works on up to
+// kBatchMax same-size pairs (tvl1_calc_batch).
+//
+// The production workload is not one 6144x4096 pair but two 3072x100 ROI strips per slice
+// pair (gen_cross_file_list.py top/bottom ROIs at scale 0.5, nscales 10 -> 9
+// levels, warps 5).  One such solve is ~400 launches of a few microseconds each on levels
+// of 8.8 K - 307 K px: kernel dispatch, not the GPU, sets its pace.  These kernels give
+// every launch a pair dimension (blockIdx.z or .y -> pair b) so a batch of strips shares
+// each dispatch.  Per pair, plane X of level s lives at X + b * (pair stride of the plane)
+// in a batch arena; which of the two u / p buffer sets is current, whether the pass ends
+// in a residual check and whether p is still 0 are per-pair bits in the kernel arguments
+// (BatchSel), because pairs leave a warp's iteration loop at different iterations.
+//
+// The arithmetic is the single-pair kernels' (warp_gather_fn, tb_iterate_store,
+// resize_px), so every pair's flow is bit-identical to oracle/.
+#pragma once
+
+namespace tvl1k {
+
+constexpr int kBatchMax = 64;
+
+struct BatchSel {            // the pairs a launch works on, passed by value
+  int n;                     // number of entries in idx
+  uint8_t idx[kBatchMax];    // pair indices
+  uint64_t ubit, pbit;       // per pair: current u set / p set (0 or 1)
+  uint64_t cerr, pzero;      // per pair: the pass ends in a residual check / p == 0
+};
+
+__device__ __forceinline__ int bsel_bit(uint64_t m, int b) { return (int)((m >> b) & 1u); }
+
+// K1 convertTo for both frames of every pair: blockIdx.z = 2 * pair + frame.
+__global__ void kb_convert(const uint8_t *__restrict__ I0, size_t p0, size_t s0,
+                           const uint8_t *__restrict__ I1, size_t p1, size_t s1,
+                           float *__restrict__ d0, float *__restrict__ d1, int W, int H, int P,
+                           size_t ps) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const int b = blockIdx.z >> 1;
+  if ((blockIdx.z & 1) == 0)
+    d0[b * ps + (size_t)y * P + x] = (float)I0[b * s0 + (size_t)y * p0 + x];
+  else
+    d1[b * ps + (size_t)y * P + x] = (float)I1[b * s1 + (size_t)y * p1 + x];
+}
+
+// K2 pyramid step for both frames of every pair (blockIdx.z = 2 * pair + frame).
+__global__ void kb_resize_down2(const float *__restrict__ a0, const float *__restrict__ a1,
+                                int sw, int sh, int sp, size_t sps, float *__restrict__ b0,
+                                float *__restrict__ b1, int dw, int dh, int dp, size_t dps,
+                                float fx, float fy) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= dw || y >= dh) return;
+  const int b = blockIdx.z >> 1;
+  const float *src = ((blockIdx.z & 1) == 0 ? a0 : a1) + b * sps;
+  float *dst = ((blockIdx.z & 1) == 0 ? b0 : b1) + b * dps;
+  dst[(size_t)y * dp + x] = resize_px(src, sw, sh, sp, x, y, fx, fy);
+}
+
+// K3 centeredGradient of every pair's I1 into its G plane (blockIdx.z = pair).
+__global__ void kb_gradient(const float *__restrict__ I, size_t ips, int W, int H, int P,
+                            float4 *__restrict__ G, size_t gps) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const float *Ib = I + blockIdx.z * ips;
+  const float *row = Ib + (size_t)y * P;
+  const float c = row[x];
+  const float gx = 0.5f * (row[imin(x + 1, W - 1)] - row[imax(x - 1, 0)]);
+  const float gy = 0.5f * (Ib[(size_t)imin(y + 1, H - 1) * P + x] - Ib[(size_t)imax(y - 1, 0) * P + x]);
+  G[blockIdx.z * gps + (size_t)y * P + x] = make_float4(c, gx, gy, 0.0f);
+}
+
+// K5 warpBackward of the selected pairs (blockIdx.z = entry of sel): the fixed 4x4 Keys
+// gather of k_warp_lds's global path from G, weight-normalised; I1wx, I1wy, rho_c.
+struct BatchWarp {
+  const float *I0;           // level s of pair 0 (pair stride ips)
+  const float4 *G;           // pair stride gps
+  const float *U[2][2];      // u sets (pair stride ps)
+  float *C[3];               // I1wx, I1wy, rho (pair stride ps)
+  size_t ips, gps, ps;
+  int W, H, P;
+  BatchSel sel;
+};
+__global__ void kb_warp(BatchWarp w) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= w.W || y >= w.H) return;
+  const int b = w.sel.idx[blockIdx.z];
+  const int us = bsel_bit(w.sel.ubit, b);
+  const size_t i = (size_t)y * w.P + x, o = b * w.ps;
+  const float u1v = w.U[us][0][o + i], u2v = w.U[us][1][o + i];
+  const float4 *G = w.G + b * w.gps;
+  const float wx = (float)x + u1v;
+  const float wy = (float)y + u2v;
+  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
+  warp_gather<false>(G, w.P, 0, 0, w.W, w.H, wx, wy, tap_floor(wx), tap_floor(wy), sum, sumx,
+                     sumy, wsum);
+  const float coeff = 1.0f / wsum;
+  const float I1wv = sum * coeff;
+  const float I1wxv = sumx * coeff;
+  const float I1wyv = sumy * coeff;
+  w.C[0][o + i] = I1wxv;
+  w.C[1][o + i] = I1wyv;
+  w.C[2][o + i] = I1wv - I1wxv * u1v - I1wyv * u2v - w.I0[b * w.ips + i];
+}
+
+// K6+K8(+K7 partials): one temporally blocked pass of t.niter iterations on each selected
+// pair (blockIdx.y = entry of sel, blockIdx.x = region) -- k_iterate_tb's body on the
+// pair's planes.  Residual partials of pair b at partials + b * nblk.
+struct BatchTB {
+  TBArgs t;                  // geometry, l_t, theta, gamma, taut (plane pointers unused)
+  float *U[2][2];            // u sets (pair stride ps)
+  float *Pp[2][4];           // p sets
+  const float *C[3];         // warp constants
+  size_t ps;
+  double *partials;
+  int nblk;                  // regions per pair
+  BatchSel sel;
+};
+template <int RH, int NG, int PX>
+__global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void kb_iterate_tb(BatchTB bt) {
+  constexpr int LPR = 64 / PX;
+  constexpr int HALF = RH / NG;
+  __shared__ typename VecT<PX>::type lds[4 * RH * LPR];
+  const int b = bt.sel.idx[blockIdx.y];
+  TBArgs t = bt.t;
+  IterArgs &a = t.it;
+  {
+    const size_t o = b * bt.ps;
+    const int us = bsel_bit(bt.sel.ubit, b), qs = bsel_bit(bt.sel.pbit, b);
+    a.u1s = bt.U[us][0] + o;
+    a.u2s = bt.U[us][1] + o;
+    a.u1d = bt.U[us ^ 1][0] + o;
+    a.u2d = bt.U[us ^ 1][1] + o;
+    a.p11s = bt.Pp[qs][0] + o;
+    a.p12s = bt.Pp[qs][1] + o;
+    a.p21s = bt.Pp[qs][2] + o;
+    a.p22s = bt.Pp[qs][3] + o;
+    a.p11d = bt.Pp[qs ^ 1][0] + o;
+    a.p12d = bt.Pp[qs ^ 1][1] + o;
+    a.p21d = bt.Pp[qs ^ 1][2] + o;
+    a.p22d = bt.Pp[qs ^ 1][3] + o;
+    a.I1wx = bt.C[0] + o;
+    a.I1wy = bt.C[1] + o;
+    a.rho = bt.C[2] + o;
+    a.calc_err = bsel_bit(bt.sel.cerr, b);
+    a.p_zero = bsel_bit(bt.sel.pzero, b);
+    a.partials = bt.partials + (size_t)b * bt.nblk;
+  }
+  const int tid = threadIdx.x;
+  const int c4 = tid % LPR;
+  const int rr = tid / LPR;
+  int bx, by;
+  tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
+  const int K = t.niter;
+  const int xr0 = bx * 56 - 4;
+  const int yr0 = by * t.out_h - K;
+  const int X = xr0 + PX * c4;
+  const int xa = imin(imax(X, 0), a.P - PX);
+  Row<false, PX> r[NG];
+  int Y[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    Y[g] = yr0 + rr + g * HALF;
+    const int ya = imin(imax(Y[g], 0), a.H - 1);
+    load_row<false, PX>(r[g], a, (size_t)ya * a.P + xa);
+  }
+  tb_iterate_store<false, RH, NG, PX, false>(t, lds, r, Y, X, c4, rr);
+}
+
+// K7 for the selected pairs: fixed-order sum of pair b's partials into out[b].
+__global__ void kb_reduce(const double *__restrict__ partials, int n, BatchSel sel,
+                          double *__restrict__ out) {
+  __shared__ double s[kBlock];
+  const int b = sel.idx[blockIdx.x];
+  const double *p = partials + (size_t)b * n;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += kBlock) acc += p[i];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = kBlock / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[b] = s[0];
+}
+
+// K9 flow upsample (u1, u2 scaled by 1/scaleStep) of every pair from its current u set
+// into the other one (blockIdx.z = 2 * entry + component).
+struct BatchUp {
+  float *U[2][2];
+  size_t ps;
+  int sw, sh, sp, dw, dh, dp;
+  float fx, fy, mul;
+  BatchSel sel;
+};
+__global__ void kb_upsample(BatchUp w) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= w.dw || y >= w.dh) return;
+  const int b = w.sel.idx[blockIdx.z >> 1], c = blockIdx.z & 1;
+  const int us = bsel_bit(w.sel.ubit, b);
+  const float *src = w.U[us][c] + b * w.ps;
+  float *dst = w.U[us ^ 1][c] + b * w.ps;
+  dst[(size_t)y * w.dp + x] = resize_px(src, w.sw, w.sh, w.sp, x, y, w.fx, w.fy) * w.mul;
+}
+
+// K10: every pair's final u set to the caller's flow (pair b at u + b * fstride bytes).
+struct BatchOut {
+  const float *U[2][2];
+  size_t ps;
+  int W, H, P;
+  float *u, *v;
+  size_t fpitch, fstride;
+  BatchSel sel;
+};
+__global__ void kb_output(BatchOut w) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= w.W || y >= w.H) return;
+  const int b = w.sel.idx[blockIdx.z];
+  const int us = bsel_bit(w.sel.ubit, b);
+  const size_t i = b * w.ps + (size_t)y * w.P + x;
+  char *ou = reinterpret_cast<char *>(w.u) + b * w.fstride + (size_t)y * w.fpitch;
+  char *ov = reinterpret_cast<char *>(w.v) + b * w.fstride + (size_t)y * w.fpitch;
+  reinterpret_cast<float *>(ou)[x] = w.U[us][0][i];
+  reinterpret_cast<float *>(ov)[x] = w.U[us][1][i];
+}
+
+}  // namespace tvl1k

@@ -19,6 +19,7 @@
 
 #include "../../include/tvl1.h"
 #include "tvl1_kernels.hpp"
+#include "tvl1_batch.hpp"
 
 using namespace tvl1k;
 
@@ -94,6 +95,17 @@ struct tvl1_ctx {
   int witer_slots[8][2] = {};   // resident k_warp_iter<M, -, BW> blocks per device [M][BW == 64]
   int witer_bw = 128;           // TVL1_WITER_BW: k_warp_iter band width (128: 2 producers, 64: 1)
   int fuse_store = 0;        // TVL1_FUSE_STORE=1: k_warp_iter always stores the constants
+  // batch arena (tvl1_calc_batch): per logical plane, kBatchMax pairs' copies
+  char *barena = nullptr;
+  size_t barena_bytes = 0;
+  int bW = 0, bH = 0, bL = 0, bn = 0;   // geometry it is laid out for
+  float *bI0s[TVL1_MAX_LEVELS] = {}, *bI1s[TVL1_MAX_LEVELS] = {};
+  size_t bips[TVL1_MAX_LEVELS] = {};    // pair stride of level s image planes (floats)
+  float4 *bG = nullptr;
+  float *bU[2][2] = {}, *bP[2][4] = {}, *bC[3] = {};
+  size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
+  double *bpartials = nullptr;
+  int bnblk = 0;                        // partials per pair
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
   int warp_th = 16;          // k_warp_lds tile height (8, 16, 32)
@@ -1058,6 +1070,292 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   return TVL1_OK;
 }
 
+
+// ---------------------------------------------------------------- batched solve
+// tvl1_calc_batch: n pairs of one size through the batched kernels (tvl1_batch.hpp), in
+// chunks of kBatchMax.  The pairs of a chunk walk the levels and warps in lock step; inside
+// a warp each pair keeps its own iteration count, stopping-rule state and u / p buffer set,
+// and a pass runs the smallest number of iterations any active pair may fuse before its
+// next check (<= kTbMax), so every pair sees exactly the single-pair schedule.
+static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n) {
+  const Geometry &g = c->geo;   // pyramid sizes of (W, H) (ensure_geometry ran)
+  if (c->barena && c->bW == W && c->bH == H && c->bL == g.L && c->bn >= n) return TVL1_OK;
+  const size_t P0 = (size_t)g.ps[0];
+  const size_t ps = align_up(P0 * H, 64);
+  const int tb_blocks = ((W + 55) / 56) * ((H + 23) / 24) + 64;
+  size_t bytes = 0;
+  size_t ips[TVL1_MAX_LEVELS];
+  for (int s = 0; s < g.L; ++s) {
+    ips[s] = align_up((size_t)g.ps[s] * g.hs[s], 64);
+    bytes += 2 * ips[s] * n * sizeof(float) + 512;
+  }
+  bytes += (ps * n * sizeof(float) + 256) * (4 + 4 + 8 + 3);   // G (float4) + U + P + C
+  bytes += (size_t)tb_blocks * n * sizeof(double) + 4096;
+  if (c->barena) {
+    HIP_TRY(c, hipDeviceSynchronize());
+    (void)hipFree(c->barena);
+    c->barena = nullptr;
+  }
+  hipError_t e = hipMalloc((void **)&c->barena, bytes);
+  if (e != hipSuccess)
+    return set_err(c, TVL1_ENOMEM, "hipMalloc(%zu) for the batch arena failed: %s", bytes,
+                   hipGetErrorString(e));
+  HIP_TRY(c, hipMemsetAsync(c->barena, 0, bytes, c->own_stream));   // finite pitch padding
+  HIP_TRY(c, hipStreamSynchronize(c->own_stream));
+  char *p = c->barena;
+  auto take = [&](size_t nbytes) {
+    char *r = p;
+    p += align_up(nbytes, 256);
+    return r;
+  };
+  for (int s = 0; s < TVL1_MAX_LEVELS; ++s) c->bI0s[s] = c->bI1s[s] = nullptr;
+  for (int s = 0; s < g.L; ++s) {
+    c->bips[s] = ips[s];
+    c->bI0s[s] = (float *)take(ips[s] * n * sizeof(float));
+    c->bI1s[s] = (float *)take(ips[s] * n * sizeof(float));
+  }
+  c->bps = ps;
+  c->bG = (float4 *)take(4 * ps * n * sizeof(float));
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < 2; ++j) c->bU[k][j] = (float *)take(ps * n * sizeof(float));
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < 4; ++j) c->bP[k][j] = (float *)take(ps * n * sizeof(float));
+  for (int j = 0; j < 3; ++j) c->bC[j] = (float *)take(ps * n * sizeof(float));
+  c->bpartials = (double *)take((size_t)tb_blocks * n * sizeof(double));
+  c->bnblk = tb_blocks;
+  c->bW = W;
+  c->bH = H;
+  c->bL = g.L;
+  c->bn = n;
+  return TVL1_OK;
+}
+
+static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size_t pitch0,
+                                     size_t stride0, const uint8_t *I1, size_t pitch1,
+                                     size_t stride1, int W, int H, float *u, float *v,
+                                     size_t fpitch, size_t fstride, tvl1_stats *stats,
+                                     hipStream_t st) {
+  const tvl1_params &prm = c->prm;
+  const Geometry &g = c->geo;
+  const int L = g.L;
+  {
+    const tvl1_status r = ensure_batch(c, W, H, n);
+    if (r != TVL1_OK) return r;
+  }
+  const size_t ps = c->bps;
+  BatchSel all{};
+  all.n = n;
+  for (int b = 0; b < n; ++b) all.idx[b] = (uint8_t)b;
+
+  // [A.1] convertTo + [A.2] pyramid
+  hipLaunchKernelGGL(kb_convert, grid2(W, H, 2 * n), kBlk2, 0, st, I0, pitch0, stride0, I1,
+                     pitch1, stride1, c->bI0s[0], c->bI1s[0], W, H, g.ps[0], c->bips[0]);
+  const float fdown = (float)(1.0 / prm.scale_step);
+  for (int s = 1; s < L; ++s)
+    hipLaunchKernelGGL(kb_resize_down2, grid2(g.ws[s], g.hs[s], 2 * n), kBlk2, 0, st,
+                       c->bI0s[s - 1], c->bI1s[s - 1], g.ws[s - 1], g.hs[s - 1], g.ps[s - 1],
+                       c->bips[s - 1], c->bI0s[s], c->bI1s[s], g.ws[s], g.hs[s], g.ps[s],
+                       c->bips[s], fdown, fdown);
+  // u = 0 at the coarsest level, set 0 of every pair
+  for (int k = 0; k < 2; ++k)
+    HIP_TRY(c, hipMemsetAsync(c->bU[0][k], 0, ps * n * sizeof(float), st));
+  HIP_TRY(c, hipGetLastError());
+
+  const float l_t = (float)(prm.lambda * prm.theta);
+  const float taut = (float)(prm.tau / prm.theta);
+  const float upmul = (float)(1.0 / prm.scale_step);
+  uint64_t ubit = 0, pbit = 0;
+  std::vector<int64_t> level_iters((size_t)n * TVL1_MAX_LEVELS, 0), checks(n, 0);
+  std::vector<int> nit(n);
+  std::vector<double> err(n), prev(n);
+  std::vector<char> act(n);
+  for (int s = L - 1; s >= 0; --s) {
+    const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
+    const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
+    hipLaunchKernelGGL(kb_gradient, grid2(lw, lh, n), kBlk2, 0, st, c->bI1s[s], c->bips[s], lw,
+                       lh, P, c->bG, ps);
+    uint64_t pzero = n == 64 ? ~0ull : ((1ull << n) - 1);   // p = 0 at every level start
+    BatchTB bt{};
+    bt.t.it.W = lw;
+    bt.t.it.H = lh;
+    bt.t.it.P = P;
+    bt.t.it.l_t = l_t;
+    bt.t.it.theta = (float)prm.theta;
+    bt.t.it.gamma = 0.0f;
+    bt.t.it.taut = taut;
+    bt.t.tiles_x = (lw + 55) / 56;
+    for (int k = 0; k < 2; ++k)
+      for (int j = 0; j < 2; ++j) bt.U[k][j] = c->bU[k][j];
+    for (int k = 0; k < 2; ++k)
+      for (int j = 0; j < 4; ++j) bt.Pp[k][j] = c->bP[k][j];
+    for (int j = 0; j < 3; ++j) bt.C[j] = c->bC[j];
+    bt.ps = ps;
+    bt.partials = c->bpartials;
+    for (int wp = 0; wp < prm.warps; ++wp) {
+      BatchWarp bw{};
+      bw.I0 = c->bI0s[s];
+      bw.G = c->bG;
+      for (int k = 0; k < 2; ++k)
+        for (int j = 0; j < 2; ++j) bw.U[k][j] = c->bU[k][j];
+      for (int j = 0; j < 3; ++j) bw.C[j] = c->bC[j];
+      bw.ips = c->bips[s];
+      bw.gps = ps;
+      bw.ps = ps;
+      bw.W = lw;
+      bw.H = lh;
+      bw.P = P;
+      bw.sel = all;
+      bw.sel.ubit = ubit;
+      hipLaunchKernelGGL(kb_warp, grid2(lw, lh, n), kBlk2, 0, st, bw);
+      int nact = 0;
+      for (int b = 0; b < n; ++b) {
+        nit[b] = 0;
+        err[b] = DBL_MAX;
+        prev[b] = 0.0;
+        act[b] = prm.iterations > 0;
+        nact += act[b];
+      }
+      while (nact > 0) {
+        // each active pair's pass (the single-pair rule), the batch runs the shortest
+        int K = kTbMax;
+        std::vector<int> kb(n, 0);
+        std::vector<char> ends(n, 0);
+        for (int b = 0; b < n; ++b) {
+          if (!act[b]) continue;
+          int k = 0;
+          double ps_ = prev[b];
+          while (k < kTbMax && nit[b] + k < prm.iterations) {
+            const bool ce = (prm.epsilon > 0) && ((nit[b] + k) & 1) && (ps_ < scaledEps);
+            ++k;
+            if (ce) {
+              ends[b] = 1;
+              break;
+            }
+            ps_ -= scaledEps;
+          }
+          kb[b] = k;
+          K = std::min(K, k);
+        }
+        BatchSel sel{};
+        BatchSel chk{};
+        for (int b = 0; b < n; ++b) {
+          if (!act[b]) continue;
+          sel.idx[sel.n++] = (uint8_t)b;
+          if (ends[b] && kb[b] == K) {
+            sel.cerr |= 1ull << b;
+            chk.idx[chk.n++] = (uint8_t)b;
+          }
+        }
+        sel.ubit = ubit;
+        sel.pbit = pbit;
+        sel.pzero = pzero;
+        bt.t.niter = K;
+        bt.t.out_h = 32 - 2 * K;
+        const int blocks = bt.t.tiles_x * ((lh + bt.t.out_h - 1) / bt.t.out_h);
+        if (blocks > c->bnblk)
+          return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", blocks, c->bnblk);
+        bt.nblk = blocks;
+        bt.sel = sel;
+        hipLaunchKernelGGL((kb_iterate_tb<32, 1, 2>), dim3(blocks, sel.n), dim3(32 * 32), 0, st, bt);
+        for (int j = 0; j < sel.n; ++j) {
+          const int b = sel.idx[j];
+          for (int i = 0; i < K; ++i)
+            if (!(((sel.cerr >> b) & 1) && i == K - 1)) prev[b] -= scaledEps;
+          nit[b] += K;
+          ubit ^= 1ull << b;
+          pbit ^= 1ull << b;
+          pzero &= ~(1ull << b);
+          err[b] = DBL_MAX;
+        }
+        if (chk.n > 0) {
+          hipLaunchKernelGGL(kb_reduce, dim3(chk.n), dim3(kBlock), 0, st, c->bpartials, blocks,
+                             chk, c->pinned_dev + 8);
+          HIP_TRY(c, hipEventRecord(c->ev_check, st));
+          HIP_TRY(c, hipEventSynchronize(c->ev_check));
+          for (int j = 0; j < chk.n; ++j) {
+            const int b = chk.idx[j];
+            err[b] = c->pinned[8 + b];
+            prev[b] = err[b];
+            ++checks[b];
+          }
+        }
+        nact = 0;
+        for (int j = 0; j < sel.n; ++j) {
+          const int b = sel.idx[j];
+          act[b] = err[b] > scaledEps && nit[b] < prm.iterations;
+          nact += act[b];
+        }
+      }
+      for (int b = 0; b < n; ++b) {
+        level_iters[(size_t)b * TVL1_MAX_LEVELS + s] += nit[b];
+        if (stats && stats[b].warp_iterations &&
+            s * prm.warps + wp < stats[b].warp_iterations_capacity)
+          stats[b].warp_iterations[s * prm.warps + wp] = nit[b];
+      }
+    }
+    HIP_TRY(c, hipGetLastError());
+    if (s == 0) break;
+    BatchUp up{};
+    for (int k = 0; k < 2; ++k)
+      for (int j = 0; j < 2; ++j) up.U[k][j] = c->bU[k][j];
+    up.ps = ps;
+    up.sw = lw;
+    up.sh = lh;
+    up.sp = P;
+    up.dw = g.ws[s - 1];
+    up.dh = g.hs[s - 1];
+    up.dp = g.ps[s - 1];
+    up.fx = (float)(1.0 / ((double)up.dw / lw));
+    up.fy = (float)(1.0 / ((double)up.dh / lh));
+    up.mul = upmul;
+    up.sel = all;
+    up.sel.ubit = ubit;
+    hipLaunchKernelGGL(kb_upsample, grid2(up.dw, up.dh, 2 * n), kBlk2, 0, st, up);
+    ubit ^= n == 64 ? ~0ull : ((1ull << n) - 1);
+  }
+  BatchOut bo{};
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < 2; ++j) bo.U[k][j] = c->bU[k][j];
+  bo.ps = ps;
+  bo.W = W;
+  bo.H = H;
+  bo.P = g.ps[0];
+  bo.u = u;
+  bo.v = v;
+  bo.fpitch = fpitch;
+  bo.fstride = fstride;
+  bo.sel = all;
+  bo.sel.ubit = ubit;
+  hipLaunchKernelGGL(kb_output, grid2(W, H, n), kBlk2, 0, st, bo);
+  HIP_TRY(c, hipGetLastError());
+  if (stats) {
+    for (int b = 0; b < n; ++b) {
+      tvl1_stats &sb = stats[b];
+      sb.levels = L;
+      int64_t tot = 0;
+      int64_t li[TVL1_MAX_LEVELS] = {};
+      for (int s = 0; s < TVL1_MAX_LEVELS; ++s) {
+        li[s] = s < L ? level_iters[(size_t)b * TVL1_MAX_LEVELS + s] : 0;
+        sb.level_width[s] = s < L ? g.ws[s] : 0;
+        sb.level_height[s] = s < L ? g.hs[s] : 0;
+        sb.level_iterations[s] = li[s];
+        tot += li[s];
+      }
+      sb.iterations_total = tot;
+      sb.checks_total = checks[b];
+      sb.speculation_misses = 0;
+      sb.algorithmic_bytes = survey_bytes(g, prm.warps, li);
+      for (int k = 0; k < 4; ++k) {
+        sb.kernel_ms[k] = 0.0;
+        sb.kernel_launches[k] = 0;
+        sb.kernel_bytes[k] = 0.0;
+        sb.kernel_hbm_bytes[k] = 0.0;
+      }
+    }
+  }
+  return TVL1_OK;
+}
+
 extern "C" {
 
 void tvl1_params_default(tvl1_params *p) {
@@ -1139,7 +1437,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_WARP_MODE")) c->warp_mode = atoi(m);
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void **)&c->pinned, sizeof(double) * 8,
+      hipHostMalloc((void **)&c->pinned, sizeof(double) * (8 + kBatchMax),
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&c->pinned_dev, c->pinned, 0) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_check, hipEventDisableTiming) != hipSuccess) {
@@ -1225,6 +1523,42 @@ tvl1_status tvl1_calc(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8
   return solve(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch, stats, (hipStream_t)stream);
 }
 
+
+tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pitch0,
+                            size_t pair_stride0, const uint8_t *I1, size_t pitch1,
+                            size_t pair_stride1, int32_t W, int32_t H, float *u, float *v,
+                            size_t fpitch, size_t flow_pair_stride, tvl1_stats *stats,
+                            void *stream) {
+  if (n <= 0) return set_err(c, TVL1_EINVAL, "batch size must be > 0 (got %d)", n);
+  tvl1_status s = check_call(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch);
+  if (s != TVL1_OK) return s;
+  if (n > 1 && (pair_stride0 < pitch0 * (size_t)H || pair_stride1 < pitch1 * (size_t)H ||
+                flow_pair_stride < fpitch * (size_t)H))
+    return set_err(c, TVL1_EINVAL, "pair strides must cover one image / flow field");
+  HIP_TRY(c, hipSetDevice(c->device));
+  s = ensure_geometry(c, W, H);
+  if (s != TVL1_OK) return s;
+  const tvl1_params &prm = c->prm;
+  const float taut = (float)(prm.tau / prm.theta);
+  // the batched kernels cover the reference's path with gamma = 0 (every production
+  // config); other parameter sets solve the pairs one by one, same results
+  const bool batched = prm.profile == 0 && prm.gamma == 0.0 && prm.median_filtering <= 1 &&
+                       prm.fast_math == 0 && taut >= 0.0f && taut <= FLT_MAX;
+  for (int b0 = 0; b0 < n; b0 += batched ? kBatchMax : 1) {
+    const int m = batched ? std::min(kBatchMax, n - b0) : 1;
+    const uint8_t *i0 = I0 + (size_t)b0 * pair_stride0, *i1 = I1 + (size_t)b0 * pair_stride1;
+    float *ub = reinterpret_cast<float *>(reinterpret_cast<char *>(u) + (size_t)b0 * flow_pair_stride);
+    float *vb = reinterpret_cast<float *>(reinterpret_cast<char *>(v) + (size_t)b0 * flow_pair_stride);
+    s = batched ? solve_batch_chunk(c, m, i0, pitch0, pair_stride0, i1, pitch1, pair_stride1, W,
+                                    H, ub, vb, fpitch, flow_pair_stride, stats ? stats + b0 : nullptr,
+                                    (hipStream_t)stream)
+                : solve(c, i0, pitch0, i1, pitch1, W, H, ub, vb, fpitch, stats ? stats + b0 : nullptr,
+                        (hipStream_t)stream);
+    if (s != TVL1_OK) return s;
+  }
+  return TVL1_OK;
+}
+
 tvl1_status tvl1_calc_host(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8_t *I1,
                            size_t pitch1, int32_t W, int32_t H, float *u, float *v,
                            size_t fpitch, tvl1_stats *stats) {
@@ -1276,6 +1610,7 @@ void tvl1_destroy(tvl1_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   if (c->arena) (void)hipFree(c->arena);
+  if (c->barena) (void)hipFree(c->barena);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->ev_check) (void)hipEventDestroy(c->ev_check);

@@ -159,6 +159,11 @@ def load_engine() -> C.CDLL:
                               C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_size_t,
                               C.POINTER(TVL1Stats), C.c_void_p]
     lib.tvl1_calc.restype = C.c_int
+    lib.tvl1_calc_batch.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_size_t, C.c_size_t,
+                                    C.c_void_p, C.c_size_t, C.c_size_t, C.c_int32, C.c_int32,
+                                    C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
+                                    C.POINTER(TVL1Stats), C.c_void_p]
+    lib.tvl1_calc_batch.restype = C.c_int
     lib.tvl1_calc_host.argtypes = [C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t,
                                    C.POINTER(C.c_uint8), C.c_size_t, C.c_int32, C.c_int32,
                                    C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_size_t,
@@ -277,6 +282,33 @@ class Engine:
                                 C.c_void_p(stream) if stream else None)
         self._check(rc, "tvl1_calc")
         return stats_dict(st) if st is not None else None
+
+    def calc_batch_device(self, n: int, dI0: int, pitch0: int, stride0: int, dI1: int,
+                          pitch1: int, stride1: int, w: int, h: int, du: int, dv: int,
+                          flow_pitch: int, flow_stride: int, stream: int = 0,
+                          warp_iters: bool = False):
+        """tvl1_calc_batch on device buffers: n pairs of one size, pair b at base + b*stride
+        (bytes).  Returns one stats dict per pair (+ per-warp iterations if asked)."""
+        sts = (TVL1Stats * n)()
+        wis = []
+        if warp_iters:
+            cap = TVL1_MAX_LEVELS * max(1, self.params.warps)
+            for b in range(n):
+                wi = np.full(cap, -1, np.int32)
+                sts[b].warp_iterations = wi.ctypes.data_as(C.POINTER(C.c_int32))
+                sts[b].warp_iterations_capacity = cap
+                wis.append(wi)
+        rc = self.lib.tvl1_calc_batch(self.ctx, n, C.c_void_p(dI0), pitch0, stride0,
+                                      C.c_void_p(dI1), pitch1, stride1, w, h, C.c_void_p(du),
+                                      C.c_void_p(dv), flow_pitch, flow_stride, sts,
+                                      C.c_void_p(stream) if stream else None)
+        self._check(rc, "tvl1_calc_batch")
+        out = [stats_dict(sts[b]) for b in range(n)]
+        if warp_iters:
+            for b in range(n):
+                L = out[b]["levels"]
+                out[b]["warp_iters"] = wis[b][: L * self.params.warps].reshape(L, self.params.warps)
+        return out
 
     def close(self):
         if self.ctx:

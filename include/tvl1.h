@@ -138,6 +138,21 @@ tvl1_status tvl1_calc(tvl1_ctx *ctx,
                       float *u, float *v, size_t flow_pitch,
                       tvl1_stats *stats, void *stream);
 
+/* Batched solve (build addition for the production workload, SURVEY 3.2: two 3072x100
+ * ROI strips per slice pair, each a solve of ~400 tiny launches): n pairs of one size,
+ * pair b at I0 + b*pair_stride0, I1 + b*pair_stride1 (bytes; device pointers, as in
+ * tvl1_calc), flow of pair b at u / v + b*flow_pair_stride.  Up to 64 pairs share every
+ * kernel launch; each pair's flow and per-warp iteration counts are those of tvl1_calc
+ * (bit-identical).  stats: NULL or an array of n.  gamma != 0, profile 1, median filtering
+ * and fast_math solve the pairs one by one.  Asynchronous on `stream` like tvl1_calc, but
+ * the host waits at residual checks. */
+tvl1_status tvl1_calc_batch(tvl1_ctx *ctx, int32_t n,
+                            const uint8_t *I0, size_t pitch0, size_t pair_stride0,
+                            const uint8_t *I1, size_t pitch1, size_t pair_stride1,
+                            int32_t width, int32_t height,
+                            float *u, float *v, size_t flow_pitch, size_t flow_pair_stride,
+                            tvl1_stats *stats, void *stream);
+
 /* Same on HOST memory: upload, solve, download, synchronize.
  * (GpuMat::upload optflow.cpp:315-316 ... download :475-476) */
 tvl1_status tvl1_calc_host(tvl1_ctx *ctx,

@@ -19,7 +19,7 @@ def declared_functions():
 
 def test_header_declares_the_boundary():
     names = declared_functions()
-    for must in ("tvl1_create", "tvl1_calc", "tvl1_calc_host", "tvl1_destroy",
+    for must in ("tvl1_create", "tvl1_calc", "tvl1_calc_host", "tvl1_calc_batch", "tvl1_destroy",
                  "tvl1_last_error", "tvl1_postprocess", "tvl1_params_default"):
         assert must in names
 

@@ -1,0 +1,106 @@
+"""tvl1_calc_batch (the production strip workload): every pair of a batch must
+get exactly the single-pair result -- bit-identical flow and the same per-warp iteration
+counts as the oracle -- whatever the other pairs of the batch do."""
+import numpy as np
+import pytest
+
+from optflow_amd import capi, synth
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def bits_equal(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint32),
+                          np.ascontiguousarray(b).view(np.uint32))
+
+
+def run_batch(eng, I0s, I1s):
+    """Pairs packed contiguously on the device (pair stride = one image)."""
+    n, h, w = I0s.shape
+    dev = torch.device("cuda", 0)
+    d0 = torch.from_numpy(np.ascontiguousarray(I0s)).to(dev)
+    d1 = torch.from_numpy(np.ascontiguousarray(I1s)).to(dev)
+    du = torch.zeros((n, h, w), dtype=torch.float32, device=dev)
+    dv = torch.zeros((n, h, w), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    st = eng.calc_batch_device(n, d0.data_ptr(), w, w * h, d1.data_ptr(), w, w * h, w, h,
+                               du.data_ptr(), dv.data_ptr(), 4 * w, 4 * w * h, warp_iters=True)
+    torch.cuda.synchronize()
+    return du.cpu().numpy(), dv.cpu().numpy(), st
+
+
+def check_against_oracle(p, I0s, I1s, u, v, st):
+    for b in range(I0s.shape[0]):
+        ur, vr, sr, wr = capi.oracle_calc(I0s[b], I1s[b], p)
+        assert st[b]["levels"] == sr["levels"]
+        np.testing.assert_array_equal(st[b]["warp_iters"], wr, err_msg=f"pair {b}")
+        assert bits_equal(u[b], ur) and bits_equal(v[b], vr), f"pair {b} not bit-exact"
+
+
+def pairs(n, w, h, seed):
+    I0s, I1s = [], []
+    for b in range(n):
+        a, c = synth.gen_pair(w, h, seed=seed + b, z=1 + b % 3)
+        I0s.append(a)
+        I1s.append(c)
+    return np.stack(I0s), np.stack(I1s)
+
+
+@pytest.mark.parametrize("n,w,h,kw", [
+    (6, 300, 100, dict(nscales=10, warps=5)),          # production strip shape (scaled down)
+    (3, 250, 131, dict(nscales=5, warps=5)),
+    (1, 97, 40, dict(nscales=3, warps=3)),
+    (5, 200, 60, dict(nscales=4, warps=3, epsilon=0.0, iterations=7)),   # fixed work
+])
+def test_batch_matches_oracle(built, n, w, h, kw):
+    p = capi.make_params(**kw)
+    eng = capi.Engine(p)
+    I0s, I1s = pairs(n, w, h, seed=100 + n)
+    u, v, st = run_batch(eng, I0s, I1s)
+    eng.close()
+    check_against_oracle(p, I0s, I1s, u, v, st)
+
+
+def test_batch_larger_than_one_chunk(built):
+    """70 pairs: two chunks (64 + 6), plus an identical pair (stops at n = 2 everywhere)."""
+    p = capi.make_params(nscales=3, warps=2)
+    eng = capi.Engine(p)
+    I0s, I1s = pairs(70, 64, 24, seed=7)
+    I1s[5] = I0s[5]
+    u, v, st = run_batch(eng, I0s, I1s)
+    eng.close()
+    assert np.all(u[5] == 0) and np.all(st[5]["warp_iters"] == 2)
+    sel = [0, 5, 63, 64, 69]
+    check_against_oracle(p, I0s[sel], I1s[sel], u[sel], v[sel], [st[b] for b in sel])
+
+
+def test_batch_strided_stack(built):
+    """Adjacent pairs (z, z+1) of one contiguous device stack: I1 of pair b is I0 of b+1."""
+    Z, w, h = 6, 160, 48
+    stack = np.stack([synth.gen_pair(w, h, seed=3, z=z)[1] for z in range(Z)])
+    p = capi.make_params(nscales=4, warps=4)
+    eng = capi.Engine(p)
+    dev = torch.device("cuda", 0)
+    ds = torch.from_numpy(stack).to(dev)
+    n = Z - 1
+    du = torch.zeros((n, h, w), dtype=torch.float32, device=dev)
+    dv = torch.zeros((n, h, w), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    st = eng.calc_batch_device(n, ds.data_ptr(), w, w * h, ds.data_ptr() + w * h, w, w * h, w,
+                               h, du.data_ptr(), dv.data_ptr(), 4 * w, 4 * w * h,
+                               warp_iters=True)
+    torch.cuda.synchronize()
+    eng.close()
+    check_against_oracle(p, stack[:-1], stack[1:], du.cpu().numpy(), dv.cpu().numpy(), st)
+
+
+@pytest.mark.parametrize("kw", [dict(gamma=0.2), dict(median_filtering=5), dict(profile=1)])
+def test_batch_falls_back_per_pair(built, kw):
+    """Parameter sets outside the batched kernels solve pair by pair: same results."""
+    p = capi.make_params(nscales=3, warps=2, **kw)
+    eng = capi.Engine(p)
+    I0s, I1s = pairs(3, 90, 40, seed=55)
+    u, v, st = run_batch(eng, I0s, I1s)
+    eng.close()
+    check_against_oracle(p, I0s, I1s, u, v, st)
