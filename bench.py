@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--no-fast-math-line", action="store_true",
                     help="skip the secondary fast-math measurement")
     ap.add_argument("--cpu-sample", default="3072x2048")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="slice pairs solved concurrently per GPU (one ctx + stream + host "
                          "thread each); a step = one batch of this many pairs")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -96,7 +96,10 @@ def parse():
     ap.add_argument("--strides", default="1")
     ap.add_argument("--chunk", type=int, default=8,
                     help="stack: contiguous pairs per work item (slice reuse within it)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.inflight is None:   # pairs (or strip batches) in flight per GPU
+        args.inflight = 4 if args.workload == "strips" else 2
+    return args
 
 
 def cpu_baseline(I0, I1, params, sample: str):

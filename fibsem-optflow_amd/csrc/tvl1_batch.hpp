@@ -169,6 +169,53 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void kb_itera
   tb_iterate_store<false, RH, NG, PX, false>(t, lds, r, Y, X, c4, rr);
 }
 
+// The same pass as a k_iterate_roll<false, K, PX> wavefront pipeline (blockIdx.y = entry of
+// sel, 4 wavefronts per block): for strips the column bands walk all rows of the level in
+// one segment, so the halo recompute is 2K rows and 2 halo px per band, against 64x32
+// regions' 1.5-1.8x.  Residual partials of pair b at partials + b * nblk (one per wave).
+struct BatchRoll {
+  RollArgs ra;
+  float *U[2][2];
+  float *Pp[2][4];
+  const float *C[3];
+  size_t ps;
+  double *partials;
+  int nblk;
+  BatchSel sel;
+};
+template <int K, int PX>
+__global__ __launch_bounds__(256) void kb_iterate_roll(BatchRoll br) {
+  const int b = br.sel.idx[blockIdx.y];
+  RollArgs ra = br.ra;
+  IterArgs &a = ra.it;
+  {
+    const size_t o = b * br.ps;
+    const int us = bsel_bit(br.sel.ubit, b), qs = bsel_bit(br.sel.pbit, b);
+    a.u1s = br.U[us][0] + o;
+    a.u2s = br.U[us][1] + o;
+    a.u1d = br.U[us ^ 1][0] + o;
+    a.u2d = br.U[us ^ 1][1] + o;
+    a.p11s = br.Pp[qs][0] + o;
+    a.p12s = br.Pp[qs][1] + o;
+    a.p21s = br.Pp[qs][2] + o;
+    a.p22s = br.Pp[qs][3] + o;
+    a.p11d = br.Pp[qs ^ 1][0] + o;
+    a.p12d = br.Pp[qs ^ 1][1] + o;
+    a.p21d = br.Pp[qs ^ 1][2] + o;
+    a.p22d = br.Pp[qs ^ 1][3] + o;
+    a.I1wx = br.C[0] + o;
+    a.I1wy = br.C[1] + o;
+    a.rho = br.C[2] + o;
+    a.calc_err = bsel_bit(br.sel.cerr, b);
+    a.p_zero = bsel_bit(br.sel.pzero, b);
+    a.partials = br.partials + (size_t)b * br.nblk;
+  }
+  const int wid =
+      __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+  if (wid >= ra.waves) return;
+  roll_body<false, K, PX, false>(ra, wid);
+}
+
 // K7 for the selected pairs: fixed-order sum of pair b's partials into out[b].
 __global__ void kb_reduce(const double *__restrict__ partials, int n, BatchSel sel,
                           double *__restrict__ out) {

@@ -105,6 +105,7 @@ struct tvl1_ctx {
   float *bU[2][2] = {}, *bP[2][4] = {}, *bC[3] = {};
   size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
   double *bpartials = nullptr;
+  int batch_tb = 0;                     // TVL1_BATCH_TB=1: blocked regions for batch passes
   int bnblk = 0;                        // partials per pair
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
@@ -1249,14 +1250,46 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         sel.ubit = ubit;
         sel.pbit = pbit;
         sel.pzero = pzero;
-        bt.t.niter = K;
-        bt.t.out_h = 32 - 2 * K;
-        const int blocks = bt.t.tiles_x * ((lh + bt.t.out_h - 1) / bt.t.out_h);
-        if (blocks > c->bnblk)
-          return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", blocks, c->bnblk);
-        bt.nblk = blocks;
-        bt.sel = sel;
-        hipLaunchKernelGGL((kb_iterate_tb<32, 1, 2>), dim3(blocks, sel.n), dim3(32 * 32), 0, st, bt);
+        int blocks;   // residual partials per pair
+        if (c->batch_tb) {   // 64x32 blocked regions (TVL1_BATCH_TB=1)
+          bt.t.niter = K;
+          bt.t.out_h = 32 - 2 * K;
+          blocks = bt.t.tiles_x * ((lh + bt.t.out_h - 1) / bt.t.out_h);
+          if (blocks > c->bnblk)
+            return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", blocks, c->bnblk);
+          bt.nblk = blocks;
+          bt.sel = sel;
+          hipLaunchKernelGGL((kb_iterate_tb<32, 1, 2>), dim3(blocks, sel.n), dim3(32 * 32), 0, st, bt);
+        } else {   // wavefront pipelines: 128-px bands down the whole level, one per wave
+          BatchRoll br{};
+          br.ra.it = bt.t.it;
+          const int halo = (K + 1) / 2 * 2;   // roll_halo<K, 2>
+          br.ra.bands = (lw + 128 - 2 * halo - 1) / (128 - 2 * halo);
+          // segments sized so the batch's wavefronts fill whole rounds of resident slots
+          br.ra.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
+                                           : roll_segment(br.ra.bands * sel.n, lh, K,
+                                                          c->roll_slots[K][0][2]);
+          br.ra.waves = br.ra.bands * ((lh + br.ra.seg_rows - 1) / br.ra.seg_rows);
+          blocks = br.ra.waves;
+          if (blocks > c->bnblk)
+            return set_err(c, TVL1_EHIP, "internal: %d waves > batch partials %d", blocks, c->bnblk);
+          for (int k = 0; k < 2; ++k)
+            for (int j = 0; j < 2; ++j) br.U[k][j] = c->bU[k][j];
+          for (int k = 0; k < 2; ++k)
+            for (int j = 0; j < 4; ++j) br.Pp[k][j] = c->bP[k][j];
+          for (int j = 0; j < 3; ++j) br.C[j] = c->bC[j];
+          br.ps = ps;
+          br.partials = c->bpartials;
+          br.nblk = blocks;
+          br.sel = sel;
+          const dim3 grid((br.ra.waves + 3) / 4, sel.n);
+          switch (K) {
+            case 1: hipLaunchKernelGGL((kb_iterate_roll<1, 2>), grid, dim3(256), 0, st, br); break;
+            case 2: hipLaunchKernelGGL((kb_iterate_roll<2, 2>), grid, dim3(256), 0, st, br); break;
+            case 3: hipLaunchKernelGGL((kb_iterate_roll<3, 2>), grid, dim3(256), 0, st, br); break;
+            default: hipLaunchKernelGGL((kb_iterate_roll<4, 2>), grid, dim3(256), 0, st, br); break;
+          }
+        }
         for (int j = 0; j < sel.n; ++j) {
           const int b = sel.idx[j];
           for (int i = 0; i < K; ++i)
@@ -1425,6 +1458,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_WARP_NW")) c->warp_nw = atoi(m);
   if (const char *m = getenv("TVL1_FUSE_STORE")) c->fuse_store = atoi(m) != 0;
   if (const char *m = getenv("TVL1_WITER_BW")) c->witer_bw = atoi(m) == 64 ? 64 : 128;
+  if (const char *m = getenv("TVL1_BATCH_TB")) c->batch_tb = atoi(m) != 0;
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse_first = atoi(m) == 1 ? 1 : atoi(m) == 2 ? 2 : 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // tests: force the 64-bit-addressed kernels

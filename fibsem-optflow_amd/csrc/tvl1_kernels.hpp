@@ -1784,16 +1784,14 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
 template <int K, int PX>
 constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
 
-template <bool G, int K, int PX, bool FM = false>
-__global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
+// The pass of one wavefront (band / segment wid < ra.waves); k_iterate_roll and the
+// batched kb_iterate_roll differ only in how they find their planes and wid.
+template <bool G, int K, int PX, bool FM>
+__device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   constexpr int HALO = roll_halo<K, PX>();
   constexpr int BW = 64 * PX;            // band width (px)
   const IterArgs &a = ra.it;
   const int lane = threadIdx.x & 63;
-  // wave-uniform (scalar) band / segment
-  const int wid =
-      __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
-  if (wid >= ra.waves) return;                       // whole wavefronts only
   const int band = wid % ra.bands, seg = wid / ra.bands;
   RollLane L;
   L.X = band * (BW - 2 * HALO) - HALO + PX * lane;
@@ -1872,6 +1870,15 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) a.partials[wid] = acc;
   }
+}
+
+template <bool G, int K, int PX, bool FM = false>
+__global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
+  // wave-uniform (scalar) band / segment
+  const int wid =
+      __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+  if (wid >= ra.waves) return;                       // whole wavefronts only
+  roll_body<G, K, PX, FM>(ra, wid);
 }
 
 // ---------------------------------------------------------------- K5 + first K6/K8 pass

@@ -53,7 +53,11 @@ def pairs(n, w, h, seed):
     (1, 97, 40, dict(nscales=3, warps=3)),
     (5, 200, 60, dict(nscales=4, warps=3, epsilon=0.0, iterations=7)),   # fixed work
 ])
-def test_batch_matches_oracle(built, n, w, h, kw):
+@pytest.mark.parametrize("env", ["", "TVL1_BATCH_TB=1"])
+def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw):
+    monkeypatch.delenv("TVL1_BATCH_TB", raising=False)
+    if env:
+        monkeypatch.setenv(*env.split("="))
     p = capi.make_params(**kw)
     eng = capi.Engine(p)
     I0s, I1s = pairs(n, w, h, seed=100 + n)
