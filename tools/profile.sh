@@ -7,7 +7,7 @@ tag=${1:-r1}; shift
 out=gpurun_out/prof_$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-B="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-fast-math-line $*"
+B="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-fast-math-line --no-strips-line $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- python3 $B > $out/bench_trace.log 2>&1 || { echo TRACE_FAIL; tail -5 $out/bench_trace.log; exit 1; }
 for ctr in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
   name=$(echo $ctr | tr ' ' '_')
