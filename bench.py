@@ -88,7 +88,7 @@ def parse():
                          "thread each); a step = one batch of this many pairs")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip per-kernel HIP events (roofline fields become null)")
-    ap.add_argument("--batch", type=int, default=64,
+    ap.add_argument("--batch", type=int, default=256,
                     help="strips: pairs per tvl1_calc_batch call")
     ap.add_argument("--workload", choices=("pair", "stack", "strips"), default="pair",
                     help="pair: BASELINE configs[1] (C2, the headline); stack: adjacent / "
@@ -100,7 +100,7 @@ def parse():
                     help="stack: contiguous pairs per work item (slice reuse within it)")
     args = ap.parse_args()
     if args.inflight is None:   # pairs (or strip batches) in flight per GPU
-        args.inflight = 4 if args.workload == "strips" else 2
+        args.inflight = 2
     return args
 
 
@@ -359,18 +359,18 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
 
 def strips_line(args, rank, world, local_rank, dist):
     """The production-strip figure reported beside the C2 headline: 3072x100
-    ROI strip pairs, nscales 10, warps 5, batches of 64, 4 batches in flight, 2 steps."""
+    ROI strip pairs, nscales 10, warps 5, batches of 256, 2 batches in flight, 2 steps."""
     import copy
     a = copy.copy(args)
     a.width, a.height, a.nscales, a.warps = 3072, 100, 10, 5
     a.iterations, a.epsilon = 300, 0.01
-    a.batch, a.inflight, a.steps, a.warmup = 64, 4, 2, 1
+    a.batch, a.inflight, a.steps, a.warmup = 256, 2, 2, 1
     o = run_strips(a, rank, world, local_rank, dist, standalone=False)
     if o is None:
         return None
     return {"workload": o["config"]["workload"], "value": o["value"], "unit": o["unit"],
             "slice_pairs_per_s": o["config"]["slice_pairs_per_s"],
-            "ms_per_step": o["ms_per_step"], "batch": 64, "batches_in_flight_per_gpu": 4,
+            "ms_per_step": o["ms_per_step"], "batch": a.batch, "batches_in_flight_per_gpu": a.inflight,
             "iterations_per_strip": o["config"]["iterations_per_strip"],
             "cpu_baseline": o["cpu_baseline"],
             "api": "tvl1_calc_batch (DESIGN.md 4.6)"}

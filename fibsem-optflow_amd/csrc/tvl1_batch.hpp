@@ -17,16 +17,24 @@
 
 namespace tvl1k {
 
-constexpr int kBatchMax = 64;
+constexpr int kBatchMax = 256;
+
+struct BatchMask {           // one bit per pair of a chunk
+  uint64_t w[kBatchMax / 64];
+  __host__ __device__ int test(int b) const { return (int)((w[b >> 6] >> (b & 63)) & 1u); }
+  __host__ void set(int b) { w[b >> 6] |= 1ull << (b & 63); }
+  __host__ void clear(int b) { w[b >> 6] &= ~(1ull << (b & 63)); }
+  __host__ void flip(int b) { w[b >> 6] ^= 1ull << (b & 63); }
+};
 
 struct BatchSel {            // the pairs a launch works on, passed by value
   int n;                     // number of entries in idx
   uint8_t idx[kBatchMax];    // pair indices
-  uint64_t ubit, pbit;       // per pair: current u set / p set (0 or 1)
-  uint64_t cerr, pzero;      // per pair: the pass ends in a residual check / p == 0
+  BatchMask ubit, pbit;      // per pair: current u set / p set (0 or 1)
+  BatchMask cerr, pzero;     // per pair: the pass ends in a residual check / p == 0
 };
 
-__device__ __forceinline__ int bsel_bit(uint64_t m, int b) { return (int)((m >> b) & 1u); }
+__device__ __forceinline__ int bsel_bit(const BatchMask &m, int b) { return m.test(b); }
 
 // K1 convertTo for both frames of every pair: blockIdx.z = 2 * pair + frame.
 __global__ void kb_convert(const uint8_t *__restrict__ I0, size_t p0, size_t s0,

@@ -1165,7 +1165,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
   const float l_t = (float)(prm.lambda * prm.theta);
   const float taut = (float)(prm.tau / prm.theta);
   const float upmul = (float)(1.0 / prm.scale_step);
-  uint64_t ubit = 0, pbit = 0;
+  BatchMask ubit{}, pbit{};
   std::vector<int64_t> level_iters((size_t)n * TVL1_MAX_LEVELS, 0), checks(n, 0);
   std::vector<int> nit(n);
   std::vector<double> err(n), prev(n);
@@ -1175,7 +1175,8 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
     const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
     hipLaunchKernelGGL(kb_gradient, grid2(lw, lh, n), kBlk2, 0, st, c->bI1s[s], c->bips[s], lw,
                        lh, P, c->bG, ps);
-    uint64_t pzero = n == 64 ? ~0ull : ((1ull << n) - 1);   // p = 0 at every level start
+    BatchMask pzero{};   // p = 0 at every level start
+    for (int b = 0; b < n; ++b) pzero.set(b);
     BatchTB bt{};
     bt.t.it.W = lw;
     bt.t.it.H = lh;
@@ -1243,7 +1244,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           if (!act[b]) continue;
           sel.idx[sel.n++] = (uint8_t)b;
           if (ends[b] && kb[b] == K) {
-            sel.cerr |= 1ull << b;
+            sel.cerr.set(b);
             chk.idx[chk.n++] = (uint8_t)b;
           }
         }
@@ -1293,11 +1294,11 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         for (int j = 0; j < sel.n; ++j) {
           const int b = sel.idx[j];
           for (int i = 0; i < K; ++i)
-            if (!(((sel.cerr >> b) & 1) && i == K - 1)) prev[b] -= scaledEps;
+            if (!(sel.cerr.test(b) && i == K - 1)) prev[b] -= scaledEps;
           nit[b] += K;
-          ubit ^= 1ull << b;
-          pbit ^= 1ull << b;
-          pzero &= ~(1ull << b);
+          ubit.flip(b);
+          pbit.flip(b);
+          pzero.clear(b);
           err[b] = DBL_MAX;
         }
         if (chk.n > 0) {
@@ -1344,7 +1345,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
     up.sel = all;
     up.sel.ubit = ubit;
     hipLaunchKernelGGL(kb_upsample, grid2(up.dw, up.dh, 2 * n), kBlk2, 0, st, up);
-    ubit ^= n == 64 ? ~0ull : ((1ull << n) - 1);
+    for (int b = 0; b < n; ++b) ubit.flip(b);
   }
   BatchOut bo{};
   for (int k = 0; k < 2; ++k)

@@ -141,7 +141,7 @@ tvl1_status tvl1_calc(tvl1_ctx *ctx,
 /* Batched solve (build addition for the production workload, SURVEY 3.2: two 3072x100
  * ROI strips per slice pair, each a solve of ~400 tiny launches): n pairs of one size,
  * pair b at I0 + b*pair_stride0, I1 + b*pair_stride1 (bytes; device pointers, as in
- * tvl1_calc), flow of pair b at u / v + b*flow_pair_stride.  Up to 64 pairs share every
+ * tvl1_calc), flow of pair b at u / v + b*flow_pair_stride.  Up to 256 pairs share every
  * kernel launch; each pair's flow and per-warp iteration counts are those of tvl1_calc
  * (bit-identical).  stats: NULL or an array of n.  gamma != 0, profile 1, median filtering
  * and fast_math solve the pairs one by one.  Asynchronous on `stream` like tvl1_calc, but

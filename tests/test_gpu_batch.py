@@ -67,15 +67,15 @@ def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw):
 
 
 def test_batch_larger_than_one_chunk(built):
-    """70 pairs: two chunks (64 + 6), plus an identical pair (stops at n = 2 everywhere)."""
+    """260 pairs: two chunks (256 + 4), plus an identical pair (stops at n = 2 everywhere)."""
     p = capi.make_params(nscales=3, warps=2)
     eng = capi.Engine(p)
-    I0s, I1s = pairs(70, 64, 24, seed=7)
+    I0s, I1s = pairs(260, 64, 24, seed=7)
     I1s[5] = I0s[5]
     u, v, st = run_batch(eng, I0s, I1s)
     eng.close()
     assert np.all(u[5] == 0) and np.all(st[5]["warp_iters"] == 2)
-    sel = [0, 5, 63, 64, 69]
+    sel = [0, 5, 63, 64, 200, 255, 256, 259]
     check_against_oracle(p, I0s[sel], I1s[sel], u[sel], v[sel], [st[b] for b in sel])
 
 
