@@ -271,7 +271,8 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
 
     W, H, B, F = args.width, args.height, args.batch, max(1, args.inflight)
     params = capi.make_params(nscales=args.nscales, warps=args.warps,
-                              iterations=args.iterations, epsilon=args.epsilon)
+                              iterations=args.iterations, epsilon=args.epsilon,
+                              fast_math=int(args.fast_math))
     dev = torch.device("cuda", local_rank)
     slots = []
     for j in range(F):
@@ -343,7 +344,8 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "math": "IEEE (bit-identical to oracle/)", "data": "synthetic",
+        "math": ("fast (CUDA_FAST_MATH semantics)" if args.fast_math
+                 else "IEEE (bit-identical to oracle/)"), "data": "synthetic",
         "config": {"workload": (f"production ROI strips (SURVEY 3.2): {W}x{H} pairs, nscales "
                                 f"{args.nscales}, warps {args.warps}, epsilon {args.epsilon}; "
                                 f"2 strips per slice pair"),

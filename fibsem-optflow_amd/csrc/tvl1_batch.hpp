@@ -90,6 +90,7 @@ struct BatchWarp {
   int W, H, P;
   BatchSel sel;
 };
+template <bool FM>
 __global__ void kb_warp(BatchWarp w) {
   const int x = blockIdx.x * 64 + threadIdx.x;
   const int y = blockIdx.y * 4 + threadIdx.y;
@@ -102,15 +103,21 @@ __global__ void kb_warp(BatchWarp w) {
   const float wx = (float)x + u1v;
   const float wy = (float)y + u2v;
   float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
-  warp_gather<false>(G, w.P, 0, 0, w.W, w.H, wx, wy, tap_floor(wx), tap_floor(wy), sum, sumx,
-                     sumy, wsum);
-  const float coeff = 1.0f / wsum;
+  warp_gather_fn<FM>(
+      [&](int cy, int cx) {
+        const float4 g = G[(size_t)imin(imax(cy, 0), w.H - 1) * w.P + imin(imax(cx, 0), w.W - 1)];
+        return Tap3{g.x, g.y, g.z};
+      },
+      wx, wy, tap_floor(wx), tap_floor(wy), sum, sumx, sumy, wsum);
+  const float coeff = FM ? __builtin_amdgcn_rcpf(wsum) : 1.0f / wsum;
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
+  const float i0 = w.I0[b * w.ips + i];
   w.C[0][o + i] = I1wxv;
   w.C[1][o + i] = I1wyv;
-  w.C[2][o + i] = I1wv - I1wxv * u1v - I1wyv * u2v - w.I0[b * w.ips + i];
+  w.C[2][o + i] = FM ? __builtin_fmaf(-I1wyv, u2v, __builtin_fmaf(-I1wxv, u1v, I1wv)) - i0
+                     : I1wv - I1wxv * u1v - I1wyv * u2v - i0;
 }
 
 // K6+K8(+K7 partials): one temporally blocked pass of t.niter iterations on each selected
@@ -126,7 +133,7 @@ struct BatchTB {
   int nblk;                  // regions per pair
   BatchSel sel;
 };
-template <int RH, int NG, int PX>
+template <int RH, int NG, int PX, bool FM>
 __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void kb_iterate_tb(BatchTB bt) {
   constexpr int LPR = 64 / PX;
   constexpr int HALF = RH / NG;
@@ -174,7 +181,7 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void kb_itera
     const int ya = imin(imax(Y[g], 0), a.H - 1);
     load_row<false, PX>(r[g], a, (size_t)ya * a.P + xa);
   }
-  tb_iterate_store<false, RH, NG, PX, false>(t, lds, r, Y, X, c4, rr);
+  tb_iterate_store<false, RH, NG, PX, FM>(t, lds, r, Y, X, c4, rr);
 }
 
 // The same pass as a k_iterate_roll<false, K, PX> wavefront pipeline (blockIdx.y = entry of
@@ -191,7 +198,7 @@ struct BatchRoll {
   int nblk;
   BatchSel sel;
 };
-template <int K, int PX>
+template <int K, int PX, bool FM>
 __global__ __launch_bounds__(256) void kb_iterate_roll(BatchRoll br) {
   const int b = br.sel.idx[blockIdx.y];
   RollArgs ra = br.ra;
@@ -221,7 +228,40 @@ __global__ __launch_bounds__(256) void kb_iterate_roll(BatchRoll br) {
   const int wid =
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
   if (wid >= ra.waves) return;
-  roll_body<false, K, PX, false>(ra, wid);
+  roll_body<false, K, PX, FM>(ra, wid);
+}
+
+// build-only median filter (k_median) of every selected pair's current u set into the
+// other set (blockIdx.z = 2 * entry + component)
+struct BatchMedian {
+  float *U[2][2];
+  size_t ps;
+  int W, H, P, ksize;
+  BatchSel sel;
+};
+__global__ void kb_median(BatchMedian w) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= w.W || y >= w.H) return;
+  const int b = w.sel.idx[blockIdx.z >> 1], c = blockIdx.z & 1;
+  const int us = bsel_bit(w.sel.ubit, b);
+  const float *src = w.U[us][c] + b * w.ps;
+  const int r = w.ksize / 2;
+  float v[25];
+  int n = 0;
+  for (int dy = -r; dy <= r; ++dy)
+    for (int dx = -r; dx <= r; ++dx)
+      v[n++] = src[(size_t)imin(imax(y + dy, 0), w.H - 1) * w.P + imin(imax(x + dx, 0), w.W - 1)];
+  for (int i = 1; i < n; ++i) {
+    const float t = v[i];
+    int j = i - 1;
+    while (j >= 0 && v[j] > t) {
+      v[j + 1] = v[j];
+      --j;
+    }
+    v[j + 1] = t;
+  }
+  w.U[us ^ 1][c][b * w.ps + (size_t)y * w.P + x] = v[n / 2];
 }
 
 // K7 for the selected pairs: fixed-order sum of pair b's partials into out[b].

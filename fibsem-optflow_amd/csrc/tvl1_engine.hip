@@ -1165,6 +1165,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
   const float l_t = (float)(prm.lambda * prm.theta);
   const float taut = (float)(prm.tau / prm.theta);
   const float upmul = (float)(1.0 / prm.scale_step);
+  const bool fm = prm.fast_math != 0;
   BatchMask ubit{}, pbit{};
   std::vector<int64_t> level_iters((size_t)n * TVL1_MAX_LEVELS, 0), checks(n, 0);
   std::vector<int> nit(n);
@@ -1206,9 +1207,26 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
       bw.W = lw;
       bw.H = lh;
       bw.P = P;
+      if (prm.median_filtering > 1) {   // build-only median of u before each warp
+        BatchMedian md{};
+        for (int k = 0; k < 2; ++k)
+          for (int j = 0; j < 2; ++j) md.U[k][j] = c->bU[k][j];
+        md.ps = ps;
+        md.W = lw;
+        md.H = lh;
+        md.P = P;
+        md.ksize = prm.median_filtering;
+        md.sel = all;
+        md.sel.ubit = ubit;
+        hipLaunchKernelGGL(kb_median, grid2(lw, lh, 2 * n), kBlk2, 0, st, md);
+        for (int b = 0; b < n; ++b) ubit.flip(b);
+      }
       bw.sel = all;
       bw.sel.ubit = ubit;
-      hipLaunchKernelGGL(kb_warp, grid2(lw, lh, n), kBlk2, 0, st, bw);
+      if (fm)
+        hipLaunchKernelGGL(kb_warp<true>, grid2(lw, lh, n), kBlk2, 0, st, bw);
+      else
+        hipLaunchKernelGGL(kb_warp<false>, grid2(lw, lh, n), kBlk2, 0, st, bw);
       int nact = 0;
       for (int b = 0; b < n; ++b) {
         nit[b] = 0;
@@ -1260,7 +1278,10 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
             return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", blocks, c->bnblk);
           bt.nblk = blocks;
           bt.sel = sel;
-          hipLaunchKernelGGL((kb_iterate_tb<32, 1, 2>), dim3(blocks, sel.n), dim3(32 * 32), 0, st, bt);
+          if (fm)
+            hipLaunchKernelGGL((kb_iterate_tb<32, 1, 2, true>), dim3(blocks, sel.n), dim3(32 * 32), 0, st, bt);
+          else
+            hipLaunchKernelGGL((kb_iterate_tb<32, 1, 2, false>), dim3(blocks, sel.n), dim3(32 * 32), 0, st, bt);
         } else {   // wavefront pipelines: 128-px bands down the whole level, one per wave
           BatchRoll br{};
           br.ra.it = bt.t.it;
@@ -1284,12 +1305,18 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           br.nblk = blocks;
           br.sel = sel;
           const dim3 grid((br.ra.waves + 3) / 4, sel.n);
+#define KB_ROLL(KK)                                                                            \
+  if (fm)                                                                                      \
+    hipLaunchKernelGGL((kb_iterate_roll<KK, 2, true>), grid, dim3(256), 0, st, br);            \
+  else                                                                                         \
+    hipLaunchKernelGGL((kb_iterate_roll<KK, 2, false>), grid, dim3(256), 0, st, br);
           switch (K) {
-            case 1: hipLaunchKernelGGL((kb_iterate_roll<1, 2>), grid, dim3(256), 0, st, br); break;
-            case 2: hipLaunchKernelGGL((kb_iterate_roll<2, 2>), grid, dim3(256), 0, st, br); break;
-            case 3: hipLaunchKernelGGL((kb_iterate_roll<3, 2>), grid, dim3(256), 0, st, br); break;
-            default: hipLaunchKernelGGL((kb_iterate_roll<4, 2>), grid, dim3(256), 0, st, br); break;
+            case 1: KB_ROLL(1) break;
+            case 2: KB_ROLL(2) break;
+            case 3: KB_ROLL(3) break;
+            default: KB_ROLL(4) break;
           }
+#undef KB_ROLL
         }
         for (int j = 0; j < sel.n; ++j) {
           const int b = sel.idx[j];
@@ -1577,8 +1604,7 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pi
   const float taut = (float)(prm.tau / prm.theta);
   // the batched kernels cover the reference's path with gamma = 0 (every production
   // config); other parameter sets solve the pairs one by one, same results
-  const bool batched = prm.profile == 0 && prm.gamma == 0.0 && prm.median_filtering <= 1 &&
-                       prm.fast_math == 0 && taut >= 0.0f && taut <= FLT_MAX;
+  const bool batched = prm.profile == 0 && prm.gamma == 0.0 && taut >= 0.0f && taut <= FLT_MAX;
   for (int b0 = 0; b0 < n; b0 += batched ? kBatchMax : 1) {
     const int m = batched ? std::min(kBatchMax, n - b0) : 1;
     const uint8_t *i0 = I0 + (size_t)b0 * pair_stride0, *i1 = I1 + (size_t)b0 * pair_stride1;

@@ -143,9 +143,9 @@ tvl1_status tvl1_calc(tvl1_ctx *ctx,
  * pair b at I0 + b*pair_stride0, I1 + b*pair_stride1 (bytes; device pointers, as in
  * tvl1_calc), flow of pair b at u / v + b*flow_pair_stride.  Up to 256 pairs share every
  * kernel launch; each pair's flow and per-warp iteration counts are those of tvl1_calc
- * (bit-identical).  stats: NULL or an array of n.  gamma != 0, profile 1, median filtering
- * and fast_math solve the pairs one by one.  Asynchronous on `stream` like tvl1_calc, but
- * the host waits at residual checks. */
+ * (bit-identical; with fast_math = 1 within the same tolerance as tvl1_calc's).  stats: NULL
+ * or an array of n.  gamma != 0 and profile 1 solve the pairs one by one.  Asynchronous on
+ * `stream` like tvl1_calc, but the host waits at residual checks. */
 tvl1_status tvl1_calc_batch(tvl1_ctx *ctx, int32_t n,
                             const uint8_t *I0, size_t pitch0, size_t pair_stride0,
                             const uint8_t *I1, size_t pitch1, size_t pair_stride1,

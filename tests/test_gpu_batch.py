@@ -99,7 +99,33 @@ def test_batch_strided_stack(built):
     check_against_oracle(p, stack[:-1], stack[1:], du.cpu().numpy(), dv.cpu().numpy(), st)
 
 
-@pytest.mark.parametrize("kw", [dict(gamma=0.2), dict(median_filtering=5), dict(profile=1)])
+@pytest.mark.parametrize("kw", [dict(median_filtering=5), dict(median_filtering=3)])
+def test_batch_median(built, kw):
+    p = capi.make_params(nscales=4, warps=3, **kw)
+    eng = capi.Engine(p)
+    I0s, I1s = pairs(4, 120, 50, seed=61)
+    u, v, st = run_batch(eng, I0s, I1s)
+    eng.close()
+    check_against_oracle(p, I0s, I1s, u, v, st)
+
+
+def test_batch_fast_math_within_tolerance(built):
+    """fast_math = 1 batches (the FM kernels): the oracle's iteration schedule, mean EPE
+    <= 1e-3 px (tests/test_gpu_fastmath.py's bar)."""
+    kw = dict(nscales=10, warps=5)
+    eng = capi.Engine(capi.make_params(fast_math=1, **kw))
+    I0s, I1s = pairs(4, 300, 100, seed=71)
+    u, v, st = run_batch(eng, I0s, I1s)
+    eng.close()
+    p = capi.make_params(**kw)
+    for b in range(4):
+        ur, vr, sr, wr = capi.oracle_calc(I0s[b], I1s[b], p)
+        np.testing.assert_array_equal(st[b]["warp_iters"], wr)
+        e = capi.epe(u[b], v[b], ur, vr)
+        assert float(e.mean()) <= 1e-3 and float((e > 1e-2).mean()) <= 1e-3
+
+
+@pytest.mark.parametrize("kw", [dict(gamma=0.2), dict(profile=1)])
 def test_batch_falls_back_per_pair(built, kw):
     """Parameter sets outside the batched kernels solve pair by pair: same results."""
     p = capi.make_params(nscales=3, warps=2, **kw)
