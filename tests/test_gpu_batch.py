@@ -134,3 +134,29 @@ def test_batch_falls_back_per_pair(built, kw):
     u, v, st = run_batch(eng, I0s, I1s)
     eng.close()
     check_against_oracle(p, I0s, I1s, u, v, st)
+
+
+@pytest.mark.parametrize("where", ["top", "bottom"])
+def test_batch_roi_strips_of_a_stack(built, where):
+    """top / bottom ROI strips (a sub-view of every slice) of adjacent
+    pairs of one device stack in one call -- the production layout."""
+    Z, w, h, rows = 5, 130, 60, 20
+    stack = np.stack([synth.gen_pair(w, h, seed=9, z=z)[1] for z in range(Z)])
+    p = capi.make_params(nscales=10, warps=3)
+    eng = capi.Engine(p)
+    dev = torch.device("cuda", 0)
+    ds = torch.from_numpy(stack).to(dev)
+    n = Z - 1
+    off = 0 if where == "top" else (h - rows) * w
+    du = torch.zeros((n, rows, w), dtype=torch.float32, device=dev)
+    dv = torch.zeros((n, rows, w), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    st = eng.calc_batch_device(n, ds.data_ptr() + off, w, w * h, ds.data_ptr() + w * h + off, w,
+                               w * h, w, rows, du.data_ptr(), dv.data_ptr(), 4 * w, 4 * w * rows,
+                               warp_iters=True)
+    torch.cuda.synchronize()
+    eng.close()
+    sl = slice(0, rows) if where == "top" else slice(h - rows, h)
+    I0s = np.ascontiguousarray(stack[:-1, sl])
+    I1s = np.ascontiguousarray(stack[1:, sl])
+    check_against_oracle(p, I0s, I1s, du.cpu().numpy(), dv.cpu().numpy(), st)
