@@ -1097,10 +1097,12 @@ static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n) {
     (void)hipFree(c->barena);
     c->barena = nullptr;
   }
+  c->barena_bytes = 0;
   hipError_t e = hipMalloc((void **)&c->barena, bytes);
   if (e != hipSuccess)
     return set_err(c, TVL1_ENOMEM, "hipMalloc(%zu) for the batch arena failed: %s", bytes,
                    hipGetErrorString(e));
+  c->barena_bytes = bytes;
   HIP_TRY(c, hipMemsetAsync(c->barena, 0, bytes, c->own_stream));   // finite pitch padding
   HIP_TRY(c, hipStreamSynchronize(c->own_stream));
   char *p = c->barena;
@@ -1605,8 +1607,22 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pi
   // the batched kernels cover the reference's path with gamma = 0 (every production
   // config); other parameter sets solve the pairs one by one, same results
   const bool batched = prm.profile == 0 && prm.gamma == 0.0 && taut >= 0.0f && taut <= FLT_MAX;
-  for (int b0 = 0; b0 < n; b0 += batched ? kBatchMax : 1) {
-    const int m = batched ? std::min(kBatchMax, n - b0) : 1;
+  // chunk size: kBatchMax pairs, fewer when their batch arena would not fit in half of
+  // the device memory free now (large frames: one chunk of 256 6144x4096 pairs is 0.7 TB)
+  int chunk = kBatchMax;
+  if (batched) {
+    const Geometry &g = c->geo;
+    double per_pair = 19.0 * align_up((size_t)g.ps[0] * H, 64) * sizeof(float);
+    for (int l = 0; l < g.L; ++l) per_pair += 2.0 * (double)g.ps[l] * g.hs[l] * sizeof(float);
+    per_pair += (((W + 55) / 56) * ((H + 23) / 24) + 64) * sizeof(double);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+      const double avail = 0.5 * (double)free_b + (double)c->barena_bytes;
+      chunk = (int)std::max(1.0, std::min((double)kBatchMax, avail / per_pair));
+    }
+  }
+  for (int b0 = 0; b0 < n; b0 += batched ? chunk : 1) {
+    const int m = batched ? std::min(chunk, n - b0) : 1;
     const uint8_t *i0 = I0 + (size_t)b0 * pair_stride0, *i1 = I1 + (size_t)b0 * pair_stride1;
     float *ub = reinterpret_cast<float *>(reinterpret_cast<char *>(u) + (size_t)b0 * flow_pair_stride);
     float *vb = reinterpret_cast<float *>(reinterpret_cast<char *>(v) + (size_t)b0 * flow_pair_stride);

@@ -160,3 +160,22 @@ def test_batch_roi_strips_of_a_stack(built, where):
     I0s = np.ascontiguousarray(stack[:-1, sl])
     I1s = np.ascontiguousarray(stack[1:, sl])
     check_against_oracle(p, I0s, I1s, du.cpu().numpy(), dv.cpu().numpy(), st)
+
+
+def test_batch_of_benchmark_pairs_equals_single_solves(built):
+    """Two 6144x4096 pairs (C2) in one batch: the same bits and iteration counts as
+    tvl1_calc on each (which matches the oracle at this size, test_benchmark_pair_bit_exact)."""
+    p = capi.make_params(nscales=5, warps=30)
+    eng = capi.Engine(p)
+    I0s, I1s = [], []
+    for z in (1, 2):
+        a, c = synth.gen_pair(6144, 4096, seed=0x5EED, z=z)
+        I0s.append(a)
+        I1s.append(c)
+    I0s, I1s = np.stack(I0s), np.stack(I1s)
+    u, v, st = run_batch(eng, I0s, I1s)
+    for b in range(2):
+        us, vs, ss, ws = eng.calc_host(I0s[b], I1s[b])
+        np.testing.assert_array_equal(st[b]["warp_iters"], ws)
+        assert bits_equal(u[b], us) and bits_equal(v[b], vs)
+    eng.close()
