@@ -120,6 +120,34 @@ __global__ void kb_warp(BatchWarp w) {
                      : I1wv - I1wxv * u1v - I1wyv * u2v - i0;
 }
 
+// K5 as k_warp_ring's streaming gather (64-px bands, LDS window ring of I1 / I1x / I1y
+// built from I1) on each selected pair (blockIdx.y = entry of sel).
+struct BatchRing {
+  WarpRingArgs wa;           // geometry (bands, seg_rows, waves per pair); pointers set per pair
+  const float *I0, *I1;      // level s images of pair 0 (pair stride ips)
+  const float *U[2][2];      // u sets (pair stride ps)
+  float *C[3];
+  size_t ips, ps;
+  BatchSel sel;
+};
+template <int M, int NW>
+__global__ __launch_bounds__(64 * NW) void kb_warp_ring(BatchRing br) {
+  __shared__ float ring[3 * warp_ring_rows<M, NW>() * (64 + 2 * M)];
+  const int b = br.sel.idx[blockIdx.y];
+  WarpRingArgs a = br.wa;
+  const int us = bsel_bit(br.sel.ubit, b);
+  a.I0 = br.I0 + b * br.ips;
+  a.I1 = br.I1 + b * br.ips;
+  a.u1 = br.U[us][0] + b * br.ps;
+  a.u2 = br.U[us][1] + b * br.ps;
+  a.I1wx = br.C[0] + b * br.ps;
+  a.I1wy = br.C[1] + b * br.ps;
+  a.rho = br.C[2] + b * br.ps;
+  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
+  if (wid >= a.waves) return;
+  warp_ring_body<M, NW>(a, wid, ring);
+}
+
 // K6+K8(+K7 partials): one temporally blocked pass of t.niter iterations on each selected
 // pair (blockIdx.y = entry of sel, blockIdx.x = region) -- k_iterate_tb's body on the
 // pair's planes.  Residual partials of pair b at partials + b * nblk.

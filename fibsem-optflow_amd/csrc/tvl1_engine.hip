@@ -106,6 +106,7 @@ struct tvl1_ctx {
   size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
   double *bpartials = nullptr;
   int batch_tb = 0;                     // TVL1_BATCH_TB=1: blocked regions for batch passes
+  int batch_warp = 0;                   // TVL1_BATCH_WARP=1: per-px global gather (kb_warp)
   int bnblk = 0;                        // partials per pair
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
@@ -1225,10 +1226,30 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
       }
       bw.sel = all;
       bw.sel.ubit = ubit;
-      if (fm)
-        hipLaunchKernelGGL(kb_warp<true>, grid2(lw, lh, n), kBlk2, 0, st, bw);
-      else
-        hipLaunchKernelGGL(kb_warp<false>, grid2(lw, lh, n), kBlk2, 0, st, bw);
+      if (fm || c->batch_warp == 1) {   // per-px global gather from G
+        if (fm)
+          hipLaunchKernelGGL(kb_warp<true>, grid2(lw, lh, n), kBlk2, 0, st, bw);
+        else
+          hipLaunchKernelGGL(kb_warp<false>, grid2(lw, lh, n), kBlk2, 0, st, bw);
+      } else {   // k_warp_ring's streaming LDS-ring gather, per pair
+        BatchRing br{};
+        br.wa.W = lw;
+        br.wa.H = lh;
+        br.wa.P = P;
+        br.wa.bands = (lw + 63) / 64;
+        br.wa.seg_rows = roll_segment(br.wa.bands * n, lh, 6, c->warp_ring_slots[6][2]);
+        br.wa.waves = br.wa.bands * ((lh + br.wa.seg_rows - 1) / br.wa.seg_rows);
+        br.I0 = c->bI0s[s];
+        br.I1 = c->bI1s[s];
+        for (int k = 0; k < 2; ++k)
+          for (int j = 0; j < 2; ++j) br.U[k][j] = c->bU[k][j];
+        for (int j = 0; j < 3; ++j) br.C[j] = c->bC[j];
+        br.ips = c->bips[s];
+        br.ps = ps;
+        br.sel = all;
+        br.sel.ubit = ubit;
+        hipLaunchKernelGGL((kb_warp_ring<6, 2>), dim3(br.wa.waves, n), dim3(128), 0, st, br);
+      }
       int nact = 0;
       for (int b = 0; b < n; ++b) {
         nit[b] = 0;
@@ -1489,6 +1510,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_FUSE_STORE")) c->fuse_store = atoi(m) != 0;
   if (const char *m = getenv("TVL1_WITER_BW")) c->witer_bw = atoi(m) == 64 ? 64 : 128;
   if (const char *m = getenv("TVL1_BATCH_TB")) c->batch_tb = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_BATCH_WARP")) c->batch_warp = atoi(m);
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse_first = atoi(m) == 1 ? 1 : atoi(m) == 2 ? 2 : 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // tests: force the 64-bit-addressed kernels

@@ -802,16 +802,14 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
 }
 
 template <int M, int NW>
-__global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
+__device__ __forceinline__ void warp_ring_body(const WarpRingArgs &a, int wid, float *__restrict__ ring) {
   constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>(), PL = R * WW;
   static_assert(3 * WW < 256, "one tap row within ds_read2_b32 offsets");
   static_assert(2 * NW + 2 * M <= R, "ring too small for the margin");
   static_assert(2 * M <= 64, "second window slot per lane");
-  __shared__ float ring[3 * PL];
+  (void)PL;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
-  if (wid >= a.waves) return;   // whole blocks
   const int band = wid % a.bands, seg = wid / a.bands;
   const int x0 = band * 64;
   // the lane's two window slots: clamped column, its clamped x-1 and x+1 (byte offsets)
@@ -854,6 +852,14 @@ __global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
     warp_ring_step<M, NW>(ring, B, A, a, y0 + NW, ye, w, lane, x0, xs, xcb, nb, rowb);
     warp_ring_step<M, NW>(ring, C, B, a, y0 + 2 * NW, ye, w, lane, x0, xs, xcb, nb, rowb);
   }
+}
+
+template <int M, int NW>
+__global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
+  __shared__ float ring[3 * warp_ring_rows<M, NW>() * (64 + 2 * M)];
+  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
+  if (wid >= a.waves) return;   // whole blocks
+  warp_ring_body<M, NW>(a, wid, ring);
 }
 
 // warpBackward straight from the level image (no precomputed gradient plane): the

@@ -53,9 +53,10 @@ def pairs(n, w, h, seed):
     (1, 97, 40, dict(nscales=3, warps=3)),
     (5, 200, 60, dict(nscales=4, warps=3, epsilon=0.0, iterations=7)),   # fixed work
 ])
-@pytest.mark.parametrize("env", ["", "TVL1_BATCH_TB=1"])
+@pytest.mark.parametrize("env", ["", "TVL1_BATCH_TB=1", "TVL1_BATCH_WARP=1"])
 def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw):
     monkeypatch.delenv("TVL1_BATCH_TB", raising=False)
+    monkeypatch.delenv("TVL1_BATCH_WARP", raising=False)
     if env:
         monkeypatch.setenv(*env.split("="))
     p = capi.make_params(**kw)
