@@ -148,6 +148,57 @@ __global__ __launch_bounds__(64 * NW) void kb_warp_ring(BatchRing br) {
   warp_ring_body<M, NW>(a, wid, ring);
 }
 
+// K5 + the warp's first pass (2 iterations ending in the first check) fused, as
+// k_warp_iter (warp_iter_body), on each selected pair (blockIdx.y = entry of sel).  The
+// warp constants are always stored (pairs that continue read them in later passes).
+struct BatchWI {
+  WarpIterArgs w;            // geometry and scalars; pointers set per pair
+  const float *I0, *I1;      // level s images of pair 0 (pair stride ips)
+  float *U[2][2];
+  float *Pp[2][4];
+  float *C[3];
+  size_t ips, ps;
+  double *partials;
+  int nblk;
+  BatchSel sel;
+};
+template <int M, bool FM>
+__global__ __launch_bounds__(192) void kb_warp_iter(BatchWI bw) {
+  __shared__ float ring[kWiRows * 3 * wi_ww<M, 128>()];
+  __shared__ float cring[2 * 5 * 128];
+  const int b = bw.sel.idx[blockIdx.y];
+  WarpIterArgs w = bw.w;
+  IterArgs &a = w.ra.it;
+  {
+    const size_t o = b * bw.ps;
+    const int us = bsel_bit(bw.sel.ubit, b), qs = bsel_bit(bw.sel.pbit, b);
+    a.u1s = bw.U[us][0] + o;
+    a.u2s = bw.U[us][1] + o;
+    a.u1d = bw.U[us ^ 1][0] + o;
+    a.u2d = bw.U[us ^ 1][1] + o;
+    a.p11s = bw.Pp[qs][0] + o;
+    a.p12s = bw.Pp[qs][1] + o;
+    a.p21s = bw.Pp[qs][2] + o;
+    a.p22s = bw.Pp[qs][3] + o;
+    a.p11d = bw.Pp[qs ^ 1][0] + o;
+    a.p12d = bw.Pp[qs ^ 1][1] + o;
+    a.p21d = bw.Pp[qs ^ 1][2] + o;
+    a.p22d = bw.Pp[qs ^ 1][3] + o;
+    a.I1wx = bw.C[0] + o;
+    a.I1wy = bw.C[1] + o;
+    a.rho = bw.C[2] + o;
+    a.calc_err = 1;
+    a.p_zero = bsel_bit(bw.sel.pzero, b);
+    a.partials = bw.partials + (size_t)b * bw.nblk;
+    w.I0 = bw.I0 + b * bw.ips;
+    w.I1 = bw.I1 + b * bw.ips;
+    w.store_c = 1;
+  }
+  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
+  if (wid >= w.ra.waves) return;
+  warp_iter_body<M, FM, 128>(w, wid, ring, cring);
+}
+
 // K6+K8(+K7 partials): one temporally blocked pass of t.niter iterations on each selected
 // pair (blockIdx.y = entry of sel, blockIdx.x = region) -- k_iterate_tb's body on the
 // pair's planes.  Residual partials of pair b at partials + b * nblk.

@@ -107,6 +107,7 @@ struct tvl1_ctx {
   double *bpartials = nullptr;
   int batch_tb = 0;                     // TVL1_BATCH_TB=1: blocked regions for batch passes
   int batch_warp = 0;                   // TVL1_BATCH_WARP=1: per-px global gather (kb_warp)
+  int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
   int bnblk = 0;                        // partials per pair
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
@@ -1084,7 +1085,9 @@ static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n) {
   if (c->barena && c->bW == W && c->bH == H && c->bL == g.L && c->bn >= n) return TVL1_OK;
   const size_t P0 = (size_t)g.ps[0];
   const size_t ps = align_up(P0 * H, 64);
-  const int tb_blocks = ((W + 55) / 56) * ((H + 23) / 24) + 64;
+  // residual partials per pair: blocked regions (56 x 24 px) or rolling / fused waves
+  // (>= 56-px bands x >= 8-row segments)
+  const int tb_blocks = std::max(((W + 55) / 56) * ((H + 23) / 24), ((W + 55) / 56) * ((H + 7) / 8)) + 64;
   size_t bytes = 0;
   size_t ips[TVL1_MAX_LEVELS];
   for (int s = 0; s < g.L; ++s) {
@@ -1226,7 +1229,40 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
       }
       bw.sel = all;
       bw.sel.ubit = ubit;
-      if (fm || c->batch_warp == 1) {   // per-px global gather from G
+      // warpBackward fused with the warp's first pass, which is 2 iterations ending in the
+      // first check for every pair (procOneScale with epsilon > 0, iterations >= 2)
+      const bool fuse = c->batch_fuse && prm.epsilon > 0 && prm.iterations >= 2;
+      if (fuse) {
+        BatchWI wi{};
+        wi.w.ra.it = bt.t.it;
+        wi.w.ra.bands = (lw + 123) / 124;
+        wi.w.ra.seg_rows = roll_segment(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots[6][0]);
+        wi.w.ra.waves = wi.w.ra.bands * ((lh + wi.w.ra.seg_rows - 1) / wi.w.ra.seg_rows);
+        if (wi.w.ra.waves > c->bnblk)
+          return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", wi.w.ra.waves, c->bnblk);
+        wi.I0 = c->bI0s[s];
+        wi.I1 = c->bI1s[s];
+        for (int k = 0; k < 2; ++k)
+          for (int j = 0; j < 2; ++j) wi.U[k][j] = c->bU[k][j];
+        for (int k = 0; k < 2; ++k)
+          for (int j = 0; j < 4; ++j) wi.Pp[k][j] = c->bP[k][j];
+        for (int j = 0; j < 3; ++j) wi.C[j] = c->bC[j];
+        wi.ips = c->bips[s];
+        wi.ps = ps;
+        wi.partials = c->bpartials;
+        wi.nblk = wi.w.ra.waves;
+        wi.sel = all;
+        wi.sel.ubit = ubit;
+        wi.sel.pbit = pbit;
+        wi.sel.pzero = pzero;
+        if (fm)
+          hipLaunchKernelGGL((kb_warp_iter<6, true>), dim3(wi.w.ra.waves, n), dim3(192), 0, st, wi);
+        else
+          hipLaunchKernelGGL((kb_warp_iter<6, false>), dim3(wi.w.ra.waves, n), dim3(192), 0, st, wi);
+        hipLaunchKernelGGL(kb_reduce, dim3(n), dim3(kBlock), 0, st, c->bpartials, wi.w.ra.waves,
+                           all, c->pinned_dev + 8);
+        HIP_TRY(c, hipEventRecord(c->ev_check, st));
+      } else if (fm || c->batch_warp == 1) {   // per-px global gather from G
         if (fm)
           hipLaunchKernelGGL(kb_warp<true>, grid2(lw, lh, n), kBlk2, 0, st, bw);
         else
@@ -1257,6 +1293,21 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         prev[b] = 0.0;
         act[b] = prm.iterations > 0;
         nact += act[b];
+      }
+      if (fuse) {   // the fused first pass: n = 0 (no check), n = 1 (check)
+        HIP_TRY(c, hipEventSynchronize(c->ev_check));
+        nact = 0;
+        for (int b = 0; b < n; ++b) {
+          nit[b] = 2;
+          ubit.flip(b);
+          pbit.flip(b);
+          pzero.clear(b);
+          err[b] = c->pinned[8 + b];
+          prev[b] = err[b];
+          ++checks[b];
+          act[b] = err[b] > scaledEps && nit[b] < prm.iterations;
+          nact += act[b];
+        }
       }
       while (nact > 0) {
         // each active pair's pass (the single-pair rule), the batch runs the shortest
@@ -1511,6 +1562,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_WITER_BW")) c->witer_bw = atoi(m) == 64 ? 64 : 128;
   if (const char *m = getenv("TVL1_BATCH_TB")) c->batch_tb = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BATCH_WARP")) c->batch_warp = atoi(m);
+  if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse_first = atoi(m) == 1 ? 1 : atoi(m) == 2 ? 2 : 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // tests: force the 64-bit-addressed kernels

@@ -2249,20 +2249,18 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
   roll_advance<false, 2, PX, true, FM>(S, in, a, r, L, nb, rowb, acc);
 }
 
-template <int M, bool FM = false, int BW = 128>
-__global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
+template <int M, bool FM, int BW>
+__device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, float *__restrict__ ring,
+                                               float *__restrict__ cring) {
   constexpr int K = 2, PX = BW / 64, HALO = roll_halo<2, PX>(), WW = wi_ww<M, BW>();
   static_assert(BW == 64 || BW == 128, "one producer per 64 columns, PX = 1 or 2");
   static_assert(2 * M + 2 <= kWiRows, "window ring too small for the margin");
   static_assert(2 * M <= 64, "second window slot per lane");
   static_assert(kRollAhead == 2 && kWarpAhead == 2, "the step loops are unrolled by 3");
-  __shared__ float ring[kWiRows * 3 * WW];
-  __shared__ float cring[2 * 5 * BW];
+  (void)WW;
   const RollArgs &ra = w.ra;
   const IterArgs &a = ra.it;
   const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
-  if (wid >= ra.waves) return;   // whole blocks
   // wave 0 consumer, 1-2 producers (measured: a consumer on wave 1 or 2 of some blocks, or
   // a raised s_setprio for it, is slower)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2378,6 +2376,15 @@ __global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
       wi_prod_step<M, FM, BW>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
     }
   }
+}
+
+template <int M, bool FM = false, int BW = 128>
+__global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
+  __shared__ float ring[kWiRows * 3 * wi_ww<M, BW>()];
+  __shared__ float cring[2 * 5 * BW];
+  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
+  if (wid >= w.ra.waves) return;   // whole blocks
+  warp_iter_body<M, FM, BW>(w, wid, ring, cring);
 }
 
 // K7: fixed-order sum of the per-block partials (one block).

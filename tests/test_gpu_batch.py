@@ -53,12 +53,13 @@ def pairs(n, w, h, seed):
     (1, 97, 40, dict(nscales=3, warps=3)),
     (5, 200, 60, dict(nscales=4, warps=3, epsilon=0.0, iterations=7)),   # fixed work
 ])
-@pytest.mark.parametrize("env", ["", "TVL1_BATCH_TB=1", "TVL1_BATCH_WARP=1"])
+@pytest.mark.parametrize("env", ["", "TVL1_BATCH_TB=1", "TVL1_BATCH_WARP=1,TVL1_BATCH_FUSE=0",
+                                 "TVL1_BATCH_FUSE=0"])
 def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw):
-    monkeypatch.delenv("TVL1_BATCH_TB", raising=False)
-    monkeypatch.delenv("TVL1_BATCH_WARP", raising=False)
-    if env:
-        monkeypatch.setenv(*env.split("="))
+    for k in ("TVL1_BATCH_TB", "TVL1_BATCH_WARP", "TVL1_BATCH_FUSE"):
+        monkeypatch.delenv(k, raising=False)
+    for kv in filter(None, env.split(",")):
+        monkeypatch.setenv(*kv.split("="))
     p = capi.make_params(**kw)
     eng = capi.Engine(p)
     I0s, I1s = pairs(n, w, h, seed=100 + n)
