@@ -277,24 +277,25 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
     params = capi.make_params(nscales=args.nscales, warps=args.warps,
                               iterations=args.iterations, epsilon=args.epsilon,
                               fast_math=int(args.fast_math))
+    from optflow_amd.synth_device import DeviceStack
     dev = torch.device("cuda", local_rank)
     slots = []
     for j in range(F):
-        I0s, I1s = [], []
-        for b in range(B):
-            a, c = synth.gen_pair(W, H, seed=0x5EED + 977 * (rank * F + j) + b, z=1 + b % 7)
-            I0s.append(a)
-            I1s.append(c)
+        # slices 0..B of a synthetic stack, made on the device (synth_device, the SURVEY 8(d)
+        # recipe); pair b = (slice 0, slice b + 1), as the C2 pair is (base, slice z): I0
+        # pair stride 0, I1 strided through the stack
+        gen = DeviceStack(W, H, dev, seed=0x5EED + 977 * (rank * F + j))
+        stack = torch.stack([gen.slice(z) for z in range(B + 1)])
         eng = capi.Engine(params, device=local_rank)
-        slots.append(dict(eng=eng, I0=torch.from_numpy(np.stack(I0s)).to(dev),
-                          I1=torch.from_numpy(np.stack(I1s)).to(dev),
+        slots.append(dict(eng=eng, stack=stack,
                           u=torch.empty((B, H, W), dtype=torch.float32, device=dev),
                           v=torch.empty((B, H, W), dtype=torch.float32, device=dev)))
     torch.cuda.synchronize(dev)
 
     def solve(sl):
-        st = sl["eng"].calc_batch_device(B, sl["I0"].data_ptr(), W, W * H, sl["I1"].data_ptr(),
-                                         W, W * H, W, H, sl["u"].data_ptr(), sl["v"].data_ptr(),
+        base = sl["stack"].data_ptr()
+        st = sl["eng"].calc_batch_device(B, base, W, 0, base + W * H, W, W * H, W, H,
+                                         sl["u"].data_ptr(), sl["v"].data_ptr(),
                                          4 * W, 4 * W * H, stream=sl["eng"].stream)
         torch.cuda.synchronize(dev)
         return st
@@ -333,7 +334,8 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
     value = solves / elapsed
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        a, c = synth.gen_pair(W, H, seed=0x5EED, z=1)
+        st0 = slots[0]["stack"]
+        a, c = st0[0].cpu().numpy(), st0[1].cpu().numpy()
         lib = capi.load_oracle()
         t1 = time.perf_counter()
         n_rep = 4
@@ -349,7 +351,8 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
         "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "math": ("fast (CUDA_FAST_MATH semantics)" if args.fast_math
-                 else "IEEE (bit-identical to oracle/)"), "data": "synthetic",
+                 else "IEEE (bit-identical to oracle/)"),
+        "data": "synthetic (slice 0 vs slices 1..B of a device-generated stack)",
         "config": {"workload": (f"production ROI strips (SURVEY 3.2): {W}x{H} pairs, nscales "
                                 f"{args.nscales}, warps {args.warps}, epsilon {args.epsilon}; "
                                 f"2 strips per slice pair"),

@@ -1670,9 +1670,11 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pi
   if (n <= 0) return set_err(c, TVL1_EINVAL, "batch size must be > 0 (got %d)", n);
   tvl1_status s = check_call(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch);
   if (s != TVL1_OK) return s;
-  if (n > 1 && (pair_stride0 < pitch0 * (size_t)H || pair_stride1 < pitch1 * (size_t)H ||
+  // an input stride of 0 gives every pair the same frame (e.g. one reference slice)
+  if (n > 1 && ((pair_stride0 != 0 && pair_stride0 < pitch0 * (size_t)H) ||
+                (pair_stride1 != 0 && pair_stride1 < pitch1 * (size_t)H) ||
                 flow_pair_stride < fpitch * (size_t)H))
-    return set_err(c, TVL1_EINVAL, "pair strides must cover one image / flow field");
+    return set_err(c, TVL1_EINVAL, "pair strides must be 0 or cover one image; the flow stride one field");
   HIP_TRY(c, hipSetDevice(c->device));
   s = ensure_geometry(c, W, H);
   if (s != TVL1_OK) return s;

@@ -140,7 +140,8 @@ tvl1_status tvl1_calc(tvl1_ctx *ctx,
 
 /* Batched solve (build addition for the production workload, SURVEY 3.2: two 3072x100
  * ROI strips per slice pair, each a solve of ~400 tiny launches): n pairs of one size,
- * pair b at I0 + b*pair_stride0, I1 + b*pair_stride1 (bytes; device pointers, as in
+ * pair b at I0 + b*pair_stride0, I1 + b*pair_stride1 (bytes; 0 = the same frame for every
+ * pair; device pointers, as in
  * tvl1_calc), flow of pair b at u / v + b*flow_pair_stride.  Up to 256 pairs share every
  * kernel launch; each pair's flow and per-warp iteration counts are those of tvl1_calc
  * (bit-identical; with fast_math = 1 within the same tolerance as tvl1_calc's).  stats: NULL

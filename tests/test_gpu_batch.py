@@ -181,3 +181,23 @@ def test_batch_of_benchmark_pairs_equals_single_solves(built):
         np.testing.assert_array_equal(st[b]["warp_iters"], ws)
         assert bits_equal(u[b], us) and bits_equal(v[b], vs)
     eng.close()
+
+
+def test_batch_shared_reference_frame(built):
+    """pair_stride0 = 0: every pair registers against the same I0."""
+    w, h, n = 140, 50, 4
+    I0, _ = synth.gen_pair(w, h, seed=13)
+    I1s = np.stack([synth.gen_pair(w, h, seed=13, z=z)[1] for z in range(1, n + 1)])
+    p = capi.make_params(nscales=5, warps=3)
+    eng = capi.Engine(p)
+    dev = torch.device("cuda", 0)
+    d0 = torch.from_numpy(I0).to(dev)
+    d1 = torch.from_numpy(I1s).to(dev)
+    du = torch.zeros((n, h, w), dtype=torch.float32, device=dev)
+    dv = torch.zeros((n, h, w), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    st = eng.calc_batch_device(n, d0.data_ptr(), w, 0, d1.data_ptr(), w, w * h, w, h,
+                               du.data_ptr(), dv.data_ptr(), 4 * w, 4 * w * h, warp_iters=True)
+    torch.cuda.synchronize()
+    eng.close()
+    check_against_oracle(p, np.stack([I0] * n), I1s, du.cpu().numpy(), dv.cpu().numpy(), st)
