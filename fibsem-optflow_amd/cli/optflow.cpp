@@ -18,9 +18,8 @@
 //                                           file (network upload is out of scope)
 //
 // Deliberate differences (documented in DESIGN.md):
-//   * feature pre-alignment (SURF/ORB + homography, features.cpp) is out of scope:
-//     where the reference would align (features flag, size mismatch, or no ROI) the
-//     identity transform is used and a warning printed;
+//   * feature pre-alignment (features.cpp) runs on the engine's GPU ORB path; SURF
+//     (features = 2, the default type) is served by ORB with a warning;
 //   * per-image "rois" are honoured (the reference passes images["rois"], :140, so
 //     they are silently ignored there);
 //   * a malformed JSON file is an error (the reference ignores parse failure);
@@ -141,6 +140,7 @@ struct DeviceCtx {
   hipStream_t stream = nullptr;
   // device buffers, grown on demand
   uint8_t *d0 = nullptr, *d1 = nullptr;
+  uint8_t *dw = nullptr;   // warpAffine target of frame1 (feature pre-alignment)
   size_t cap_img = 0;
   float *du = nullptr, *dv = nullptr;
   size_t cap_flow = 0;
@@ -159,8 +159,10 @@ bool ensure(DeviceCtx &dc, size_t img_bytes, size_t flow_bytes, bool &realloc, s
     realloc = true;
     if (dc.d0) (void)hipFree(dc.d0);
     if (dc.d1) (void)hipFree(dc.d1);
+    if (dc.dw) (void)hipFree(dc.dw);
     if (hipMalloc((void **)&dc.d0, img_bytes) != hipSuccess ||
-        hipMalloc((void **)&dc.d1, img_bytes) != hipSuccess) {
+        hipMalloc((void **)&dc.d1, img_bytes) != hipSuccess ||
+        hipMalloc((void **)&dc.dw, img_bytes) != hipSuccess) {
       err = "hipMalloc failed for frames";
       return false;
     }
@@ -269,7 +271,7 @@ struct PairResult {
 // solve_wrapper (optflow.cpp:395-496) for one ROI.
 bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1, const Rect &r0,
                    const Rect &r1, Value &im, const Value &args, bool features,
-                   PairResult &res, std::string &err) {
+                   const float *affine, PairResult &res, std::string &err) {
   const int W = r0.width, H = r0.height;
   tvl1_params prm = generate_TV_args(im, args);
   if (tvl1_set_params(dc.ctx, &prm) != TVL1_OK) {
@@ -294,7 +296,11 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
   // or the map itself (mode 1);
   // "map": flow + grid (mode 1); otherwise unchanged.  Then zero where I1 <= 1.
   const int mode = features ? (otype == "flow" ? 2 : 1) : (otype == "map" ? 1 : 0);
-  s = tvl1_postprocess(dc.ctx, dc.du, dc.dv, fp, b, pitch1, W, H, mode, dc.stream);
+  if (features && affine)   // the features branch with the alignment's affine (:429-443)
+    s = tvl1_postprocess_affine(dc.ctx, dc.du, dc.dv, fp, b, pitch1, W, H, otype == "flow" ? 1 : 0,
+                                affine, dc.stream);
+  else
+    s = tvl1_postprocess(dc.ctx, dc.du, dc.dv, fp, b, pitch1, W, H, mode, dc.stream);
   if (s != TVL1_OK) {
     err = tvl1_last_error(dc.ctx);
     return false;
@@ -342,16 +348,72 @@ bool in_bounds(const Rect &r, const ofio::Image8 &f) {
          r.y + r.height <= f.height;
 }
 
-// Identity "alignment": frame1 resampled into frame0's geometry (warpAffine with an
-// identity matrix, BORDER_CONSTANT 0) = crop / zero-pad.
-ofio::Image8 identity_align(const ofio::Image8 &f1, int W, int H) {
-  ofio::Image8 o;
-  o.width = W;
-  o.height = H;
-  o.data.assign((size_t)W * H, 0);
-  for (int y = 0; y < std::min(H, f1.height); ++y)
-    memcpy(o.row(y), f1.row(y), (size_t)std::min(W, f1.width));
-  return o;
+// orb_defaults (features.cpp:19-32) + the ratio / homo / ransac keys of find_alignment
+// (:109, :133), each looked up in the image's args first, then the global args.
+tvl1_align_params align_params_of(const Value &im, const Value &args) {
+  tvl1_align_params p;
+  tvl1_align_params_default(&p);
+  auto i = [&](const char *k, int d) { return im.get(k, Value(args.get(k, Value(d)).asInt())).asInt(); };
+  auto f = [&](const char *k, double d) {
+    return im.get(k, Value(args.get(k, Value(d)).asDouble())).asDouble();
+  };
+  p.nfeatures = i("nfeatures", p.nfeatures);
+  p.scale_factor = (float)f("scaleFactor", p.scale_factor);
+  p.nlevels = i("nlevels", p.nlevels);
+  p.edge_threshold = i("edgeThreshold", p.edge_threshold);
+  p.first_level = i("firstLevel", p.first_level);
+  p.wta_k = i("WTA_K", p.wta_k);
+  p.patch_size = i("patchSize", p.patch_size);
+  p.fast_threshold = i("fastThreshold", p.fast_threshold);
+  p.blur_for_descriptor = im.get("blurForDescriptor", Value(args.get("blurForDescriptor", Value(false)).asBool())).asBool();
+  p.ratio = (float)f("ratio", p.ratio);
+  p.method = i("homo", p.method);
+  p.ransac_threshold = f("ransac", p.ransac_threshold);
+  return p;
+}
+
+// find_alignment(frame1, frame0) + warpAffine(frame1 -> frame0 size) (optflow.cpp:372-376,
+// features.cpp:46-167).  The aligned frame replaces frame1 on the device (and on the host,
+// for the random_points mask), as frame1_GPU = new_frame1 does in the reference.
+bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, ofio::Image8 &f1, const Value &im,
+                  const Value &args, float affine[6], std::string &err) {
+  const int feature_type = im.get("features", Value(args.get("features", Value(2)).asInt())).asInt();
+  if (feature_type != 1)   // SURF_TYPE (features.h:9) and anything else
+    fprintf(stderr, "SURF features are not part of this build; using ORB features for the "
+                    "alignment of %s.\n", im["p"].asString().c_str());
+  const tvl1_align_params p = align_params_of(im, args);
+  int32_t n_good = 0, outcome = 0;
+  tvl1_status s = tvl1_find_alignment(dc.ctx, dc.d1, (size_t)f1.width, f1.width, f1.height, dc.d0,
+                                      (size_t)f0.width, f0.width, f0.height, &p, affine, &n_good,
+                                      &outcome, dc.stream);
+  if (s != TVL1_OK) {
+    err = std::string("find_alignment: ") + tvl1_last_error(dc.ctx);
+    return false;
+  }
+  if (args.get("debug", Value(false)).asBool())
+    printf("Number of good features: %d\n", n_good);
+  if (outcome == 1) printf("Not enough matches. Using no transformation\n");
+  if (outcome == 2)
+    printf("More than twenty percent variance in zoom or no homography found, this is probably "
+           "an error, ignoring the transformation.\n");
+  s = tvl1_warp_affine_u8(dc.ctx, dc.d1, (size_t)f1.width, f1.width, f1.height, dc.dw,
+                          (size_t)f0.width, f0.width, f0.height, affine, dc.stream);
+  if (s != TVL1_OK) {
+    err = std::string("warpAffine: ") + tvl1_last_error(dc.ctx);
+    return false;
+  }
+  f1.width = f0.width;
+  f1.height = f0.height;
+  f1.data.resize((size_t)f0.width * f0.height);
+  if (hipMemcpyAsync(f1.data.data(), dc.dw, f1.data.size(), hipMemcpyDeviceToHost, dc.stream) !=
+          hipSuccess ||
+      hipStreamSynchronize(dc.stream) != hipSuccess) {
+    err = "download of the aligned frame failed";
+    return false;
+  }
+  std::swap(dc.d1, dc.dw);
+  dc.key1.clear();  // the device copy is the aligned frame, not the slice
+  return true;
 }
 
 // solve_rois (optflow.cpp:312-392)
@@ -360,17 +422,9 @@ bool solve_rois(DeviceCtx &dc, ofio::Image8 f0, ofio::Image8 f1, bool f0_residen
                 PairResult &res, std::string &err) {
   bool features = resolve_features(im, args);
   const std::string otype = output_type_of(im, args);
-  const bool need_align = features || f0.width != f1.width || f0.height != f1.height ||
-                          rois.isMember("default");
-  if (need_align) {
-    fprintf(stderr, "Feature pre-alignment is not part of this build; using the identity "
-                    "transform for %s.\n", im["p"].asString().c_str());
-    if (f1.width != f0.width || f1.height != f0.height) {
-      f1 = identity_align(f1, f0.width, f0.height);
-      f1_resident = false;
-      dc.key1.clear();  // the device copy is the aligned frame, not the slice
-    }
-  }
+  // cv::Mat affine(cv::Size(3,2), CV_32FC1) (optflow.cpp:319) is uninitialised until
+  // find_alignment fills it; the identity stands in for that here.
+  float affine[6] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f};
   size_t img_bytes = std::max(f0.data.size(), f1.data.size());
   size_t flow_bytes = 0;
   for (auto &k : rois.memberNames()) {
@@ -398,7 +452,6 @@ bool solve_rois(DeviceCtx &dc, ofio::Image8 f0, ofio::Image8 f1, bool f0_residen
   for (const auto &key : rois.memberNames()) {  // sorted, like jsoncpp getMemberNames
     im["output_suffix"] = (key == "top" || key == "bottom") ? "_" + key : std::string();
     Rect r0, r1;
-    bool feat = features;
     if (key == "custom_diff") {
       if (features) fprintf(stderr, "Features isn't compatible with different ROIs for each image.\n Ignoring features.\n");
       r0 = roi_from_array(rois[key]["0"]);
@@ -409,7 +462,14 @@ bool solve_rois(DeviceCtx &dc, ofio::Image8 f0, ofio::Image8 f1, bool f0_residen
         continue;
       }
     } else {
-      if (need_align) feat = true;
+      const bool size_differs = f0.width != f1.width || f0.height != f1.height;
+      if (features || size_differs || key == "default") {   // optflow.cpp:366-377
+        if (size_differs || (key == "default" && !features))
+          fprintf(stderr, "Rows or columns differ between frames no ROI selected, reverting to "
+                          "features even though it wasn't selected.\n");
+        if (!align_frame1(dc, f0, f1, im, args, affine, err)) return false;
+        features = true;
+      }
       r0 = r1 = roi_from_array(rois[key]);
     }
     if (!in_bounds(r0, f0) || !in_bounds(r1, f1)) {
@@ -417,7 +477,7 @@ bool solve_rois(DeviceCtx &dc, ofio::Image8 f0, ofio::Image8 f1, bool f0_residen
       ok = false;
       continue;
     }
-    if (!solve_wrapper(dc, f0, f1, r0, r1, im, args, feat, res, err)) ok = false;
+    if (!solve_wrapper(dc, f0, f1, r0, r1, im, args, features, affine, res, err)) ok = false;
   }
   if (otype == "random_points") res.pms.push_back(move_pm(im));
   return ok;

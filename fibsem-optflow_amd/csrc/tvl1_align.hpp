@@ -1,0 +1,426 @@
+// tvl1_align.hpp — feature pre-alignment: the reference's find_alignment
+// (/root/reference/src/features.cpp:46-167) and the cv::cuda::warpAffine calls around it
+// (optflow.cpp:369-371 on frame1, :429-443 on the map fields), MI355X-native.
+//
+//   * keypoints: ORB's recipe (cv::cuda::ORB, features.cpp:56-61) -- a scale pyramid
+//     (scaleFactor, nlevels), FAST-9 corners (fastThreshold) at least edgeThreshold px from
+//     the border, ranked by the Harris response (k = 0.04, 7x7 window) after 3x3
+//     non-maximum suppression, the best nfeatures kept with ORB's per-level quota;
+//     orientation by the intensity centroid of the radius-15 disc; 256-bit rotated-BRIEF
+//     descriptors (WTA_K = 2) from a fixed pseudo-random pattern of point pairs in the
+//     31x31 patch;
+//   * matching: brute-force Hamming 2-NN on the GPU (cuda::DescriptorMatcher::
+//     createBFMatcher(NORM_HAMMING)->knnMatch(.., 2)), the reference's ratio test and
+//     distance sort (features.cpp:98-113);
+//   * model: cv::findHomography(RANSAC | LMEDS, ransac threshold) restated on the host --
+//     4-point normalised DLT hypotheses, inlier count (RANSAC) or median residual (LMEDS),
+//     a least-squares DLT refit on the inliers; then the reference's zoom check and the
+//     top 2x3 of the homography as the affine (features.cpp:131-166).
+//
+// PARITY UNPINNED and approximate by construction: OpenCV's ORB bit pattern
+// (bit_pattern_31_), its FAST score, its RNG and its Levenberg-Marquardt refinement are not
+// restated, and SURF (features = 2, non-free) is served by the same ORB path with a
+// warning.  The contract kept is the reference's: the same inputs (JSON keys with their
+// defaults), an affine that maps frame1 onto frame0, the same rejection rules and messages.
+// tests/test_align_gpu.py recovers known affine motions of synthetic slices.
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <random>
+#include <vector>
+
+namespace tvl1k {
+
+constexpr int kOrbPatch = 31, kOrbHalf = 15, kOrbBits = 256;
+
+// FAST-9 on a float level image (values 0..255) at px (x, y): a contiguous arc of >= 9 of
+// the 16 radius-3 circle px all brighter than c + t or all darker than c - t.
+__constant__ int kFastDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+__constant__ int kFastDy[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
+
+__global__ void ka_fast_harris(const float *__restrict__ I, int W, int H, int P, int border,
+                               float t, float *__restrict__ score) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  float out = 0.0f;
+  if (x >= border && y >= border && x < W - border && y < H - border) {
+    const float c = I[(size_t)y * P + x];
+    unsigned bright = 0, dark = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float v = I[(size_t)(y + kFastDy[k]) * P + x + kFastDx[k]];
+      bright |= (v > c + t ? 1u : 0u) << k;
+      dark |= (v < c - t ? 1u : 0u) << k;
+    }
+    auto arc9 = [](unsigned m) {
+      const unsigned mm = m | (m << 16);   // wrap around the circle
+      unsigned run = mm;
+#pragma unroll
+      for (int k = 1; k < 9; ++k) run &= mm >> k;
+      return run != 0;
+    };
+    if (arc9(bright) || arc9(dark)) {
+      // Harris response over a 7x7 window of Sobel gradients (scaled to 0..1 intensities)
+      float a = 0.f, b = 0.f, cc = 0.f;
+      for (int dy = -3; dy <= 3; ++dy)
+        for (int dx = -3; dx <= 3; ++dx) {
+          const int yy = y + dy, xx = x + dx;
+          const float *r0 = I + (size_t)(yy - 1) * P, *r1 = I + (size_t)yy * P,
+                      *r2 = I + (size_t)(yy + 1) * P;
+          const float gx = (r0[xx + 1] - r0[xx - 1]) + 2.f * (r1[xx + 1] - r1[xx - 1]) +
+                           (r2[xx + 1] - r2[xx - 1]);
+          const float gy = (r2[xx - 1] - r0[xx - 1]) + 2.f * (r2[xx] - r0[xx]) +
+                           (r2[xx + 1] - r0[xx + 1]);
+          a += gx * gx;
+          b += gy * gy;
+          cc += gx * gy;
+        }
+      const float s = 1.0f / (4.f * 255.f * 49.f);
+      a *= s * s;
+      b *= s * s;
+      cc *= s * s;
+      out = fmaxf(a * b - cc * cc - 0.04f * (a + b) * (a + b), 1e-30f);
+    }
+  }
+  score[(size_t)y * W + x] = out;
+}
+
+// blurForDescriptor: 7x7 Gaussian, sigma 2 (ORB's GaussianBlur before the descriptors)
+__global__ void ka_blur7(const float *__restrict__ I, int W, int H, int P, float *__restrict__ O) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const float g[7] = {0.07015933f, 0.13107488f, 0.19071282f, 0.21610594f, 0.19071282f,
+                      0.13107488f, 0.07015933f};
+  float s = 0.f;
+  for (int dy = -3; dy <= 3; ++dy) {
+    const float *r = I + (size_t)imin(imax(y + dy, 0), H - 1) * P;
+    float t = 0.f;
+    for (int dx = -3; dx <= 3; ++dx) t += g[dx + 3] * r[imin(imax(x + dx, 0), W - 1)];
+    s += g[dy + 3] * t;
+  }
+  O[(size_t)y * P + x] = s;
+}
+
+struct OrbCand {
+  float x, y, score;
+};
+
+// 3x3 non-maximum suppression of the corner scores; survivors appended to cand (cap).
+__global__ void ka_nms(const float *__restrict__ score, int W, int H, OrbCand *__restrict__ cand,
+                       unsigned *__restrict__ count, unsigned cap) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x < 1 || y < 1 || x >= W - 1 || y >= H - 1) return;
+  const float s = score[(size_t)y * W + x];
+  if (s <= 0.0f) return;
+  for (int dy = -1; dy <= 1; ++dy)
+    for (int dx = -1; dx <= 1; ++dx) {
+      if (!dx && !dy) continue;
+      const float o = score[(size_t)(y + dy) * W + x + dx];
+      // ties broken by position so exactly one of two equal neighbours survives
+      if (o > s || (o == s && (dy < 0 || (dy == 0 && dx < 0)))) return;
+    }
+  const unsigned i = atomicAdd(count, 1u);
+  if (i < cap) cand[i] = OrbCand{(float)x, (float)y, s};
+}
+
+struct OrbKp {
+  float x, y;        // level coordinates
+  float angle;       // radians (filled by ka_describe)
+  int level;
+};
+
+// Orientation (intensity centroid over the radius-15 disc) and the 256-bit rotated BRIEF
+// descriptor of each keypoint; one thread per keypoint.  pat: 256 x (ax, ay, bx, by).
+__global__ void ka_describe(const float *const *__restrict__ levels, const int *__restrict__ lP,
+                            OrbKp *__restrict__ kps, int n, const int4 *__restrict__ pat,
+                            uint32_t *__restrict__ desc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  OrbKp k = kps[i];
+  const float *I = levels[k.level];
+  const int P = lP[k.level];
+  const int cx = (int)k.x, cy = (int)k.y;
+  float m01 = 0.f, m10 = 0.f;
+  for (int v = -kOrbHalf; v <= kOrbHalf; ++v)
+    for (int u = -kOrbHalf; u <= kOrbHalf; ++u) {
+      if (u * u + v * v > kOrbHalf * kOrbHalf) continue;
+      const float val = I[(size_t)(cy + v) * P + cx + u];
+      m10 += u * val;
+      m01 += v * val;
+    }
+  const float ang = atan2f(m01, m10);
+  k.angle = ang;
+  kps[i] = k;
+  const float cs = cosf(ang), sn = sinf(ang);
+  for (int w = 0; w < kOrbBits / 32; ++w) {
+    uint32_t bits = 0;
+    for (int j = 0; j < 32; ++j) {
+      const int4 q = pat[w * 32 + j];
+      const int ax = (int)rintf(q.x * cs - q.y * sn), ay = (int)rintf(q.x * sn + q.y * cs);
+      const int bx = (int)rintf(q.z * cs - q.w * sn), by = (int)rintf(q.z * sn + q.w * cs);
+      const float va = I[(size_t)(cy + ay) * P + cx + ax];
+      const float vb = I[(size_t)(cy + by) * P + cx + bx];
+      bits |= (va < vb ? 1u : 0u) << j;
+    }
+    desc[(size_t)i * (kOrbBits / 32) + w] = bits;
+  }
+}
+
+// Brute-force Hamming 2-NN of every query descriptor against all train descriptors.
+__global__ void ka_match2(const uint32_t *__restrict__ q, int nq, const uint32_t *__restrict__ t,
+                          int nt, int2 *__restrict__ best, int2 *__restrict__ dist) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  uint32_t d[8];
+#pragma unroll
+  for (int w = 0; w < 8; ++w) d[w] = q[(size_t)i * 8 + w];
+  int b0 = -1, b1 = -1, d0 = 1 << 30, d1 = 1 << 30;
+  for (int j = 0; j < nt; ++j) {
+    int h = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) h += __popc(d[w] ^ t[(size_t)j * 8 + w]);
+    if (h < d0) {
+      d1 = d0;
+      b1 = b0;
+      d0 = h;
+      b0 = j;
+    } else if (h < d1) {
+      d1 = h;
+      b1 = j;
+    }
+  }
+  best[i] = make_int2(b0, b1);
+  dist[i] = make_int2(d0, d1);
+}
+
+// cv::cuda::warpAffine(src, dst, M, dsize, INTER_LINEAR, BORDER_CONSTANT 0): dst(x, y) =
+// src(iM (x, y, 1)) with iM = the inverse of M (float coefficients), bilinear taps
+// (cuda LinearFilter form) with out-of-image taps 0.
+__device__ __forceinline__ float affine_sample(const float *__restrict__ src, int sw, int sh,
+                                               size_t sp, float xs, float ys) {
+  const float x1f = floorf(xs), y1f = floorf(ys);
+  const int x1 = (int)x1f, y1 = (int)y1f, x2 = x1 + 1, y2 = y1 + 1;
+  auto at = [&](int yy, int xx) -> float {
+    return (xx >= 0 && yy >= 0 && xx < sw && yy < sh) ? src[(size_t)yy * sp + xx] : 0.0f;
+  };
+  float out = 0.0f;
+  out = out + at(y1, x1) * (((float)x2 - xs) * ((float)y2 - ys));
+  out = out + at(y1, x2) * ((xs - (float)x1) * ((float)y2 - ys));
+  out = out + at(y2, x1) * (((float)x2 - xs) * (ys - (float)y1));
+  out = out + at(y2, x2) * ((xs - (float)x1) * (ys - (float)y1));
+  return out;
+}
+
+struct Affine {
+  float m[6];   // the inverse transform, row-major 2x3
+};
+
+__global__ void ka_warp_u8(const uint8_t *__restrict__ src, size_t sp, int sw, int sh,
+                           uint8_t *__restrict__ dst, size_t dp, int dw, int dh, Affine iM) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= dw || y >= dh) return;
+  const float xs = iM.m[0] * x + iM.m[1] * y + iM.m[2];
+  const float ys = iM.m[3] * x + iM.m[4] * y + iM.m[5];
+  const float x1f = floorf(xs), y1f = floorf(ys);
+  const int x1 = (int)x1f, y1 = (int)y1f, x2 = x1 + 1, y2 = y1 + 1;
+  auto at = [&](int yy, int xx) -> float {
+    return (xx >= 0 && yy >= 0 && xx < sw && yy < sh) ? (float)src[(size_t)yy * sp + xx] : 0.0f;
+  };
+  float out = 0.0f;
+  out = out + at(y1, x1) * (((float)x2 - xs) * ((float)y2 - ys));
+  out = out + at(y1, x2) * ((xs - (float)x1) * ((float)y2 - ys));
+  out = out + at(y2, x1) * (((float)x2 - xs) * (ys - (float)y1));
+  out = out + at(y2, x2) * ((xs - (float)x1) * (ys - (float)y1));
+  dst[(size_t)y * dp + x] = (uint8_t)fminf(fmaxf(rintf(out), 0.0f), 255.0f);
+}
+
+// solve_wrapper's features branch (optflow.cpp:411-443, 468-473) on a flow ROI: map =
+// flow + grid, warped by the affine (the map planes staged in m1/m2), then flow = warped -
+// grid (output_type "flow") or the warped map, and 0 where I1 <= 1.  Two launches: stage,
+// then warp (a px reads other px of the staged map).
+__global__ void ka_map_stage(const float *__restrict__ u, const float *__restrict__ v, size_t fp,
+                             int W, int H, float *__restrict__ m1, float *__restrict__ m2) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const float *ur = reinterpret_cast<const float *>(reinterpret_cast<const char *>(u) + (size_t)y * fp);
+  const float *vr = reinterpret_cast<const float *>(reinterpret_cast<const char *>(v) + (size_t)y * fp);
+  m1[(size_t)y * W + x] = ur[x] + (float)x;
+  m2[(size_t)y * W + x] = vr[x] + (float)y;
+}
+__global__ void ka_map_warp(const float *__restrict__ m1, const float *__restrict__ m2, int W, int H,
+                            Affine iM, int flow_out, const uint8_t *__restrict__ I1, size_t p1,
+                            float *__restrict__ u, float *__restrict__ v, size_t fp) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const float xs = iM.m[0] * x + iM.m[1] * y + iM.m[2];
+  const float ys = iM.m[3] * x + iM.m[4] * y + iM.m[5];
+  float a = affine_sample(m1, W, H, W, xs, ys);
+  float b = affine_sample(m2, W, H, W, xs, ys);
+  if (flow_out) {
+    a = a - (float)x;
+    b = b - (float)y;
+  }
+  if (I1[(size_t)y * p1 + x] <= 1) a = b = 0.0f;
+  reinterpret_cast<float *>(reinterpret_cast<char *>(u) + (size_t)y * fp)[x] = a;
+  reinterpret_cast<float *>(reinterpret_cast<char *>(v) + (size_t)y * fp)[x] = b;
+}
+
+// ---------------------------------------------------------------- host: homography
+struct Pt {
+  double x, y;
+};
+
+// normalised DLT of a homography from n >= 4 correspondences (a -> b); false if degenerate
+static bool dlt_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, double H[9]) {
+  const size_t n = a.size();
+  if (n < 4) return false;
+  auto norm = [](const std::vector<Pt> &p, double T[9]) {
+    double mx = 0, my = 0;
+    for (auto &q : p) mx += q.x, my += q.y;
+    mx /= p.size();
+    my /= p.size();
+    double d = 0;
+    for (auto &q : p) d += std::hypot(q.x - mx, q.y - my);
+    d /= p.size();
+    const double s = d > 0 ? std::sqrt(2.0) / d : 1.0;
+    const double t[9] = {s, 0, -s * mx, 0, s, -s * my, 0, 0, 1};
+    std::copy(t, t + 9, T);
+  };
+  double Ta[9], Tb[9];
+  norm(a, Ta);
+  norm(b, Tb);
+  // normal equations of A h = 0 with h8 = 1 (8 unknowns), least squares
+  double M[8][9] = {};
+  for (size_t i = 0; i < n; ++i) {
+    const double x = Ta[0] * a[i].x + Ta[2], y = Ta[4] * a[i].y + Ta[5];
+    const double u = Tb[0] * b[i].x + Tb[2], w = Tb[4] * b[i].y + Tb[5];
+    const double r1[9] = {x, y, 1, 0, 0, 0, -u * x, -u * y, u};
+    const double r2[9] = {0, 0, 0, x, y, 1, -w * x, -w * y, w};
+    for (int j = 0; j < 8; ++j)
+      for (int k = 0; k < 9; ++k) M[j][k] += r1[j] * r1[k] + r2[j] * r2[k];
+  }
+  for (int c = 0; c < 8; ++c) {   // Gaussian elimination with partial pivoting
+    int p = c;
+    for (int r = c + 1; r < 8; ++r)
+      if (std::fabs(M[r][c]) > std::fabs(M[p][c])) p = r;
+    if (std::fabs(M[p][c]) < 1e-12) return false;
+    for (int k = 0; k < 9; ++k) std::swap(M[c][k], M[p][k]);
+    for (int r = 0; r < 8; ++r) {
+      if (r == c) continue;
+      const double f = M[r][c] / M[c][c];
+      for (int k = c; k < 9; ++k) M[r][k] -= f * M[c][k];
+    }
+  }
+  double Hn[9];
+  for (int j = 0; j < 8; ++j) Hn[j] = M[j][8] / M[j][j];
+  Hn[8] = 1.0;
+  // H = Tb^-1 Hn Ta
+  const double sb = Tb[0];
+  const double Tbi[9] = {1 / sb, 0, -Tb[2] / sb, 0, 1 / sb, -Tb[5] / sb, 0, 0, 1};
+  double T1[9] = {};
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < 3; ++k) T1[r * 3 + c] += Hn[r * 3 + k] * Ta[k * 3 + c];
+  for (int r = 0; r < 9; ++r) H[r] = 0;
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < 3; ++k) H[r * 3 + c] += Tbi[r * 3 + k] * T1[k * 3 + c];
+  if (std::fabs(H[8]) < 1e-15) return false;
+  for (int r = 0; r < 9; ++r) H[r] /= H[8];
+  return std::isfinite(H[0]) && std::isfinite(H[4]);
+}
+
+static inline double reproj_err2(const double H[9], const Pt &a, const Pt &b) {
+  const double w = H[6] * a.x + H[7] * a.y + H[8];
+  const double x = (H[0] * a.x + H[1] * a.y + H[2]) / w, y = (H[3] * a.x + H[4] * a.y + H[5]) / w;
+  return (x - b.x) * (x - b.x) + (y - b.y) * (y - b.y);
+}
+
+// cv::findHomography(src, dst, method, ransacReprojThreshold) restated: RANSAC (8) or LMEDS
+// (4), <= 2000 iterations with the 0.995-confidence stopping rule, refit on the inliers.
+// Deterministic (fixed seed).  Returns false when no model is found.
+static bool find_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, int method,
+                            double thresh, double H[9]) {
+  const int n = (int)a.size();
+  if (n < 4) return false;
+  std::mt19937 rng(0x12345678u);
+  std::uniform_int_distribution<int> pick(0, n - 1);
+  const bool lmeds = method == 4;
+  const double t2 = thresh * thresh;
+  double best[9];
+  int best_in = -1;
+  double best_med = 1e300;
+  int iters = 2000;
+  for (int it = 0; it < iters; ++it) {
+    int s[4];
+    for (int k = 0; k < 4; ++k) {
+      bool dup;
+      do {
+        s[k] = pick(rng);
+        dup = false;
+        for (int j = 0; j < k; ++j) dup |= s[j] == s[k];
+      } while (dup);
+    }
+    std::vector<Pt> sa = {a[s[0]], a[s[1]], a[s[2]], a[s[3]]}, sb = {b[s[0]], b[s[1]], b[s[2]], b[s[3]]};
+    double h[9];
+    if (!dlt_homography(sa, sb, h)) continue;
+    if (lmeds) {
+      std::vector<double> e(n);
+      for (int i = 0; i < n; ++i) e[i] = reproj_err2(h, a[i], b[i]);
+      std::nth_element(e.begin(), e.begin() + n / 2, e.end());
+      if (e[n / 2] < best_med) {
+        best_med = e[n / 2];
+        std::copy(h, h + 9, best);
+      }
+    } else {
+      int in = 0;
+      for (int i = 0; i < n; ++i) in += reproj_err2(h, a[i], b[i]) <= t2;
+      if (in > best_in) {
+        best_in = in;
+        std::copy(h, h + 9, best);
+        const double ratio = (double)in / n;   // RANSACUpdateNumIters, confidence 0.995
+        const double denom = std::log(1.0 - std::pow(ratio, 4));
+        if (denom < 0) iters = std::min(iters, (int)std::ceil(std::log(1 - 0.995) / denom));
+      }
+    }
+  }
+  if (!lmeds && best_in < 4) return false;
+  if (lmeds && best_med >= 1e300) return false;
+  // inliers of the best hypothesis, then a least-squares refit
+  const double lt2 = lmeds ? 2.5 * 2.5 * 1.4826 * 1.4826 * (1 + 5.0 / std::max(1, n - 4)) * best_med : t2;
+  std::vector<Pt> ia, ib;
+  for (int i = 0; i < n; ++i)
+    if (reproj_err2(best, a[i], b[i]) <= lt2) {
+      ia.push_back(a[i]);
+      ib.push_back(b[i]);
+    }
+  double h[9];
+  if (ia.size() >= 4 && dlt_homography(ia, ib, h)) std::copy(h, h + 9, best);
+  std::copy(best, best + 9, H);
+  return true;
+}
+
+// ORB's fixed test pattern stand-in: 256 point pairs in the 31x31 patch, isotropic Gaussian
+// (sigma = patch / 5) clipped to the disc that stays inside the patch under rotation.
+static std::vector<int> orb_pattern() {
+  std::mt19937 rng(0x0B5EEDu);
+  std::normal_distribution<double> g(0.0, kOrbPatch / 5.0);
+  std::vector<int> p;
+  p.reserve(kOrbBits * 4);
+  while ((int)p.size() < kOrbBits * 4) {
+    const int x = (int)std::lround(g(rng)), y = (int)std::lround(g(rng));
+    if (x * x + y * y > 13 * 13) continue;   // |rotated offset| <= 13 < 15
+    p.push_back(x);
+    p.push_back(y);
+  }
+  return p;
+}
+
+}  // namespace tvl1k

@@ -20,6 +20,7 @@
 #include "../../include/tvl1.h"
 #include "tvl1_kernels.hpp"
 #include "tvl1_batch.hpp"
+#include "tvl1_align.hpp"
 
 using namespace tvl1k;
 
@@ -108,6 +109,8 @@ struct tvl1_ctx {
   int batch_tb = 0;                     // TVL1_BATCH_TB=1: blocked regions for batch passes
   int batch_warp = 0;                   // TVL1_BATCH_WARP=1: per-px global gather (kb_warp)
   int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
+  float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
+  size_t map_bytes = 0;
   int bnblk = 0;                        // partials per pair
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
@@ -1491,6 +1494,135 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
   return TVL1_OK;
 }
 
+
+// ---------------------------------------------------------------- feature pre-alignment
+// find_alignment (features.cpp:46-167) on the GPU + host (tvl1_align.hpp).
+namespace {
+struct OrbSet {
+  std::vector<OrbKp> kps;     // level coordinates
+  std::vector<Pt> pts;        // level-0 coordinates
+  uint32_t *desc = nullptr;   // device, 8 words per keypoint
+};
+
+static tvl1_status orb_detect(tvl1_ctx *c, const uint8_t *img, size_t pitch, int W, int H,
+                              const tvl1_align_params &ap, const int4 *dpat, OrbSet &out,
+                              hipStream_t st) {
+  const int L = std::max(1, ap.nlevels);
+  const double sf = ap.scale_factor;
+  std::vector<int> lw(L), lh(L), lp(L);
+  std::vector<float *> lev(L, nullptr);
+  for (int l = 0; l < L; ++l) {
+    const double scale = 1.0 / std::pow(sf, l - ap.first_level);
+    lw[l] = l == 0 ? W : std::max(1, (int)std::lrint(W * scale));
+    lh[l] = l == 0 ? H : std::max(1, (int)std::lrint(H * scale));
+    lp[l] = (int)align_up((size_t)lw[l], 64);
+  }
+  std::vector<void *> owned;
+  auto alloc = [&](size_t bytes) -> void * {
+    void *p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(bytes, 256)) != hipSuccess) return nullptr;
+    owned.push_back(p);
+    return p;
+  };
+  auto cleanup = [&]() {
+    for (void *p : owned) (void)hipFree(p);
+  };
+  for (int l = 0; l < L; ++l) {
+    lev[l] = (float *)alloc((size_t)lp[l] * lh[l] * sizeof(float));
+    if (!lev[l]) { cleanup(); return set_err(c, TVL1_ENOMEM, "alignment: level allocation failed"); }
+  }
+  hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 1), kBlk2, 0, st, img, pitch, img, pitch, lev[0],
+                     lev[0], W, H, lp[0]);
+  for (int l = 1; l < L; ++l)
+    hipLaunchKernelGGL(k_resize_hp, grid2(lw[l], lh[l], 1), kBlk2, 0, st, lev[l - 1], nullptr,
+                       nullptr, lw[l - 1], lh[l - 1], lp[l - 1], lev[l], nullptr, nullptr, lw[l],
+                       lh[l], lp[l], (double)lw[l - 1] / lw[l], (double)lh[l - 1] / lh[l], 0, 0,
+                       1.0f);
+  // ORB's per-level quota (ORB_Impl::detectAndCompute: nfeatures * (1 - f) / (1 - f^L) f^l)
+  std::vector<int> quota(L, 0);
+  {
+    const double f = 1.0 / sf;
+    double nd = ap.nfeatures * (1 - f) / (1 - std::pow(f, L));
+    int sum = 0;
+    for (int l = 0; l < L - 1; ++l) {
+      quota[l] = (int)std::lrint(nd);
+      sum += quota[l];
+      nd *= f;
+    }
+    quota[L - 1] = std::max(ap.nfeatures - sum, 0);
+  }
+  const int border = std::max(ap.edge_threshold, kOrbHalf + 1);
+  float *score = (float *)alloc((size_t)W * H * sizeof(float));
+  const unsigned cap = 1u << 20;
+  OrbCand *cand = (OrbCand *)alloc(cap * sizeof(OrbCand));
+  unsigned *cnt = (unsigned *)alloc(sizeof(unsigned));
+  if (!score || !cand || !cnt) { cleanup(); return set_err(c, TVL1_ENOMEM, "alignment: scratch allocation failed"); }
+  std::vector<OrbCand> host;
+  for (int l = 0; l < L; ++l) {
+    if (lw[l] <= 2 * border || lh[l] <= 2 * border || quota[l] == 0) continue;
+    hipLaunchKernelGGL(ka_fast_harris, grid2(lw[l], lh[l]), kBlk2, 0, st, lev[l], lw[l], lh[l],
+                       lp[l], border, (float)ap.fast_threshold, score);
+    HIP_TRY(c, hipMemsetAsync(cnt, 0, sizeof(unsigned), st));
+    hipLaunchKernelGGL(ka_nms, grid2(lw[l], lh[l]), kBlk2, 0, st, score, lw[l], lh[l], cand, cnt, cap);
+    unsigned n = 0;
+    HIP_TRY(c, hipMemcpyAsync(&n, cnt, sizeof n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    n = std::min(n, cap);
+    host.resize(n);
+    if (n) HIP_TRY(c, hipMemcpy(host.data(), cand, n * sizeof(OrbCand), hipMemcpyDeviceToHost));
+    // KeyPointsFilter::retainBest: the quota's best responses (ties by position: deterministic)
+    std::sort(host.begin(), host.end(), [](const OrbCand &a, const OrbCand &b) {
+      return a.score != b.score ? a.score > b.score : (a.y != b.y ? a.y < b.y : a.x < b.x);
+    });
+    const double scale = std::pow(sf, l - ap.first_level);
+    for (unsigned i = 0; i < std::min<unsigned>(n, (unsigned)quota[l]); ++i) {
+      out.kps.push_back(OrbKp{host[i].x, host[i].y, 0.0f, l});
+      out.pts.push_back(Pt{host[i].x * scale, host[i].y * scale});
+    }
+  }
+  if (ap.blur_for_descriptor) {
+    for (int l = 0; l < L; ++l) {
+      float *b = (float *)alloc((size_t)lp[l] * lh[l] * sizeof(float));
+      if (!b) { cleanup(); return set_err(c, TVL1_ENOMEM, "alignment: blur allocation failed"); }
+      hipLaunchKernelGGL(ka_blur7, grid2(lw[l], lh[l]), kBlk2, 0, st, lev[l], lw[l], lh[l], lp[l], b);
+      lev[l] = b;
+    }
+  }
+  const int nk = (int)out.kps.size();
+  if (nk > 0) {
+    OrbKp *dk = (OrbKp *)alloc(nk * sizeof(OrbKp));
+    float **dlev = (float **)alloc(L * sizeof(float *));
+    int *dlp = (int *)alloc(L * sizeof(int));
+    if (hipMalloc((void **)&out.desc, (size_t)nk * 32) != hipSuccess || !dk || !dlev || !dlp) {
+      cleanup();
+      return set_err(c, TVL1_ENOMEM, "alignment: descriptor allocation failed");
+    }
+    HIP_TRY(c, hipMemcpyAsync(dk, out.kps.data(), nk * sizeof(OrbKp), hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(dlev, lev.data(), L * sizeof(float *), hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(dlp, lp.data(), L * sizeof(int), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(ka_describe, dim3((nk + 127) / 128), dim3(128), 0, st,
+                       (const float *const *)dlev, dlp, dk, nk, dpat, out.desc);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(st));
+  }
+  cleanup();
+  return TVL1_OK;
+}
+
+static void affine_inverse(const float M[6], Affine &iM) {
+  const double a = M[0], b = M[1], cc = M[2], d = M[3], e = M[4], f = M[5];
+  double D = a * e - b * d;
+  D = D != 0 ? 1.0 / D : 0.0;
+  const double A11 = e * D, A22 = a * D, A12 = -b * D, A21 = -d * D;
+  iM.m[0] = (float)A11;
+  iM.m[1] = (float)A12;
+  iM.m[2] = (float)(-A11 * cc - A12 * f);
+  iM.m[3] = (float)A21;
+  iM.m[4] = (float)A22;
+  iM.m[5] = (float)(-A21 * cc - A22 * f);
+}
+}  // namespace
+
 extern "C" {
 
 void tvl1_params_default(tvl1_params *p) {
@@ -1712,6 +1844,144 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pi
   return TVL1_OK;
 }
 
+
+void tvl1_align_params_default(tvl1_align_params *p) {
+  if (!p) return;
+  // orb_defaults (features.cpp:19-31), the ratio test (:109), findHomography (:133)
+  p->nfeatures = 5000;
+  p->scale_factor = 1.2f;
+  p->nlevels = 8;
+  p->edge_threshold = 31;
+  p->first_level = 0;
+  p->wta_k = 2;
+  p->patch_size = 31;
+  p->fast_threshold = 20;
+  p->blur_for_descriptor = 0;
+  p->ratio = 0.8f;
+  p->method = 8;   // cv::RANSAC
+  p->ransac_threshold = 5.0;
+}
+
+tvl1_status tvl1_find_alignment(tvl1_ctx *c, const uint8_t *frame1, size_t pitch1, int32_t w1,
+                                int32_t h1, const uint8_t *frame0, size_t pitch0, int32_t w0,
+                                int32_t h0, const tvl1_align_params *ap, float affine[6],
+                                int32_t *n_good, int32_t *outcome, void *stream) {
+  if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  if (!frame1 || !frame0 || !ap || !affine) return set_err(c, TVL1_EINVAL, "null argument");
+  if (w1 <= 0 || h1 <= 0 || w0 <= 0 || h0 <= 0) return set_err(c, TVL1_ESIZE, "bad frame size");
+  if (ap->nlevels <= 0 || !(ap->scale_factor > 1.0f) || ap->nfeatures <= 0)
+    return set_err(c, TVL1_EINVAL, "bad ORB parameters");
+  if (ap->wta_k != 2 || ap->patch_size != 31)
+    return set_err(c, TVL1_EINVAL, "only WTA_K = 2 and patchSize = 31 are supported");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  static const std::vector<int> pat = orb_pattern();
+  int4 *dpat = nullptr;
+  HIP_TRY(c, hipMalloc((void **)&dpat, pat.size() * sizeof(int)));
+  HIP_TRY(c, hipMemcpy(dpat, pat.data(), pat.size() * sizeof(int), hipMemcpyHostToDevice));
+  OrbSet q, t;   // query = frame1, train = frame0 (find_alignment(frame1_GPU, frame0_GPU))
+  tvl1_status s = orb_detect(c, frame1, pitch1, w1, h1, *ap, dpat, q, st);
+  if (s == TVL1_OK) s = orb_detect(c, frame0, pitch0, w0, h0, *ap, dpat, t, st);
+  (void)hipFree(dpat);
+  std::vector<int2> best, dist;
+  const int nq = (int)q.kps.size(), nt = (int)t.kps.size();
+  if (s == TVL1_OK && nq > 0 && nt > 0) {
+    int2 *db = nullptr, *dd = nullptr;
+    if (hipMalloc((void **)&db, nq * sizeof(int2)) != hipSuccess ||
+        hipMalloc((void **)&dd, nq * sizeof(int2)) != hipSuccess) {
+      s = set_err(c, TVL1_ENOMEM, "alignment: match allocation failed");
+    } else {
+      hipLaunchKernelGGL(ka_match2, dim3((nq + 127) / 128), dim3(128), 0, st, q.desc, nq, t.desc,
+                         nt, db, dd);
+      best.resize(nq);
+      dist.resize(nq);
+      if (hipMemcpyAsync(best.data(), db, nq * sizeof(int2), hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipMemcpyAsync(dist.data(), dd, nq * sizeof(int2), hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        s = set_err(c, TVL1_EHIP, "alignment: match download failed");
+    }
+    (void)hipFree(db);
+    (void)hipFree(dd);
+  }
+  if (q.desc) (void)hipFree(q.desc);
+  if (t.desc) (void)hipFree(t.desc);
+  if (s != TVL1_OK) return s;
+  // the ratio test over the first min(train rows - 1, queries) queries (features.cpp:105-112)
+  struct Good {
+    int qi, ti, d;
+  };
+  std::vector<Good> good;
+  for (int i = 0; i < std::min(nt - 1, nq); ++i)
+    if (best[i].y >= 0 && dist[i].x < ap->ratio * dist[i].y) good.push_back(Good{i, best[i].x, dist[i].x});
+  std::stable_sort(good.begin(), good.end(), [](const Good &a, const Good &b) { return a.d < b.d; });
+  if (n_good) *n_good = (int32_t)good.size();
+  const float ident[6] = {1, 0, 0, 0, 1, 0};
+  int oc = 0;
+  if (good.size() > 10) {
+    std::vector<Pt> p0, p1;
+    for (auto &g : good) {
+      p0.push_back(q.pts[g.qi]);
+      p1.push_back(t.pts[g.ti]);
+    }
+    double H[9];
+    const bool ok = find_homography(p0, p1, ap->method, ap->ransac_threshold, H);
+    if (!ok || std::fabs(1 - H[0]) > 0.20 || std::fabs(1 - H[4]) > 0.20) {
+      std::copy(ident, ident + 6, affine);
+      oc = 2;
+    } else {
+      for (int k = 0; k < 6; ++k) affine[k] = (float)H[k];
+    }
+  } else {
+    std::copy(ident, ident + 6, affine);
+    oc = 1;
+  }
+  if (outcome) *outcome = oc;
+  return TVL1_OK;
+}
+
+tvl1_status tvl1_warp_affine_u8(tvl1_ctx *c, const uint8_t *src, size_t sp, int32_t sw, int32_t sh,
+                                uint8_t *dst, size_t dp, int32_t dw, int32_t dh,
+                                const float affine[6], void *stream) {
+  if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  if (!src || !dst || !affine) return set_err(c, TVL1_EINVAL, "null argument");
+  if (sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0) return set_err(c, TVL1_ESIZE, "bad size");
+  HIP_TRY(c, hipSetDevice(c->device));
+  Affine iM;
+  affine_inverse(affine, iM);
+  hipLaunchKernelGGL(ka_warp_u8, grid2(dw, dh), kBlk2, 0, (hipStream_t)stream, src, sp, sw, sh,
+                     dst, dp, dw, dh, iM);
+  HIP_TRY(c, hipGetLastError());
+  return TVL1_OK;
+}
+
+tvl1_status tvl1_postprocess_affine(tvl1_ctx *c, float *u, float *v, size_t fp, const uint8_t *I1,
+                                    size_t p1, int32_t W, int32_t H, int32_t flow_output,
+                                    const float affine[6], void *stream) {
+  if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  if (!u || !v || !I1 || !affine) return set_err(c, TVL1_EINVAL, "null argument");
+  if (W <= 0 || H <= 0) return set_err(c, TVL1_ESIZE, "bad size");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t need = 2 * (size_t)W * H * sizeof(float);
+  if (need > c->map_bytes) {
+    if (c->map_scratch) {
+      HIP_TRY(c, hipStreamSynchronize(st));
+      (void)hipFree(c->map_scratch);
+      c->map_scratch = nullptr;
+    }
+    HIP_TRY(c, hipMalloc((void **)&c->map_scratch, need));
+    c->map_bytes = need;
+  }
+  float *m1 = c->map_scratch, *m2 = c->map_scratch + (size_t)W * H;
+  Affine iM;
+  affine_inverse(affine, iM);
+  hipLaunchKernelGGL(ka_map_stage, grid2(W, H), kBlk2, 0, st, u, v, fp, W, H, m1, m2);
+  hipLaunchKernelGGL(ka_map_warp, grid2(W, H), kBlk2, 0, st, m1, m2, W, H, iM, flow_output ? 1 : 0,
+                     I1, p1, u, v, fp);
+  HIP_TRY(c, hipGetLastError());
+  return TVL1_OK;
+}
+
 tvl1_status tvl1_calc_host(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8_t *I1,
                            size_t pitch1, int32_t W, int32_t H, float *u, float *v,
                            size_t fpitch, tvl1_stats *stats) {
@@ -1764,6 +2034,7 @@ void tvl1_destroy(tvl1_ctx *c) {
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   if (c->arena) (void)hipFree(c->arena);
   if (c->barena) (void)hipFree(c->barena);
+  if (c->map_scratch) (void)hipFree(c->map_scratch);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->ev_check) (void)hipEventDestroy(c->ev_check);

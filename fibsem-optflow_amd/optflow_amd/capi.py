@@ -19,7 +19,7 @@ ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
 ORACLE_SO = REPO_ROOT / "oracle" / "liboracle_tvl1.so"
 
 TVL1_MAX_LEVELS = 32
-ABI_VERSION = 3          # TVL1_ABI_VERSION of include/tvl1.h
+ABI_VERSION = 4          # TVL1_ABI_VERSION of include/tvl1.h
 STATUS = {0: "TVL1_OK", 1: "TVL1_EINVAL", 2: "TVL1_ESIZE", 3: "TVL1_EHIP",
           4: "TVL1_ENOMEM", 5: "TVL1_ENODEV"}
 
@@ -60,6 +60,25 @@ class TVL1Stats(C.Structure):
         ("kernel_launches", C.c_int64 * 4),
         ("kernel_bytes", C.c_double * 4),
         ("kernel_hbm_bytes", C.c_double * 4),
+    ]
+
+
+class TVL1AlignParams(C.Structure):
+    """tvl1_align_params (include/tvl1.h): orb_defaults (features.cpp:19-31) + ratio / homo /
+    ransac (:109, :133)."""
+    _fields_ = [
+        ("nfeatures", C.c_int32),
+        ("scale_factor", C.c_float),
+        ("nlevels", C.c_int32),
+        ("edge_threshold", C.c_int32),
+        ("first_level", C.c_int32),
+        ("wta_k", C.c_int32),
+        ("patch_size", C.c_int32),
+        ("fast_threshold", C.c_int32),
+        ("blur_for_descriptor", C.c_int32),
+        ("ratio", C.c_float),
+        ("method", C.c_int32),
+        ("ransac_threshold", C.c_double),
     ]
 
 
@@ -164,6 +183,21 @@ def load_engine() -> C.CDLL:
                                     C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
                                     C.POINTER(TVL1Stats), C.c_void_p]
     lib.tvl1_calc_batch.restype = C.c_int
+    lib.tvl1_align_params_default.argtypes = [C.POINTER(TVL1AlignParams)]
+    lib.tvl1_align_params_default.restype = None
+    lib.tvl1_find_alignment.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
+                                        C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
+                                        C.POINTER(TVL1AlignParams), C.POINTER(C.c_float),
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_void_p]
+    lib.tvl1_find_alignment.restype = C.c_int
+    lib.tvl1_warp_affine_u8.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
+                                        C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
+                                        C.POINTER(C.c_float), C.c_void_p]
+    lib.tvl1_warp_affine_u8.restype = C.c_int
+    lib.tvl1_postprocess_affine.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                            C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
+                                            C.c_int32, C.POINTER(C.c_float), C.c_void_p]
+    lib.tvl1_postprocess_affine.restype = C.c_int
     lib.tvl1_calc_host.argtypes = [C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t,
                                    C.POINTER(C.c_uint8), C.c_size_t, C.c_int32, C.c_int32,
                                    C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_size_t,
@@ -309,6 +343,29 @@ class Engine:
                 L = out[b]["levels"]
                 out[b]["warp_iters"] = wis[b][: L * self.params.warps].reshape(L, self.params.warps)
         return out
+
+    def find_alignment(self, d1: int, pitch1: int, w1: int, h1: int, d0: int, pitch0: int,
+                       w0: int, h0: int, **kw):
+        """tvl1_find_alignment(frame1, frame0) on device frames -> (affine (2, 3), n_good,
+        outcome)."""
+        ap = TVL1AlignParams()
+        self.lib.tvl1_align_params_default(C.byref(ap))
+        for k, v in kw.items():
+            setattr(ap, k, v)
+        aff = (C.c_float * 6)()
+        ng, oc = C.c_int32(0), C.c_int32(0)
+        rc = self.lib.tvl1_find_alignment(self.ctx, C.c_void_p(d1), pitch1, w1, h1, C.c_void_p(d0),
+                                          pitch0, w0, h0, C.byref(ap), aff, C.byref(ng),
+                                          C.byref(oc), None)
+        self._check(rc, "tvl1_find_alignment")
+        return np.array(list(aff), np.float32).reshape(2, 3), int(ng.value), int(oc.value)
+
+    def warp_affine_u8(self, src: int, sp: int, sw: int, sh: int, dst: int, dp: int, dw: int,
+                       dh: int, affine) -> None:
+        a = (C.c_float * 6)(*[float(x) for x in np.asarray(affine, np.float32).ravel()])
+        self._check(self.lib.tvl1_warp_affine_u8(self.ctx, C.c_void_p(src), sp, sw, sh,
+                                                 C.c_void_p(dst), dp, dw, dh, a, None),
+                    "tvl1_warp_affine_u8")
 
     def close(self):
         if self.ctx:

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TVL1_ABI_VERSION 3
+#define TVL1_ABI_VERSION 4
 #define TVL1_MAX_LEVELS 32
 
 typedef enum tvl1_status {
@@ -153,6 +153,50 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *ctx, int32_t n,
                             int32_t width, int32_t height,
                             float *u, float *v, size_t flow_pitch, size_t flow_pair_stride,
                             tvl1_stats *stats, void *stream);
+
+/* ---- Feature pre-alignment (features.cpp:46-167, optflow.cpp:366-377) ----
+ * find_alignment(frame1, frame0): ORB keypoints and descriptors on the GPU, brute-force
+ * Hamming 2-NN + ratio test, RANSAC / LMEDS homography on the host; affine = its top 2x3
+ * (maps frame1 coordinates onto frame0), or the identity when <= 10 matches survive the
+ * ratio test (outcome 1) or the homography is missing or zooms by more than 20 % (outcome
+ * 2).  SURF (features = 2) is served by the ORB path.  Parity with OpenCV unpinned (see
+ * fibsem-optflow_amd/csrc/tvl1_align.hpp).  Inputs are device pointers; synchronous. */
+typedef struct tvl1_align_params {
+  int32_t nfeatures;           /* 5000 features.cpp:22 */
+  float scale_factor;          /* 1.2  :23 */
+  int32_t nlevels;             /* 8    :24 */
+  int32_t edge_threshold;      /* 31   :25 */
+  int32_t first_level;         /* 0    :26 */
+  int32_t wta_k;               /* 2    :27 (only 2 is supported) */
+  int32_t patch_size;          /* 31   :28 (only 31 is supported) */
+  int32_t fast_threshold;      /* 20   :29 */
+  int32_t blur_for_descriptor; /* 0    :30 */
+  float ratio;                 /* 0.8  :109 */
+  int32_t method;              /* homo: 8 = RANSAC (default, :133), 4 = LMEDS */
+  double ransac_threshold;     /* ransac: 5 (:133) */
+} tvl1_align_params;
+
+void tvl1_align_params_default(tvl1_align_params *p);
+
+tvl1_status tvl1_find_alignment(tvl1_ctx *ctx,
+                                const uint8_t *frame1, size_t pitch1, int32_t w1, int32_t h1,
+                                const uint8_t *frame0, size_t pitch0, int32_t w0, int32_t h0,
+                                const tvl1_align_params *params, float affine[6],
+                                int32_t *n_good, int32_t *outcome, void *stream);
+
+/* cv::cuda::warpAffine(src, dst, M, dsize, INTER_LINEAR, BORDER_CONSTANT, 0) on u8
+ * (optflow.cpp:370): dst(x, y) = src(M^-1 (x, y)).  Device pointers, async on stream. */
+tvl1_status tvl1_warp_affine_u8(tvl1_ctx *ctx, const uint8_t *src, size_t src_pitch,
+                                int32_t sw, int32_t sh, uint8_t *dst, size_t dst_pitch,
+                                int32_t dw, int32_t dh, const float affine[6], void *stream);
+
+/* solve_wrapper's features branch with the alignment's affine (optflow.cpp:411-443,
+ * 468-473): map = flow + grid, warpAffine(map, M), then flow = map' - grid (flow_output 1)
+ * or map' (0), and 0 where I1 <= 1.  Device pointers, async on stream. */
+tvl1_status tvl1_postprocess_affine(tvl1_ctx *ctx, float *u, float *v, size_t flow_pitch,
+                                    const uint8_t *I1, size_t pitch1, int32_t width,
+                                    int32_t height, int32_t flow_output, const float affine[6],
+                                    void *stream);
 
 /* Same on HOST memory: upload, solve, download, synchronize.
  * (GpuMat::upload optflow.cpp:315-316 ... download :475-476) */

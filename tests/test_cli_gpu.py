@@ -63,16 +63,42 @@ def test_flow_output_top_bottom_rois(tmp_path, pair):
 
 
 def test_map_output_default_roi(tmp_path, pair):
-    """No ROI -> 'default' full frame; the reference would pre-align (features); this
-    build uses the identity transform, so map = flow + grid (then masked)."""
+    """No ROI -> 'default' full frame -> pre-alignment (optflow.cpp:366-377).  ratio 0
+    leaves no match through the ratio test, so find_alignment falls back to the identity
+    (features.cpp:157-166) and the features branch gives map = flow + grid (then masked)."""
     I0, I1 = pair
-    cfg = {"output_dir": str(tmp_path), "scale": 1, "nscales": 3, "warps": 3,
+    cfg = {"output_dir": str(tmp_path), "scale": 1, "nscales": 3, "warps": 3, "ratio": 0.0,
            "images": [{"p": str(tmp_path / "p.png"), "q": str(tmp_path / "q.png"),
                        "output_name": "m"}]}
-    run_cli(cfg, tmp_path)
+    r = run_cli(cfg, tmp_path)
+    assert "Not enough matches. Using no transformation" in r.stdout
+    assert "reverting to features" in r.stderr
     u, v = oracle_post(I0, I1, capi.make_params(nscales=3, warps=3), 1)
     assert np.array_equal(tif(tmp_path / "m_1.00_x.tiff"), u)
     assert np.array_equal(tif(tmp_path / "m_1.00_y.tiff"), v)
+
+
+def test_size_mismatch_is_aligned(tmp_path, built):
+    """frame1 = frame0 inside a larger canvas at offset (dx, dy): the CLI aligns frame1 onto
+    frame0 (ORB + RANSAC, warpAffine), the flow between the aligned frames is ~0, and the
+    features branch maps it back through the affine: map_x(x, y) ~ x + dx, map_y ~ y + dy.
+    Approximate by construction (the homography is a fit): median within 0.25 px."""
+    h, w, dx, dy = 360, 480, 17, 11
+    f0 = np.clip(np.rint(synth.base_texture(w, h, seed=5)), 2, 255).astype(np.uint8)
+    f1 = np.zeros((h + 40, w + 40), np.uint8)
+    f1[dy:dy + h, dx:dx + w] = f0
+    Image.fromarray(f0).save(tmp_path / "a.png")
+    Image.fromarray(f1).save(tmp_path / "b.png")
+    cfg = {"output_dir": str(tmp_path), "scale": 1, "nscales": 3, "warps": 2, "features": 1,
+           "images": [{"p": str(tmp_path / "a.png"), "q": str(tmp_path / "b.png"),
+                       "output_name": "al"}]}
+    r = run_cli(cfg, tmp_path)
+    assert "Not enough matches" not in r.stdout and "twenty percent" not in r.stdout
+    mx, my = tif(tmp_path / "al_1.00_x.tiff"), tif(tmp_path / "al_1.00_y.tiff")
+    assert mx.shape == (h, w)
+    ys, xs = np.mgrid[20:h - 40, 20:w - 40]
+    assert abs(np.median(mx[20:h - 40, 20:w - 40] - xs) - dx) < 0.25
+    assert abs(np.median(my[20:h - 40, 20:w - 40] - ys) - dy) < 0.25
 
 
 def test_prescale_half(tmp_path, pair):
