@@ -36,55 +36,78 @@ constexpr int kOrbPatch = 31, kOrbHalf = 15, kOrbBits = 256;
 
 // FAST-9 on a float level image (values 0..255) at px (x, y): a contiguous arc of >= 9 of
 // the 16 radius-3 circle px all brighter than c + t or all darker than c - t.
-__constant__ int kFastDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-__constant__ int kFastDy[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
+constexpr int kFastDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+constexpr int kFastDy[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
 
-__global__ void ka_fast_harris(const float *__restrict__ I, int W, int H, int P, int border,
-                               float t, float *__restrict__ score) {
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  if (x >= W || y >= H) return;
-  float out = 0.0f;
-  if (x >= border && y >= border && x < W - border && y < H - border) {
-    const float c = I[(size_t)y * P + x];
-    unsigned bright = 0, dark = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const float v = I[(size_t)(y + kFastDy[k]) * P + x + kFastDx[k]];
-      bright |= (v > c + t ? 1u : 0u) << k;
-      dark |= (v < c - t ? 1u : 0u) << k;
-    }
-    auto arc9 = [](unsigned m) {
-      const unsigned mm = m | (m << 16);   // wrap around the circle
-      unsigned run = mm;
-#pragma unroll
-      for (int k = 1; k < 9; ++k) run &= mm >> k;
-      return run != 0;
-    };
-    if (arc9(bright) || arc9(dark)) {
-      // Harris response over a 7x7 window of Sobel gradients (scaled to 0..1 intensities)
-      float a = 0.f, b = 0.f, cc = 0.f;
-      for (int dy = -3; dy <= 3; ++dy)
-        for (int dx = -3; dx <= 3; ++dx) {
-          const int yy = y + dy, xx = x + dx;
-          const float *r0 = I + (size_t)(yy - 1) * P, *r1 = I + (size_t)yy * P,
-                      *r2 = I + (size_t)(yy + 1) * P;
-          const float gx = (r0[xx + 1] - r0[xx - 1]) + 2.f * (r1[xx + 1] - r1[xx - 1]) +
-                           (r2[xx + 1] - r2[xx - 1]);
-          const float gy = (r2[xx - 1] - r0[xx - 1]) + 2.f * (r2[xx] - r0[xx]) +
-                           (r2[xx + 1] - r0[xx + 1]);
-          a += gx * gx;
-          b += gy * gy;
-          cc += gx * gy;
-        }
-      const float s = 1.0f / (4.f * 255.f * 49.f);
-      a *= s * s;
-      b *= s * s;
-      cc *= s * s;
-      out = fmaxf(a * b - cc * cc - 0.04f * (a + b) * (a + b), 1e-30f);
-    }
+// Block = 64 x 16 px (4 wavefronts x 4 rows).  The image tile with a 4-px apron and the
+// Sobel gradients of the 70 x 22 window positions are staged in LDS, so a corner's 7 x 7
+// Harris sum reads LDS instead of ~400 scattered global loads.  Same expressions in the same
+// order as a direct evaluation: the scores do not depend on the tiling.
+constexpr int kFhW = 64, kFhH = 16, kFhTW = kFhW + 8, kFhTH = kFhH + 8;
+constexpr int kFhGW = kFhW + 6, kFhGH = kFhH + 6;
+__global__ void __launch_bounds__(256) ka_fast_harris(const float *__restrict__ I, int W, int H,
+                                                      int P, int border, float t,
+                                                      float *__restrict__ score) {
+  __shared__ float img[kFhTH][kFhTW];
+  __shared__ float gxs[kFhGH][kFhGW], gys[kFhGH][kFhGW];
+  const int x0 = blockIdx.x * kFhW, y0 = blockIdx.y * kFhH;
+  for (int i = threadIdx.x; i < kFhTW * kFhTH; i += 256) {
+    const int ty = i / kFhTW, tx = i - ty * kFhTW;
+    const int yy = imin(imax(y0 - 4 + ty, 0), H - 1), xx = imin(imax(x0 - 4 + tx, 0), W - 1);
+    img[ty][tx] = I[(size_t)yy * P + xx];
   }
-  score[(size_t)y * W + x] = out;
+  __syncthreads();
+  for (int i = threadIdx.x; i < kFhGW * kFhGH; i += 256) {
+    const int gy = i / kFhGW, gx = i - gy * kFhGW;
+    const int ty = gy + 1, tx = gx + 1;   // gradient position (x0-3+gx, y0-3+gy) in the tile
+    const float *r0 = img[ty - 1], *r1 = img[ty], *r2 = img[ty + 1];
+    gxs[gy][gx] = (r0[tx + 1] - r0[tx - 1]) + 2.f * (r1[tx + 1] - r1[tx - 1]) +
+                  (r2[tx + 1] - r2[tx - 1]);
+    gys[gy][gx] = (r2[tx - 1] - r0[tx - 1]) + 2.f * (r2[tx] - r0[tx]) + (r2[tx + 1] - r0[tx + 1]);
+  }
+  __syncthreads();
+  const int lx = threadIdx.x & 63;
+  const int x = x0 + lx;
+  for (int ly = threadIdx.x >> 6; ly < kFhH; ly += 4) {
+    const int y = y0 + ly;
+    if (x >= W || y >= H) continue;
+    float out = 0.0f;
+    if (x >= border && y >= border && x < W - border && y < H - border) {
+      const float c = img[ly + 4][lx + 4];
+      unsigned bright = 0, dark = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float v = img[ly + 4 + kFastDy[k]][lx + 4 + kFastDx[k]];
+        bright |= (v > c + t ? 1u : 0u) << k;
+        dark |= (v < c - t ? 1u : 0u) << k;
+      }
+      auto arc9 = [](unsigned m) {
+        const unsigned mm = m | (m << 16);   // wrap around the circle
+        unsigned run = mm;
+#pragma unroll
+        for (int k = 1; k < 9; ++k) run &= mm >> k;
+        return run != 0;
+      };
+      if (arc9(bright) || arc9(dark)) {
+        // Harris response over a 7x7 window of Sobel gradients (scaled to 0..1 intensities)
+        float a = 0.f, b = 0.f, cc = 0.f;
+        for (int dy = -3; dy <= 3; ++dy)
+          for (int dx = -3; dx <= 3; ++dx) {
+            const float gx = gxs[ly + 3 + dy][lx + 3 + dx];
+            const float gy = gys[ly + 3 + dy][lx + 3 + dx];
+            a += gx * gx;
+            b += gy * gy;
+            cc += gx * gy;
+          }
+        const float s = 1.0f / (4.f * 255.f * 49.f);
+        a *= s * s;
+        b *= s * s;
+        cc *= s * s;
+        out = fmaxf(a * b - cc * cc - 0.04f * (a + b) * (a + b), 1e-30f);
+      }
+    }
+    score[(size_t)y * W + x] = out;
+  }
 }
 
 // blurForDescriptor: 7x7 Gaussian, sigma 2 (ORB's GaussianBlur before the descriptors)
@@ -104,27 +127,111 @@ __global__ void ka_blur7(const float *__restrict__ I, int W, int H, int P, float
   O[(size_t)y * P + x] = s;
 }
 
-struct OrbCand {
-  float x, y, score;
-};
+// 3x3 non-maximum suppression of the corner scores.  A survivor is appended to its level's
+// key list as the unique 64-bit key (score bits << 32) | ~(y * W + x): positive float bits
+// order like the scores, and equal scores order by position (top-left first), so "the best
+// quota keys" is one well-defined set whatever order the atomics append in.  No two
+// survivors are neighbours (ties go to the top-left one), so a level has at most
+// ceil(W/2) * ceil(H/2) of them: cap is that bound and nothing is ever dropped.
+// A block covers a 64 x kNmsRows tile: its survivors are gathered in LDS (at most one per
+// 2 x 2 px) and claimed with ONE global atomic per block -- same-address atomics are
+// serialised at the L2, so one per survivor (~10^5 per level) cost a millisecond a level.
+constexpr int kNmsRows = 64;
+__global__ void __launch_bounds__(256) ka_nms(const float *__restrict__ score, int W, int H,
+                                              uint64_t *__restrict__ keys,
+                                              unsigned *__restrict__ count, unsigned cap) {
+  __shared__ uint64_t lk[32 * (kNmsRows / 2)];
+  __shared__ unsigned ln, lbase;
+  const int tx = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) ln = 0;
+  __syncthreads();
+  const int x = blockIdx.x * 64 + tx;
+  for (int r = wv; r < kNmsRows; r += 4) {
+    const int y = blockIdx.y * kNmsRows + r;
+    if (x < 1 || y < 1 || x >= W - 1 || y >= H - 1) continue;
+    const float s = score[(size_t)y * W + x];
+    bool keep = s > 0.0f;
+    for (int dy = -1; dy <= 1 && keep; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (!dx && !dy) continue;
+        const float o = score[(size_t)(y + dy) * W + x + dx];
+        // ties broken by position so exactly one of two equal neighbours survives
+        if (o > s || (o == s && (dy < 0 || (dy == 0 && dx < 0)))) keep = false;
+      }
+    if (keep)
+      lk[atomicAdd(&ln, 1u)] =
+          ((uint64_t)__float_as_uint(s) << 32) | (uint64_t)(0xFFFFFFFFu - (unsigned)(y * W + x));
+  }
+  __syncthreads();
+  const unsigned n = ln;
+  if (n == 0) return;
+  if (threadIdx.x == 0) lbase = atomicAdd(count, n);
+  __syncthreads();
+  for (unsigned i = threadIdx.x; i < n; i += 256)
+    if (lbase + i < cap) keys[lbase + i] = lk[i];
+}
 
-// 3x3 non-maximum suppression of the corner scores; survivors appended to cand (cap).
-__global__ void ka_nms(const float *__restrict__ score, int W, int H, OrbCand *__restrict__ cand,
-                       unsigned *__restrict__ count, unsigned cap) {
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  if (x < 1 || y < 1 || x >= W - 1 || y >= H - 1) return;
-  const float s = score[(size_t)y * W + x];
-  if (s <= 0.0f) return;
-  for (int dy = -1; dy <= 1; ++dy)
-    for (int dx = -1; dx <= 1; ++dx) {
-      if (!dx && !dy) continue;
-      const float o = score[(size_t)(y + dy) * W + x + dx];
-      // ties broken by position so exactly one of two equal neighbours survives
-      if (o > s || (o == s && (dy < 0 || (dy == 0 && dx < 0)))) return;
+// KeyPointsFilter::retainBest per level: the quota largest keys of each level, by an MSB-first
+// radix select (8 passes of 8 bits, histograms in LDS) to the quota-th largest key T, then
+// every key >= T copied out (exactly quota of them: keys are unique).  One workgroup per
+// level; the host orders the <= quota survivors.
+struct SelLevel {
+  unsigned off, cap, quota;
+};
+__global__ void __launch_bounds__(1024) ka_select(const uint64_t *__restrict__ keys,
+                                                  const unsigned *__restrict__ count,
+                                                  const SelLevel *__restrict__ lv,
+                                                  uint64_t *__restrict__ out, unsigned kmax,
+                                                  unsigned *__restrict__ nsel) {
+  __shared__ unsigned hist[256];
+  __shared__ uint64_t s_prefix, s_mask;
+  __shared__ unsigned s_k, s_n;
+  const int l = blockIdx.x;
+  const SelLevel L = lv[l];
+  const unsigned n = min(count[l], L.cap);
+  const uint64_t *K = keys + L.off;
+  uint64_t *O = out + (size_t)l * kmax;
+  const unsigned t = threadIdx.x;
+  if (n <= L.quota) {
+    for (unsigned i = t; i < n; i += blockDim.x) O[i] = K[i];
+    if (t == 0) nsel[l] = n;
+    return;
+  }
+  if (t == 0) {
+    s_prefix = 0;
+    s_mask = 0;
+    s_k = L.quota;
+    s_n = 0;
+  }
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (unsigned i = t; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    const uint64_t prefix = s_prefix, mask = s_mask;
+    for (unsigned i = t; i < n; i += blockDim.x) {
+      const uint64_t k = K[i];
+      if ((k & mask) == prefix) atomicAdd(&hist[(unsigned)(k >> shift) & 0xFFu], 1u);
     }
-  const unsigned i = atomicAdd(count, 1u);
-  if (i < cap) cand[i] = OrbCand{(float)x, (float)y, s};
+    __syncthreads();
+    if (t == 0) {
+      unsigned k = s_k, cum = 0;
+      int d = 255;
+      for (; d > 0; --d) {
+        if (cum + hist[d] >= k) break;
+        cum += hist[d];
+      }
+      s_k = k - cum;   // rank of T among the keys of digit d
+      s_prefix = prefix | ((uint64_t)d << shift);
+      s_mask = mask | ((uint64_t)0xFF << shift);
+    }
+    __syncthreads();
+  }
+  const uint64_t T = s_prefix;
+  for (unsigned i = t; i < n; i += blockDim.x) {
+    const uint64_t k = K[i];
+    if (k >= T) O[atomicAdd(&s_n, 1u)] = k;
+  }
+  __syncthreads();
+  if (t == 0) nsel[l] = s_n;
 }
 
 struct OrbKp {
@@ -170,31 +277,66 @@ __global__ void ka_describe(const float *const *__restrict__ levels, const int *
   }
 }
 
-// Brute-force Hamming 2-NN of every query descriptor against all train descriptors.
-__global__ void ka_match2(const uint32_t *__restrict__ q, int nq, const uint32_t *__restrict__ t,
-                          int nt, int2 *__restrict__ best, int2 *__restrict__ dist) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nq) return;
+// Brute-force Hamming 2-NN of every query descriptor against all train descriptors
+// (cuda BFMatcher knnMatch k = 2).  Grid (query groups of 64, train segments): a wavefront
+// holds 64 queries in registers and streams its train segment through LDS, 64 descriptors
+// per tile; each segment's stable top-2 (ties: lower train index) goes to part[], and
+// ka_match2_merge folds the segments in index order, which gives exactly the top-2 of one
+// sequential scan.
+struct Top2 {
+  int b0, b1, d0, d1;
+};
+__device__ __forceinline__ void top2_push(Top2 &t, int h, int j) {
+  if (h < t.d0) {
+    t.d1 = t.d0;
+    t.b1 = t.b0;
+    t.d0 = h;
+    t.b0 = j;
+  } else if (h < t.d1) {
+    t.d1 = h;
+    t.b1 = j;
+  }
+}
+__global__ void __launch_bounds__(64) ka_match2(const uint32_t *__restrict__ q, int nq,
+                                                const uint32_t *__restrict__ t, int nt, int seg,
+                                                Top2 *__restrict__ part) {
+  __shared__ uint32_t tile[64 * 8];
+  const int lane = threadIdx.x;
+  const int i = blockIdx.x * 64 + lane;
+  const int j0 = blockIdx.y * seg, j1 = min(nt, j0 + seg);
   uint32_t d[8];
 #pragma unroll
-  for (int w = 0; w < 8; ++w) d[w] = q[(size_t)i * 8 + w];
-  int b0 = -1, b1 = -1, d0 = 1 << 30, d1 = 1 << 30;
-  for (int j = 0; j < nt; ++j) {
-    int h = 0;
+  for (int w = 0; w < 8; ++w) d[w] = i < nq ? q[(size_t)i * 8 + w] : 0u;
+  Top2 r{-1, -1, 1 << 30, 1 << 30};
+  for (int jt = j0; jt < j1; jt += 64) {
+    const int nj = min(64, j1 - jt);
+    __syncthreads();
+    if (lane < nj) {
 #pragma unroll
-    for (int w = 0; w < 8; ++w) h += __popc(d[w] ^ t[(size_t)j * 8 + w]);
-    if (h < d0) {
-      d1 = d0;
-      b1 = b0;
-      d0 = h;
-      b0 = j;
-    } else if (h < d1) {
-      d1 = h;
-      b1 = j;
+      for (int w = 0; w < 8; ++w) tile[w * 64 + lane] = t[(size_t)(jt + lane) * 8 + w];
+    }
+    __syncthreads();
+    for (int k = 0; k < nj; ++k) {
+      int h = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) h += __popc(d[w] ^ tile[w * 64 + k]);
+      top2_push(r, h, jt + k);
     }
   }
-  best[i] = make_int2(b0, b1);
-  dist[i] = make_int2(d0, d1);
+  if (i < nq) part[(size_t)blockIdx.y * nq + i] = r;
+}
+__global__ void ka_match2_merge(const Top2 *__restrict__ part, int nq, int nseg,
+                                int2 *__restrict__ best, int2 *__restrict__ dist) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  Top2 r = part[i];
+  for (int s = 1; s < nseg; ++s) {
+    const Top2 p = part[(size_t)s * nq + i];
+    if (p.b0 >= 0) top2_push(r, p.d0, p.b0);
+    if (p.b1 >= 0) top2_push(r, p.d1, p.b1);
+  }
+  best[i] = make_int2(r.b0, r.b1);
+  dist[i] = make_int2(r.d0, r.d1);
 }
 
 // cv::cuda::warpAffine(src, dst, M, dsize, INTER_LINEAR, BORDER_CONSTANT 0): dst(x, y) =

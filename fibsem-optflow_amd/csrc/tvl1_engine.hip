@@ -7,6 +7,7 @@
 // every stage runs on the device; the only device->host traffic inside a solve is
 // the residual of "check" iterations, read exactly where OpenCV reads it.
 #include <hip/hip_runtime.h>
+#include <chrono>
 
 #include <cfloat>
 #include <cmath>
@@ -111,6 +112,9 @@ struct tvl1_ctx {
   int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
   size_t map_bytes = 0;
+  char *align_scratch = nullptr;        // tvl1_find_alignment's pyramid, keys, descriptors
+  size_t align_bytes = 0;
+  int4 *align_pat = nullptr;            // the rBRIEF pair pattern (device, set once)
   int bnblk = 0;                        // partials per pair
   int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
@@ -1501,111 +1505,176 @@ namespace {
 struct OrbSet {
   std::vector<OrbKp> kps;     // level coordinates
   std::vector<Pt> pts;        // level-0 coordinates
-  uint32_t *desc = nullptr;   // device, 8 words per keypoint
+  uint32_t *desc = nullptr;   // device, 8 words per keypoint (in the ctx's align scratch)
 };
 
-static tvl1_status orb_detect(tvl1_ctx *c, const uint8_t *img, size_t pitch, int W, int H,
-                              const tvl1_align_params &ap, const int4 *dpat, OrbSet &out,
-                              hipStream_t st) {
-  const int L = std::max(1, ap.nlevels);
+// One frame's ORB pyramid geometry and its quota per level (ORB_Impl::detectAndCompute:
+// nfeatures * (1 - f) / (1 - f^L) * f^l, the remainder on the last level).
+struct OrbGeom {
+  int L = 0;
+  std::vector<int> w, h, p, quota;
+  std::vector<unsigned> cap, off;   // key-list capacity / offset per level
+  size_t keys = 0, lev_floats = 0;
+  unsigned kmax = 0;
+};
+
+static OrbGeom orb_geom(int W, int H, const tvl1_align_params &ap) {
+  OrbGeom g;
+  g.L = std::max(1, ap.nlevels);
   const double sf = ap.scale_factor;
-  std::vector<int> lw(L), lh(L), lp(L);
-  std::vector<float *> lev(L, nullptr);
-  for (int l = 0; l < L; ++l) {
+  g.w.resize(g.L);
+  g.h.resize(g.L);
+  g.p.resize(g.L);
+  g.quota.assign(g.L, 0);
+  g.cap.resize(g.L);
+  g.off.resize(g.L);
+  for (int l = 0; l < g.L; ++l) {
     const double scale = 1.0 / std::pow(sf, l - ap.first_level);
-    lw[l] = l == 0 ? W : std::max(1, (int)std::lrint(W * scale));
-    lh[l] = l == 0 ? H : std::max(1, (int)std::lrint(H * scale));
-    lp[l] = (int)align_up((size_t)lw[l], 64);
+    g.w[l] = l == 0 ? W : std::max(1, (int)std::lrint(W * scale));
+    g.h[l] = l == 0 ? H : std::max(1, (int)std::lrint(H * scale));
+    g.p[l] = (int)align_up((size_t)g.w[l], 64);
+    g.lev_floats += align_up((size_t)g.p[l] * g.h[l], 64);
+    g.cap[l] = (unsigned)(((size_t)g.w[l] + 1) / 2 * (((size_t)g.h[l] + 1) / 2));
+    g.off[l] = (unsigned)g.keys;
+    g.keys += align_up(g.cap[l], 32);
   }
-  std::vector<void *> owned;
-  auto alloc = [&](size_t bytes) -> void * {
-    void *p = nullptr;
-    if (hipMalloc(&p, std::max<size_t>(bytes, 256)) != hipSuccess) return nullptr;
-    owned.push_back(p);
+  const double f = 1.0 / sf;
+  double nd = ap.nfeatures * (1 - f) / (1 - std::pow(f, g.L));
+  int sum = 0;
+  for (int l = 0; l < g.L - 1; ++l) {
+    g.quota[l] = (int)std::lrint(nd);
+    sum += g.quota[l];
+    nd *= f;
+  }
+  g.quota[g.L - 1] = std::max(ap.nfeatures - sum, 0);
+  for (int l = 0; l < g.L; ++l) g.kmax = std::max(g.kmax, (unsigned)g.quota[l]);
+  return g;
+}
+
+// The align scratch: [kps | desc q | desc t | match best | match dist | pyramid | blurred
+// pyramid | score | keys | counts | selected keys | nsel | level table], carved per frame.
+struct AlignCarve {
+  float *lev = nullptr, *blur = nullptr, *score = nullptr;
+  uint64_t *keys = nullptr, *sel = nullptr;
+  unsigned *cnt = nullptr, *nsel = nullptr;
+  SelLevel *lv = nullptr;
+  float **dlev = nullptr;
+  int *dlp = nullptr;
+  OrbKp *kps = nullptr;
+  uint32_t *desc[2] = {nullptr, nullptr};
+  int2 *best = nullptr, *dist = nullptr;
+  Top2 *part = nullptr;
+};
+constexpr int kMatchSegs = 16;   // train segments of ka_match2 (grid y)
+
+static size_t align_carve(char *base, const OrbGeom &g, bool blur, int nfeat, AlignCarve &cv) {
+  size_t o = 0;
+  auto take = [&](size_t bytes) -> char * {
+    char *p = base ? base + o : nullptr;
+    o += align_up(std::max<size_t>(bytes, 1), 256);
     return p;
   };
-  auto cleanup = [&]() {
-    for (void *p : owned) (void)hipFree(p);
-  };
-  for (int l = 0; l < L; ++l) {
-    lev[l] = (float *)alloc((size_t)lp[l] * lh[l] * sizeof(float));
-    if (!lev[l]) { cleanup(); return set_err(c, TVL1_ENOMEM, "alignment: level allocation failed"); }
+  // geometry-independent parts first: the two frames' carves share them
+  cv.kps = (OrbKp *)take((size_t)nfeat * sizeof(OrbKp));
+  cv.desc[0] = (uint32_t *)take((size_t)nfeat * 32);
+  cv.desc[1] = (uint32_t *)take((size_t)nfeat * 32);
+  cv.best = (int2 *)take((size_t)nfeat * sizeof(int2));
+  cv.dist = (int2 *)take((size_t)nfeat * sizeof(int2));
+  cv.part = (Top2 *)take((size_t)nfeat * kMatchSegs * sizeof(Top2));
+  cv.lev = (float *)take(g.lev_floats * 4);
+  cv.blur = blur ? (float *)take(g.lev_floats * 4) : nullptr;
+  cv.score = (float *)take((size_t)g.w[0] * g.h[0] * 4);
+  cv.keys = (uint64_t *)take(g.keys * 8);
+  cv.cnt = (unsigned *)take(g.L * 4);
+  cv.sel = (uint64_t *)take((size_t)g.L * g.kmax * 8);
+  cv.nsel = (unsigned *)take(g.L * 4);
+  cv.lv = (SelLevel *)take(g.L * sizeof(SelLevel));
+  cv.dlev = (float **)take(g.L * sizeof(float *));
+  cv.dlp = (int *)take(g.L * 4);
+  return o;
+}
+
+// ORB detect + describe of one frame (cv::cuda::ORB::detectAndCompute, features.cpp:60-61)
+// into out; descriptors go to desc.  All levels are queued back to back: one host sync for
+// the selected keys, one for the descriptors.
+static tvl1_status orb_detect(tvl1_ctx *c, const uint8_t *img, size_t pitch, const OrbGeom &g,
+                              const tvl1_align_params &ap, const AlignCarve &cv, uint32_t *desc,
+                              OrbSet &out, hipStream_t st) {
+  const int L = g.L, W = g.w[0], H = g.h[0];
+  std::vector<float *> lev(L);
+  {
+    size_t o = 0;
+    for (int l = 0; l < L; ++l) {
+      lev[l] = cv.lev + o;
+      o += align_up((size_t)g.p[l] * g.h[l], 64);
+    }
   }
   hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 1), kBlk2, 0, st, img, pitch, img, pitch, lev[0],
-                     lev[0], W, H, lp[0]);
+                     lev[0], W, H, g.p[0]);
   for (int l = 1; l < L; ++l)
-    hipLaunchKernelGGL(k_resize_hp, grid2(lw[l], lh[l], 1), kBlk2, 0, st, lev[l - 1], nullptr,
-                       nullptr, lw[l - 1], lh[l - 1], lp[l - 1], lev[l], nullptr, nullptr, lw[l],
-                       lh[l], lp[l], (double)lw[l - 1] / lw[l], (double)lh[l - 1] / lh[l], 0, 0,
-                       1.0f);
-  // ORB's per-level quota (ORB_Impl::detectAndCompute: nfeatures * (1 - f) / (1 - f^L) f^l)
-  std::vector<int> quota(L, 0);
-  {
-    const double f = 1.0 / sf;
-    double nd = ap.nfeatures * (1 - f) / (1 - std::pow(f, L));
-    int sum = 0;
-    for (int l = 0; l < L - 1; ++l) {
-      quota[l] = (int)std::lrint(nd);
-      sum += quota[l];
-      nd *= f;
-    }
-    quota[L - 1] = std::max(ap.nfeatures - sum, 0);
-  }
+    hipLaunchKernelGGL(k_resize_hp, grid2(g.w[l], g.h[l], 1), kBlk2, 0, st, lev[l - 1], nullptr,
+                       nullptr, g.w[l - 1], g.h[l - 1], g.p[l - 1], lev[l], nullptr, nullptr,
+                       g.w[l], g.h[l], g.p[l], (double)g.w[l - 1] / g.w[l],
+                       (double)g.h[l - 1] / g.h[l], 0, 0, 1.0f);
   const int border = std::max(ap.edge_threshold, kOrbHalf + 1);
-  float *score = (float *)alloc((size_t)W * H * sizeof(float));
-  const unsigned cap = 1u << 20;
-  OrbCand *cand = (OrbCand *)alloc(cap * sizeof(OrbCand));
-  unsigned *cnt = (unsigned *)alloc(sizeof(unsigned));
-  if (!score || !cand || !cnt) { cleanup(); return set_err(c, TVL1_ENOMEM, "alignment: scratch allocation failed"); }
-  std::vector<OrbCand> host;
+  std::vector<SelLevel> lv(L);
+  HIP_TRY(c, hipMemsetAsync(cv.cnt, 0, L * sizeof(unsigned), st));
   for (int l = 0; l < L; ++l) {
-    if (lw[l] <= 2 * border || lh[l] <= 2 * border || quota[l] == 0) continue;
-    hipLaunchKernelGGL(ka_fast_harris, grid2(lw[l], lh[l]), kBlk2, 0, st, lev[l], lw[l], lh[l],
-                       lp[l], border, (float)ap.fast_threshold, score);
-    HIP_TRY(c, hipMemsetAsync(cnt, 0, sizeof(unsigned), st));
-    hipLaunchKernelGGL(ka_nms, grid2(lw[l], lh[l]), kBlk2, 0, st, score, lw[l], lh[l], cand, cnt, cap);
-    unsigned n = 0;
-    HIP_TRY(c, hipMemcpyAsync(&n, cnt, sizeof n, hipMemcpyDeviceToHost, st));
-    HIP_TRY(c, hipStreamSynchronize(st));
-    n = std::min(n, cap);
-    host.resize(n);
-    if (n) HIP_TRY(c, hipMemcpy(host.data(), cand, n * sizeof(OrbCand), hipMemcpyDeviceToHost));
-    // KeyPointsFilter::retainBest: the quota's best responses (ties by position: deterministic)
-    std::sort(host.begin(), host.end(), [](const OrbCand &a, const OrbCand &b) {
-      return a.score != b.score ? a.score > b.score : (a.y != b.y ? a.y < b.y : a.x < b.x);
-    });
-    const double scale = std::pow(sf, l - ap.first_level);
-    for (unsigned i = 0; i < std::min<unsigned>(n, (unsigned)quota[l]); ++i) {
-      out.kps.push_back(OrbKp{host[i].x, host[i].y, 0.0f, l});
-      out.pts.push_back(Pt{host[i].x * scale, host[i].y * scale});
+    lv[l] = SelLevel{g.off[l], g.cap[l], (unsigned)g.quota[l]};
+    if (g.w[l] <= 2 * border || g.h[l] <= 2 * border || g.quota[l] == 0) {
+      lv[l].quota = 0;
+      lv[l].cap = 0;
+      continue;
+    }
+    hipLaunchKernelGGL(ka_fast_harris, dim3((g.w[l] + kFhW - 1) / kFhW, (g.h[l] + kFhH - 1) / kFhH),
+                       dim3(256), 0, st, lev[l], g.w[l], g.h[l], g.p[l], border,
+                       (float)ap.fast_threshold, cv.score);
+    hipLaunchKernelGGL(ka_nms, dim3((g.w[l] + 63) / 64, (g.h[l] + kNmsRows - 1) / kNmsRows),
+                       dim3(256), 0, st, cv.score, g.w[l], g.h[l], cv.keys + g.off[l],
+                       cv.cnt + l, g.cap[l]);
+  }
+  HIP_TRY(c, hipMemcpyAsync(cv.lv, lv.data(), L * sizeof(SelLevel), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(ka_select, dim3(L), dim3(1024), 0, st, cv.keys, cv.cnt, cv.lv, cv.sel,
+                     g.kmax, cv.nsel);
+  std::vector<unsigned> nsel(L);
+  std::vector<uint64_t> sel((size_t)L * g.kmax);
+  HIP_TRY(c, hipMemcpyAsync(nsel.data(), cv.nsel, L * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(sel.data(), cv.sel, sel.size() * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  for (int l = 0; l < L; ++l) {
+    const unsigned n = std::min(nsel[l], (unsigned)g.quota[l]);
+    uint64_t *k = sel.data() + (size_t)l * g.kmax;
+    std::sort(k, k + n, [](uint64_t a, uint64_t b) { return a > b; });   // best first
+    const double scale = std::pow(ap.scale_factor, l - ap.first_level);
+    for (unsigned i = 0; i < n; ++i) {
+      const unsigned pos = 0xFFFFFFFFu - (unsigned)(k[i] & 0xFFFFFFFFu);
+      const float x = (float)(pos % (unsigned)g.w[l]), y = (float)(pos / (unsigned)g.w[l]);
+      out.kps.push_back(OrbKp{x, y, 0.0f, l});
+      out.pts.push_back(Pt{x * scale, y * scale});
     }
   }
   if (ap.blur_for_descriptor) {
+    size_t o = 0;
     for (int l = 0; l < L; ++l) {
-      float *b = (float *)alloc((size_t)lp[l] * lh[l] * sizeof(float));
-      if (!b) { cleanup(); return set_err(c, TVL1_ENOMEM, "alignment: blur allocation failed"); }
-      hipLaunchKernelGGL(ka_blur7, grid2(lw[l], lh[l]), kBlk2, 0, st, lev[l], lw[l], lh[l], lp[l], b);
+      float *b = cv.blur + o;
+      o += align_up((size_t)g.p[l] * g.h[l], 64);
+      hipLaunchKernelGGL(ka_blur7, grid2(g.w[l], g.h[l]), kBlk2, 0, st, lev[l], g.w[l], g.h[l],
+                         g.p[l], b);
       lev[l] = b;
     }
   }
   const int nk = (int)out.kps.size();
+  out.desc = desc;
   if (nk > 0) {
-    OrbKp *dk = (OrbKp *)alloc(nk * sizeof(OrbKp));
-    float **dlev = (float **)alloc(L * sizeof(float *));
-    int *dlp = (int *)alloc(L * sizeof(int));
-    if (hipMalloc((void **)&out.desc, (size_t)nk * 32) != hipSuccess || !dk || !dlev || !dlp) {
-      cleanup();
-      return set_err(c, TVL1_ENOMEM, "alignment: descriptor allocation failed");
-    }
-    HIP_TRY(c, hipMemcpyAsync(dk, out.kps.data(), nk * sizeof(OrbKp), hipMemcpyHostToDevice, st));
-    HIP_TRY(c, hipMemcpyAsync(dlev, lev.data(), L * sizeof(float *), hipMemcpyHostToDevice, st));
-    HIP_TRY(c, hipMemcpyAsync(dlp, lp.data(), L * sizeof(int), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(ka_describe, dim3((nk + 127) / 128), dim3(128), 0, st,
-                       (const float *const *)dlev, dlp, dk, nk, dpat, out.desc);
+    HIP_TRY(c, hipMemcpyAsync(cv.kps, out.kps.data(), nk * sizeof(OrbKp), hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(cv.dlev, lev.data(), L * sizeof(float *), hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(cv.dlp, g.p.data(), L * sizeof(int), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(ka_describe, dim3((nk + 63) / 64), dim3(64), 0, st,
+                       (const float *const *)cv.dlev, cv.dlp, cv.kps, nk, c->align_pat, desc);
     HIP_TRY(c, hipGetLastError());
+    // the host vectors above are the copy sources: they must outlive the copies
     HIP_TRY(c, hipStreamSynchronize(st));
   }
-  cleanup();
   return TVL1_OK;
 }
 
@@ -1875,37 +1944,58 @@ tvl1_status tvl1_find_alignment(tvl1_ctx *c, const uint8_t *frame1, size_t pitch
     return set_err(c, TVL1_EINVAL, "only WTA_K = 2 and patchSize = 31 are supported");
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
-  static const std::vector<int> pat = orb_pattern();
-  int4 *dpat = nullptr;
-  HIP_TRY(c, hipMalloc((void **)&dpat, pat.size() * sizeof(int)));
-  HIP_TRY(c, hipMemcpy(dpat, pat.data(), pat.size() * sizeof(int), hipMemcpyHostToDevice));
-  OrbSet q, t;   // query = frame1, train = frame0 (find_alignment(frame1_GPU, frame0_GPU))
-  tvl1_status s = orb_detect(c, frame1, pitch1, w1, h1, *ap, dpat, q, st);
-  if (s == TVL1_OK) s = orb_detect(c, frame0, pitch0, w0, h0, *ap, dpat, t, st);
-  (void)hipFree(dpat);
+  if (!c->align_pat) {
+    static const std::vector<int> pat = orb_pattern();
+    HIP_TRY(c, hipMalloc((void **)&c->align_pat, pat.size() * sizeof(int)));
+    HIP_TRY(c, hipMemcpy(c->align_pat, pat.data(), pat.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  const OrbGeom g1 = orb_geom(w1, h1, *ap), g0 = orb_geom(w0, h0, *ap);
+  const bool blur = ap->blur_for_descriptor != 0;
+  AlignCarve cv;
+  const size_t need = std::max(align_carve(nullptr, g1, blur, ap->nfeatures, cv),
+                               align_carve(nullptr, g0, blur, ap->nfeatures, cv));
+  if (need > c->align_bytes) {
+    if (c->align_scratch) {
+      HIP_TRY(c, hipDeviceSynchronize());
+      (void)hipFree(c->align_scratch);
+      c->align_scratch = nullptr;
+      c->align_bytes = 0;
+    }
+    if (hipMalloc((void **)&c->align_scratch, need) != hipSuccess)
+      return set_err(c, TVL1_ENOMEM, "alignment: scratch allocation of %zu bytes failed", need);
+    c->align_bytes = need;
+  }
+  static const bool timing = getenv("TVL1_ALIGN_TIMING") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const auto t0 = now();
+  // query = frame1, train = frame0 (find_alignment(frame1_GPU, frame0_GPU)); the two frames
+  // share the scratch's pyramid and keys and keep their descriptors apart
+  OrbSet q, t;
+  align_carve(c->align_scratch, g1, blur, ap->nfeatures, cv);
+  tvl1_status s = orb_detect(c, frame1, pitch1, g1, *ap, cv, cv.desc[0], q, st);
+  const auto t1 = now();
+  AlignCarve cv0;
+  align_carve(c->align_scratch, g0, blur, ap->nfeatures, cv0);
+  if (s == TVL1_OK) s = orb_detect(c, frame0, pitch0, g0, *ap, cv0, cv0.desc[1], t, st);
+  const auto t2 = now();
+  if (s != TVL1_OK) return s;
   std::vector<int2> best, dist;
   const int nq = (int)q.kps.size(), nt = (int)t.kps.size();
-  if (s == TVL1_OK && nq > 0 && nt > 0) {
-    int2 *db = nullptr, *dd = nullptr;
-    if (hipMalloc((void **)&db, nq * sizeof(int2)) != hipSuccess ||
-        hipMalloc((void **)&dd, nq * sizeof(int2)) != hipSuccess) {
-      s = set_err(c, TVL1_ENOMEM, "alignment: match allocation failed");
-    } else {
-      hipLaunchKernelGGL(ka_match2, dim3((nq + 127) / 128), dim3(128), 0, st, q.desc, nq, t.desc,
-                         nt, db, dd);
-      best.resize(nq);
-      dist.resize(nq);
-      if (hipMemcpyAsync(best.data(), db, nq * sizeof(int2), hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipMemcpyAsync(dist.data(), dd, nq * sizeof(int2), hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipStreamSynchronize(st) != hipSuccess)
-        s = set_err(c, TVL1_EHIP, "alignment: match download failed");
-    }
-    (void)hipFree(db);
-    (void)hipFree(dd);
+  if (nq > 0 && nt > 0) {
+    const int nseg = std::max(1, std::min(kMatchSegs, (nt + 255) / 256));
+    const int seg = (int)align_up((size_t)((nt + nseg - 1) / nseg), 64);
+    hipLaunchKernelGGL(ka_match2, dim3((nq + 63) / 64, nseg), dim3(64), 0, st, q.desc, nq,
+                       t.desc, nt, seg, cv.part);
+    hipLaunchKernelGGL(ka_match2_merge, dim3((nq + 255) / 256), dim3(256), 0, st, cv.part, nq,
+                       nseg, cv.best, cv.dist);
+    best.resize(nq);
+    dist.resize(nq);
+    HIP_TRY(c, hipMemcpyAsync(best.data(), cv.best, nq * sizeof(int2), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipMemcpyAsync(dist.data(), cv.dist, nq * sizeof(int2), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
   }
-  if (q.desc) (void)hipFree(q.desc);
-  if (t.desc) (void)hipFree(t.desc);
-  if (s != TVL1_OK) return s;
+  const auto t3 = now();
   // the ratio test over the first min(train rows - 1, queries) queries (features.cpp:105-112)
   struct Good {
     int qi, ti, d;
@@ -1936,6 +2026,10 @@ tvl1_status tvl1_find_alignment(tvl1_ctx *c, const uint8_t *frame1, size_t pitch
     oc = 1;
   }
   if (outcome) *outcome = oc;
+  if (timing)
+    fprintf(stderr, "[align] detect1 %.2f ms, detect0 %.2f ms, match %.2f ms, model %.2f ms "
+                    "(%d / %d keypoints, %zu good)\n",
+            ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, now()), nq, nt, good.size());
   return TVL1_OK;
 }
 
@@ -2035,6 +2129,8 @@ void tvl1_destroy(tvl1_ctx *c) {
   if (c->arena) (void)hipFree(c->arena);
   if (c->barena) (void)hipFree(c->barena);
   if (c->map_scratch) (void)hipFree(c->map_scratch);
+  if (c->align_scratch) (void)hipFree(c->align_scratch);
+  if (c->align_pat) (void)hipFree(c->align_pat);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->ev_check) (void)hipEventDestroy(c->ev_check);
