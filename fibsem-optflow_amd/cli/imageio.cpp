@@ -33,14 +33,24 @@ bool read_file(const std::string &path, std::string &out, std::string &err, bool
     }
     return true;
   }
-  std::ifstream f(path, std::ios::binary);
+  FILE *f = fopen(path.c_str(), "rb");
   if (!f) {
     err = "cannot open " + path;
     return false;
   }
-  std::ostringstream ss;
-  ss << f.rdbuf();
-  out = ss.str();
+  // one sized read (an ostringstream copy cost ~10 ms per 25-MB slice)
+  bool ok = fseek(f, 0, SEEK_END) == 0;
+  const long size = ok ? ftell(f) : -1;
+  ok = ok && size >= 0 && fseek(f, 0, SEEK_SET) == 0;
+  if (ok) {
+    out.resize((size_t)size);
+    ok = fread(&out[0], 1, out.size(), f) == out.size();
+  }
+  fclose(f);
+  if (!ok) {
+    err = "cannot read " + path;
+    return false;
+  }
   return true;
 }
 
@@ -120,35 +130,64 @@ static bool decode_png(const std::string &buf, Image8 &img, std::string &err) {
     err = "PNG: corrupt image data";
     return false;
   }
-  // unfilter in place (each row: 1 filter byte + rowbytes)
-  std::vector<uint8_t> prev(rowbytes, 0);
-  std::vector<uint8_t> px((size_t)rowbytes * H);
+  // unfilter (each row: 1 filter byte + rowbytes), one tight loop per filter type; 8-bit
+  // gray rows unfilter straight into the image
+  const bool gray8 = ctype == 0 && depth == 8;
+  std::vector<uint8_t> px(gray8 ? 0 : (size_t)rowbytes * H);
+  if (gray8) {
+    img.width = (int)W;
+    img.height = (int)H;
+    img.data.resize((size_t)W * H);
+  }
+  std::vector<uint8_t> zero(rowbytes, 0);
   for (uint32_t y = 0; y < H; ++y) {
     const uint8_t f = raw[y * (rowbytes + 1)];
     const uint8_t *in = raw.data() + y * (rowbytes + 1) + 1;
-    uint8_t *out = px.data() + (size_t)y * rowbytes;
-    for (size_t i = 0; i < rowbytes; ++i) {
-      const unsigned a = i >= bpp ? out[i - bpp] : 0;
-      const unsigned b = prev[i];
-      const unsigned c = i >= bpp ? prev[i - bpp] : 0;
-      unsigned v = in[i];
-      switch (f) {
-        case 0: break;
-        case 1: v += a; break;
-        case 2: v += b; break;
-        case 3: v += (a + b) >> 1; break;
-        case 4: {
-          const int pp = (int)a + (int)b - (int)c;
-          const int pa = abs(pp - (int)a), pb = abs(pp - (int)b), pc = abs(pp - (int)c);
-          v += (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
-          break;
+    uint8_t *out = gray8 ? img.row((int)y) : px.data() + (size_t)y * rowbytes;
+    const uint8_t *prev = y == 0 ? zero.data() : (gray8 ? img.row((int)y - 1) : out - rowbytes);
+    const size_t lead = std::min(bpp, rowbytes);
+    switch (f) {
+      case 0:
+        memcpy(out, in, rowbytes);
+        break;
+      case 1:
+        memcpy(out, in, lead);
+        for (size_t i = lead; i < rowbytes; ++i) out[i] = (uint8_t)(in[i] + out[i - bpp]);
+        break;
+      case 2:
+        for (size_t i = 0; i < rowbytes; ++i) out[i] = (uint8_t)(in[i] + prev[i]);
+        break;
+      case 3:
+        for (size_t i = 0; i < lead; ++i) out[i] = (uint8_t)(in[i] + (prev[i] >> 1));
+        for (size_t i = lead; i < rowbytes; ++i)
+          out[i] = (uint8_t)(in[i] + ((unsigned)out[i - bpp] + prev[i]) / 2);
+        break;
+      case 4:
+        for (size_t i = 0; i < lead; ++i) out[i] = (uint8_t)(in[i] + prev[i]);   // Paeth(0, b, 0) = b
+        if (bpp == 1) {   // the serial chain runs through a: keep it in a register, no branches
+          int a = out[0];
+          for (size_t i = 1; i < rowbytes; ++i) {
+            const int b = prev[i], c = prev[i - 1];
+            const int pa = abs(b - c), pb = abs(a - c), pc = abs(a + b - 2 * c);
+            const int bc = pb <= pc ? b : c;
+            a = (uint8_t)(in[i] + ((pa <= pb) & (pa <= pc) ? a : bc));
+            out[i] = (uint8_t)a;
+          }
+        } else {
+          for (size_t i = lead; i < rowbytes; ++i) {
+            const int a = out[i - bpp], b = prev[i], c = prev[i - bpp];
+            const int pa = abs(b - c), pb = abs(a - c), pc = abs(a + b - 2 * c);
+            const int pr = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+            out[i] = (uint8_t)(in[i] + pr);
+          }
         }
-        default: err = "PNG: bad filter type"; return false;
-      }
-      out[i] = (uint8_t)v;
+        break;
+      default:
+        err = "PNG: bad filter type";
+        return false;
     }
-    memcpy(prev.data(), out, rowbytes);
   }
+  if (gray8) return true;
   img.width = (int)W;
   img.height = (int)H;
   img.data.assign((size_t)W * H, 0);
@@ -379,6 +418,18 @@ static bool decode_tiff(const std::string &buf, Image8 &img, std::string &err) {
   img.width = (int)W;
   img.height = (int)H;
   img.data.assign((size_t)W * H, 0);
+  if (spp == 1 && bps == 8) {   // 8-bit gray: rows as they are (inverted for WhiteIsZero)
+    for (uint32_t y = 0; y < H; ++y) {
+      const uint8_t *row = px.data() + (size_t)y * rowbytes;
+      uint8_t *o = img.row((int)y);
+      if (photo == 0) {
+        for (uint32_t x = 0; x < W; ++x) o[x] = (uint8_t)(255 - row[x]);
+      } else {
+        memcpy(o, row, W);
+      }
+    }
+    return true;
+  }
   for (uint32_t y = 0; y < H; ++y) {
     const uint8_t *row = px.data() + (size_t)y * rowbytes;
     uint8_t *o = img.row((int)y);

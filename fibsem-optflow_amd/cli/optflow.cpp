@@ -24,12 +24,18 @@
 //     they are silently ignored there);
 //   * a malformed JSON file is an error (the reference ignores parse failure);
 //   * build-only keys: "devices" (list of GPU ordinals, pairs sharded over them),
-//     "inflight" (pairs in flight per GPU, default 2), "medianFiltering",
+//     "inflight" (pairs in flight per GPU, default 2), "decode_threads" (slice decode-ahead
+//     pool, default min(16, cores - 1)), "medianFiltering",
 //     "matches_file", "stats_json", "skip_existing".
 #include <hip/hip_runtime.h>
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <future>
+#include <memory>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -205,6 +211,34 @@ GlibcRand &g_rand() {
 }
 
 // random_points (optflow.cpp:522-572) + the libstdc++ std::random_shuffle it uses.
+// The point_matches fields of random_points (optflow.cpp:537-569) for the chosen points;
+// any == false gives the dummy point.
+void emit_points(const std::vector<std::pair<int, int>> &pts, const std::vector<float> &vx,
+                 const std::vector<float> &vy, bool any, Value &im, const Rect &r0, const Rect &r1,
+                 float inv_scale, bool features) {
+  Value &pm = im["point_matches"];
+  for (size_t i = 0; i < pts.size(); ++i) {
+    const int px = pts[i].first, py = pts[i].second;
+    pm["w"].append(1);
+    pm["p"][0].append((double)((px + r0.x) * inv_scale));
+    pm["p"][1].append((double)((py + r0.y) * inv_scale));
+    if (features) {
+      pm["q"][0].append((double)((vx[i] + r1.x) * inv_scale));
+      pm["q"][1].append((double)((vy[i] + r1.y) * inv_scale));
+    } else {
+      pm["q"][0].append((double)((px + r1.x + vx[i]) * inv_scale));
+      pm["q"][1].append((double)((py + r1.y + vy[i]) * inv_scale));
+    }
+  }
+  if (!any) {  // dummy point so the fields are full
+    pm["p"][0].append(-1);
+    pm["p"][1].append(-1);
+    pm["q"][0].append(-1);
+    pm["q"][1].append(-1);
+    pm["w"].append(0);
+  }
+}
+
 void random_points(const std::vector<float> &fx, const std::vector<float> &fy, int W, int H,
                    Value &im, const Value &args, const Rect &r0, const Rect &r1,
                    const std::vector<uint8_t> &mask, bool features) {
@@ -216,7 +250,6 @@ void random_points(const std::vector<float> &fx, const std::vector<float> &fy, i
     for (int x = 0; x < W; ++x)
       if (mask[(size_t)y * W + x]) loc.emplace_back(x, y);
   const int npoints = im.get("npoints", args.get("npoints", 25).asInt()).asInt();
-  Value &pm = im["point_matches"];
   {
     std::lock_guard<std::mutex> lk(g_rand_mutex);
     if (!debug) g_rand().seed((unsigned)std::time(0));
@@ -225,27 +258,80 @@ void random_points(const std::vector<float> &fx, const std::vector<float> &fy, i
       if (i != j) std::swap(loc[i], loc[j]);
     }
   }
-  for (int i = 0; i < npoints && (size_t)i < loc.size(); ++i) {
-    const int px = loc[i].first, py = loc[i].second;
-    const float vx = fx[(size_t)py * W + px], vy = fy[(size_t)py * W + px];
-    pm["w"].append(1);
-    pm["p"][0].append((double)((px + r0.x) * inv_scale));
-    pm["p"][1].append((double)((py + r0.y) * inv_scale));
-    if (features) {
-      pm["q"][0].append((double)((vx + r1.x) * inv_scale));
-      pm["q"][1].append((double)((vy + r1.y) * inv_scale));
-    } else {
-      pm["q"][0].append((double)((px + r1.x + vx) * inv_scale));
-      pm["q"][1].append((double)((py + r1.y + vy) * inv_scale));
+  std::vector<std::pair<int, int>> pts(loc.begin(), loc.begin() + std::min<size_t>(loc.size(), std::max(npoints, 0)));
+  std::vector<float> vx(pts.size()), vy(pts.size());
+  for (size_t i = 0; i < pts.size(); ++i) {
+    vx[i] = fx[(size_t)pts[i].second * W + pts[i].first];
+    vy[i] = fy[(size_t)pts[i].second * W + pts[i].first];
+  }
+  emit_points(pts, vx, vy, !loc.empty(), im, r0, r1, inv_scale, features);
+}
+
+// random_points without the debug flag, where the reference seeds rand() with the time
+// (optflow.cpp:532-535) and keeps the first npoints of a random_shuffle of all the masked
+// px: npoints distinct uniformly random masked px in random order is the same distribution.
+// Drawn by a partial Fisher-Yates over the implicit list (row counts + a sparse swap map),
+// and only those px's flow values are read back: no 25 M-entry shuffle, no full download.
+// Debug runs keep the exact shuffle (random_points above) so their output is reproducible.
+bool random_points_sampled(DeviceCtx &dc, size_t fp, int W, int H, const ofio::Image8 &f0,
+                           const ofio::Image8 &f1, const Rect &r0, const Rect &r1, Value &im,
+                           const Value &args, bool features, std::string &err) {
+  const float scale = im.get("scale", args.get("scale", 0.5).asFloat()).asFloat();
+  const float inv_scale = 1. / scale;
+  const int npoints = im.get("npoints", args.get("npoints", 25).asInt()).asInt();
+  // mask = (frame0 > 1) | (frame1 > 1) on the ROIs (optflow.cpp:486-494), counted per row
+  std::vector<uint64_t> prefix((size_t)H + 1, 0);
+  for (int y = 0; y < H; ++y) {
+    const uint8_t *a = f0.row(r0.y + y) + r0.x, *b = f1.row(r1.y + y) + r1.x;
+    unsigned c = 0;
+    for (int x = 0; x < W; ++x) c += (a[x] > 1) | (b[x] > 1);
+    prefix[y + 1] = prefix[y] + c;
+  }
+  const uint64_t total = prefix[H];
+  std::vector<uint64_t> pick;
+  {
+    std::lock_guard<std::mutex> lk(g_rand_mutex);
+    g_rand().seed((unsigned)std::time(0));
+    std::map<uint64_t, uint64_t> swapped;   // sparse Fisher-Yates: index -> current value
+    auto at = [&](uint64_t i) {
+      auto it = swapped.find(i);
+      return it == swapped.end() ? i : it->second;
+    };
+    const uint64_t k = std::min<uint64_t>(total, (uint64_t)std::max(npoints, 0));
+    for (uint64_t i = 0; i < k; ++i) {
+      const uint64_t r = ((uint64_t)g_rand().next() << 31) ^ (uint64_t)g_rand().next();
+      const uint64_t j = i + r % (total - i);
+      const uint64_t vi = at(i), vj = at(j);
+      swapped[i] = vj;
+      swapped[j] = vi;
+      pick.push_back(vj);
     }
   }
-  if (loc.empty()) {  // dummy point so the fields are full
-    pm["p"][0].append(-1);
-    pm["p"][1].append(-1);
-    pm["q"][0].append(-1);
-    pm["q"][1].append(-1);
-    pm["w"].append(0);
+  std::vector<std::pair<int, int>> pts;
+  for (uint64_t idx : pick) {
+    const int y = (int)(std::upper_bound(prefix.begin(), prefix.end(), idx) - prefix.begin()) - 1;
+    uint64_t left = idx - prefix[y];
+    const uint8_t *a = f0.row(r0.y + y) + r0.x, *b = f1.row(r1.y + y) + r1.x;
+    int x = 0;
+    for (;; ++x)
+      if (((a[x] > 1) | (b[x] > 1)) && left-- == 0) break;
+    pts.emplace_back(x, y);
   }
+  std::vector<float> vx(pts.size()), vy(pts.size());
+  for (size_t i = 0; i < pts.size(); ++i) {
+    const size_t off = (size_t)pts[i].second * fp + (size_t)pts[i].first * 4;
+    if (hipMemcpyAsync(&vx[i], (const char *)dc.du + off, 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
+        hipMemcpyAsync(&vy[i], (const char *)dc.dv + off, 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess) {
+      err = "flow read-back failed";
+      return false;
+    }
+  }
+  if (hipStreamSynchronize(dc.stream) != hipSuccess) {
+    err = "flow read-back failed";
+    return false;
+  }
+  emit_points(pts, vx, vy, total > 0, im, r0, r1, inv_scale, features);
+  return true;
 }
 
 // move_pm (optflow.cpp:574-593)
@@ -304,6 +390,25 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
   if (s != TVL1_OK) {
     err = tvl1_last_error(dc.ctx);
     return false;
+  }
+  const bool sampled = otype == "random_points" && !args.get("debug", false).asBool();
+  if (sampled) {
+    if (hipStreamSynchronize(dc.stream) != hipSuccess) {
+      err = "solve failed";
+      return false;
+    }
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    Value sv;
+    sv["roi"][0] = r0.x;
+    sv["roi"][1] = r0.y;
+    sv["roi"][2] = W;
+    sv["roi"][3] = H;
+    sv["seconds"] = secs;
+    sv["levels"] = st.levels;
+    sv["iterations"] = (int64_t)st.iterations_total;
+    sv["checks"] = (int64_t)st.checks_total;
+    res.stats["solves"].append(sv);
+    return random_points_sampled(dc, fp, W, H, f0, f1, r0, r1, im, args, features, err);
   }
   std::vector<float> fx((size_t)W * H), fy((size_t)W * H);
   if (hipMemcpyAsync(fx.data(), dc.du, fx.size() * 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
@@ -488,6 +593,71 @@ struct Job {
   Value im;
 };
 
+// Decode-ahead pool.  A 6144x4096 PNG takes ~0.3 s of one core to decode
+// (zlib inflate ~0.23 s), 5x one pair's GPU solve, so slices are read + pre-scaled by a
+// pool of host threads while the GPU works: a worker queues every slice of its current and
+// next chunk of pairs and then takes them in pair order.
+struct Loaded {
+  bool ok = false;
+  ofio::Image8 img;
+  std::string err;
+};
+using LoadFuture = std::shared_future<std::shared_ptr<Loaded>>;
+
+class DecodePool {
+ public:
+  explicit DecodePool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
+  }
+  ~DecodePool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  // imread(IMREAD_GRAYSCALE) + resize(scale) (optflow.cpp:104-131) on a pool thread
+  LoadFuture load(const std::string &path, float scale) {
+    auto task = std::make_shared<std::packaged_task<std::shared_ptr<Loaded>()>>([path, scale] {
+      auto r = std::make_shared<Loaded>();
+      ofio::Image8 img;
+      if (!ofio::read_gray8(path, img, r->err) || img.width == 0 || img.height == 0) return r;
+      if (scale != 1) ofio::resize_u8(img, scale, scale, r->img);
+      else r->img = std::move(img);
+      r->ok = true;
+      return r;
+    });
+    LoadFuture f = task->get_future().share();
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      q_.emplace_back([task] { (*task)(); });
+    }
+    cv_.notify_one();
+    return f;
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        job = std::move(q_.front());
+        q_.pop_front();
+      }
+      job();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::vector<std::thread> th_;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------- from_file
@@ -507,6 +677,9 @@ static int from_file(Value &args, bool plan_only) {
   }
   const bool skip_existing = args.get("skip_existing", false).asBool();
 
+  // build-only "decode_threads": host threads decoding slices ahead of the GPU
+  const unsigned hc = std::max(2u, std::thread::hardware_concurrency());
+  DecodePool pool(std::max(1, args.get("decode_threads", (int)std::min(16u, hc - 1)).asInt()));
   std::atomic<size_t> next{0};
   const size_t chunk = std::max<size_t>(1, std::min<size_t>(16, n / std::max<size_t>(1, devices.size() * 4)));
   std::atomic<int> hard_error{0};
@@ -526,14 +699,36 @@ static int from_file(Value &args, bool plan_only) {
       (void)hipSetDevice(device);
       (void)hipStreamCreateWithFlags(&dc.stream, hipStreamNonBlocking);
     }
-    std::string old0, old1;
+    // this worker's chunks of pairs: the current one and the next, both queued for decode
+    std::map<std::string, LoadFuture> pending;   // slice key -> its decode
+    auto scale_of = [&](size_t i) {
+      return images[i].get("scale", args.get("scale", 0.5).asFloat()).asFloat();
+    };
+    auto key_of = [&](const std::string &path, float scale) {
+      char b[32];
+      snprintf(b, sizeof b, "%0.2f", scale);
+      return path + "|" + b;
+    };
+    auto queue_chunk = [&](size_t start) {
+      for (size_t i = start; i < std::min(n, start + chunk); ++i) {
+        const float sc = scale_of(i);
+        for (const char *side : {"p", "q"}) {
+          const std::string path = images[i][side].asString(), k = key_of(path, sc);
+          if (!pending.count(k)) pending.emplace(k, pool.load(path, sc));
+        }
+      }
+    };
+    size_t next_start = next.fetch_add(chunk);
+    if (next_start < n) queue_chunk(next_start);
     for (;;) {
-      const size_t start = next.fetch_add(chunk);
+      const size_t start = next_start;
       if (start >= n) break;
+      next_start = next.fetch_add(chunk);
+      if (next_start < n) queue_chunk(next_start);
       for (size_t i = start; i < std::min(n, start + chunk); ++i) {
         Value im = images[i];
         const std::string p = im["p"].asString(), q = im["q"].asString();
-        const float scale = im.get("scale", args.get("scale", 0.5).asFloat()).asFloat();
+        const float scale = scale_of(i);
         im["scale"] = im.get("scale", (double)scale).asDouble();
         {
           std::lock_guard<std::mutex> lk(g_io_mutex);
@@ -557,11 +752,34 @@ static int from_file(Value &args, bool plan_only) {
         }
         r1 = (k1 == dc.key1);
         std::string err;
+        // the pooled decode of a slice; a queued slice leaves `pending` (retire) after the
+        // last pair of the two queued chunks that names it, whether or not it was decoded
+        // for nothing because the slice was already resident
+        auto needed_later = [&](const std::string &k) {
+          for (size_t j = i + 1; j < std::min(n, start + chunk); ++j)
+            if (key_of(images[j]["p"].asString(), scale_of(j)) == k ||
+                key_of(images[j]["q"].asString(), scale_of(j)) == k)
+              return true;
+          for (size_t j = next_start; j < std::min(n, next_start + chunk); ++j)
+            if (key_of(images[j]["p"].asString(), scale_of(j)) == k ||
+                key_of(images[j]["q"].asString(), scale_of(j)) == k)
+              return true;
+          return false;
+        };
+        auto retire = [&](const std::string &k) {
+          if (!needed_later(k)) pending.erase(k);
+        };
         auto load = [&](const std::string &name, ofio::Image8 &dst) {
-          ofio::Image8 img;
-          if (!ofio::read_gray8(name, img, err) || img.width == 0 || img.height == 0) return false;
-          if (scale != 1) ofio::resize_u8(img, scale, scale, dst);
-          else dst = std::move(img);
+          const std::string k = key_of(name, scale);
+          auto it = pending.find(k);
+          LoadFuture f = it != pending.end() ? it->second : pool.load(name, scale);
+          const std::shared_ptr<Loaded> r = f.get();
+          if (!r->ok) {
+            err = r->err;
+            return false;
+          }
+          if (needed_later(k)) dst = r->img;   // a later pair reads it again: copy
+          else dst = std::move(r->img);        // last use: nobody reads it after this
           return true;
         };
         if (!r0 && !load(p, dc.h0)) {
@@ -569,6 +787,8 @@ static int from_file(Value &args, bool plan_only) {
           printf("Error: %s \n", p.c_str());
           dc.key0.clear();
           results[i].done = true;
+          retire(k0);
+          retire(k1);
           continue;
         }
         if (!r1 && !load(q, dc.h1)) {
@@ -576,10 +796,14 @@ static int from_file(Value &args, bool plan_only) {
           printf("Error: %s \n", q.c_str());
           dc.key1.clear();
           results[i].done = true;
+          retire(k0);
+          retire(k1);
           continue;
         }
         dc.key0 = k0;
         dc.key1 = k1;
+        retire(k0);
+        retire(k1);
         const int rows = std::min(dc.h0.height, dc.h1.height), cols = std::min(dc.h0.width, dc.h1.width);
         Value rois;
         if (im.isMember("rois")) {
@@ -652,7 +876,7 @@ static int from_file(Value &args, bool plan_only) {
     }
     if (dc.ctx) tvl1_destroy(dc.ctx);
     if (dc.stream) (void)hipStreamDestroy(dc.stream);
-    for (void *ptr : {(void *)dc.d0, (void *)dc.d1, (void *)dc.du, (void *)dc.dv})
+    for (void *ptr : {(void *)dc.d0, (void *)dc.d1, (void *)dc.dw, (void *)dc.du, (void *)dc.dv})
       if (ptr) (void)hipFree(ptr);
   };
 

@@ -140,6 +140,31 @@ def test_random_points_deterministic_with_debug(tmp_path, pair):
         assert abs(pm["q"][1][k] - (y + float(v[y, x]))) < 1e-4
 
 
+def test_random_points_sampled_without_debug(tmp_path, pair):
+    """Without debug the CLI samples npoints distinct masked px directly and reads back only
+    their flow (no full shuffle, no full download).  Each point must be a distinct px with
+    q - p = the flow there, and inside the mask (frame0 > 1 or frame1 > 1)."""
+    cfg = {"output_dir": str(tmp_path), "scale": 1, "output_type": "random_points",
+           "npoints": 40, "nscales": 3, "warps": 2, "rois": {"top": 30},
+           "images": [{"p": str(tmp_path / "p.png"), "q": str(tmp_path / "q.png"),
+                       "pId": "a", "qId": "b", "pGroupId": "1.0", "qGroupId": "2.0"}]}
+    run_cli(cfg, tmp_path)
+    (m,) = json.loads((tmp_path / "point_matches_0.json").read_text())
+    pm = m["matches"]
+    assert len(pm["w"]) == 40 and set(pm["w"]) == {1}
+    I0, I1 = pair
+    u, v = oracle_post(np.ascontiguousarray(I0[:30]), np.ascontiguousarray(I1[:30]),
+                       capi.make_params(nscales=3, warps=2), 0)
+    seen = set()
+    for k in range(40):
+        x, y = int(pm["p"][0][k]), int(pm["p"][1][k])
+        assert (x, y) not in seen
+        seen.add((x, y))
+        assert I0[y, x] > 1 or I1[y, x] > 1
+        assert abs(pm["q"][0][k] - (x + float(u[y, x]))) < 1e-4
+        assert abs(pm["q"][1][k] - (y + float(v[y, x]))) < 1e-4
+
+
 def test_two_workers_match_one(tmp_path, built):
     """Pairs sharded over two workers (here both on GPU 0) give byte-identical files."""
     stack = synth.gen_stack(96, 64, 5, seed=77)

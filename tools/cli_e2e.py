@@ -1,0 +1,92 @@
+"""End-to-end throughput of the optflow CLI on a PNG stack ("a separate run
+includes PNG decode"; 8(f) N2): PNG decode + pre-scale + upload + solve + point-match
+output, timed around the whole CLI process.
+
+    python tools/cli_e2e.py [--slices 17] [--width 6144 --height 4096] [--out DIR]
+
+Writes the slices once (device-generated synthetic texture, PNG), then runs two job
+configurations, each with the decode-ahead pool and with one decode thread:
+  * "C2 full frame": scale 1, one custom full-frame ROI, nscales 5, warps 30;
+  * "production strips": scale 0.5, top/bottom 100-row ROIs, reference defaults
+    (gen_cross_file_list.py's job shape).
+Output type random_points (the production output) keeps TIFF writes out of the timing.
+Prints one JSON line per run."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "fibsem-optflow_amd"))
+OPTFLOW = ROOT / "fibsem-optflow_amd" / "bin" / "optflow"
+
+
+def make_stack(d: Path, Z: int, W: int, H: int):
+    import torch
+    from PIL import Image
+
+    from optflow_amd.synth_device import DeviceStack
+    st = DeviceStack(W, H, torch.device("cuda", 0), seed=0x5EED)
+    slices = [st.slice(z).cpu().numpy() for z in range(Z)]
+    paths = [d / f"s{z:04d}.png" for z in range(Z)]
+    with ThreadPoolExecutor(8) as ex:
+        list(ex.map(lambda a: Image.fromarray(a[0]).save(a[1], compress_level=6),
+                    zip(slices, paths)))
+    return paths
+
+
+def run(cfg, d: Path, name: str):
+    p = d / f"{name}.json"
+    p.write_text(json.dumps(cfg))
+    t0 = time.perf_counter()
+    r = subprocess.run([str(OPTFLOW), str(p)], capture_output=True, text=True, timeout=900)
+    dt = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr[-2000:])
+    return dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--slices", type=int, default=17)
+    ap.add_argument("--width", type=int, default=6144)
+    ap.add_argument("--height", type=int, default=4096)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    d = Path(args.out or tempfile.mkdtemp(prefix="cli_e2e_"))
+    d.mkdir(parents=True, exist_ok=True)
+    t0 = time.perf_counter()
+    paths = make_stack(d, args.slices, args.width, args.height)
+    print(json.dumps({"stack": f"{args.slices} x {args.width}x{args.height} PNG",
+                      "bytes": sum(os.path.getsize(p) for p in paths),
+                      "write_s": round(time.perf_counter() - t0, 1)}), flush=True)
+    pairs = [{"p": str(paths[z]), "q": str(paths[z + 1]), "output_name": f"z{z}",
+              "pId": f"{z}", "qId": f"{z + 1}", "pGroupId": f"{z}.0", "qGroupId": f"{z + 1}.0"}
+             for z in range(args.slices - 1)]
+    W, H = args.width, args.height
+    jobs = {
+        "c2_full_frame": {"scale": 1, "nscales": 5, "warps": 30,
+                          "rois": {"custom": [0, 0, W, H]}},
+        "production_strips": {"scale": 0.5, "rois": {"top": 100, "bottom": 100}},
+    }
+    for name, extra in jobs.items():
+        for threads in (None, 1):
+            cfg = {"output_dir": str(d / name), "output_type": "random_points",
+                   "matches_file": str(d / name / "pm"), "images": pairs, **extra}
+            if threads:
+                cfg["decode_threads"] = threads
+            (d / name).mkdir(exist_ok=True)
+            dt = run(cfg, d, f"{name}_{threads or 'pool'}")
+            n = len(pairs)
+            print(json.dumps({"job": name, "decode_threads": threads or "default (pool)",
+                              "pairs": n, "wall_s": round(dt, 3),
+                              "pairs_per_s": round(n / dt, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
