@@ -184,3 +184,72 @@ def test_prescale_half_is_2x2_mean(tmp_path, built):
     ref = (s[0::2, 0::2] + s[1::2, 0::2] + s[0::2, 1::2] + s[1::2, 1::2] + 2) >> 2
     assert b.shape == (20, 32)
     assert np.array_equal(b, ref)   # 32 columns = 4 full 8-wide vector blocks
+
+
+def _png_bytes(rows, width, height, ctype, depth, filters):
+    """A PNG written by hand so every filter type (0-4) is exercised row by row."""
+    import struct
+    import zlib
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+
+    bpp = max(1, {0: 1, 2: 3, 4: 2, 6: 4}[ctype] * depth // 8)
+    raw = bytearray()
+    prev = np.zeros(rows.shape[1], np.int32)
+    for y in range(height):
+        cur = rows[y].astype(np.int32)
+        f = filters[y % len(filters)]
+        a = np.concatenate([np.zeros(bpp, np.int32), cur[:-bpp]])
+        c = np.concatenate([np.zeros(bpp, np.int32), prev[:-bpp]])
+        if f == 0:
+            pred = np.zeros_like(cur)
+        elif f == 1:
+            pred = a
+        elif f == 2:
+            pred = prev
+        elif f == 3:
+            pred = (a + prev) // 2
+        else:
+            p = a + prev - c
+            pa, pb, pc = np.abs(p - a), np.abs(p - prev), np.abs(p - c)
+            pred = np.where((pa <= pb) & (pa <= pc), a, np.where(pb <= pc, prev, c))
+        raw.append(f)
+        raw += ((cur - pred) & 0xFF).astype(np.uint8).tobytes()
+        prev = cur
+    ihdr = struct.pack(">IIBBBBB", width, height, depth, ctype, 0, 0, 0)
+    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", zlib.compress(bytes(raw), 6))
+            + chunk(b"IEND", b""))
+
+
+@pytest.mark.parametrize("inflate", ["default", "zlib"])
+@pytest.mark.parametrize("kind", ["gray8", "gray16", "rgb8", "graya8"])
+def test_png_every_filter_type(tmp_path, built, kind, inflate, monkeypatch):
+    """PNG unfiltering (None, Sub, Up, Average, Paeth) for 1-, 2-, 3-byte pixels; the
+    inflate goes through libdeflate when the image has it, else zlib."""
+    rng = np.random.default_rng(11)
+    H, W = 23, 41
+    a = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    if kind == "gray8":
+        rows, ctype, depth, want = a, 0, 8, a
+    elif kind == "gray16":
+        b16 = a.astype(np.uint16) * 257 + rng.integers(0, 2, (H, W)).astype(np.uint16)
+        rows = b16.astype(">u2").view(np.uint8).reshape(H, 2 * W)
+        ctype, depth, want = 0, 16, (b16 >> 8).astype(np.uint8)
+    elif kind == "rgb8":
+        rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        rgb[: H // 2] = a[: H // 2, :, None]          # gray rows take the r == g == b path
+        rows, ctype, depth = rgb.reshape(H, 3 * W), 2, 8
+        r, g, b = (rgb[..., k].astype(np.int64) for k in range(3))
+        want = ((9798 * r + 19235 * g + (32768 - 9798 - 19235) * b + 16384) >> 15).astype(np.uint8)
+        want[: H // 2] = a[: H // 2]
+    else:
+        ga = np.stack([a, rng.integers(0, 256, (H, W), dtype=np.uint8)], -1)
+        rows, ctype, depth, want = ga.reshape(H, 2 * W), 4, 8, a
+    src = tmp_path / "in.png"
+    src.write_bytes(_png_bytes(rows, W, H, ctype, depth, [0, 1, 2, 3, 4, 4, 3, 1]))
+    if inflate == "zlib":
+        monkeypatch.setenv("OPTFLOW_NO_LIBDEFLATE", "1")
+    out = tmp_path / "out.tif"
+    run("--decode", src, out)
+    assert np.array_equal(np.array(Image.open(out)), want)
