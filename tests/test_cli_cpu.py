@@ -253,3 +253,31 @@ def test_png_every_filter_type(tmp_path, built, kind, inflate, monkeypatch):
     out = tmp_path / "out.tif"
     run("--decode", src, out)
     assert np.array_equal(np.array(Image.open(out)), want)
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_decode_ahead_over_many_chunks(tmp_path, built, threads):
+    """The decode-ahead pool (build-only "decode_threads") across several chunks of pairs:
+    adjacent and strided pairs, repeated slices, different scales and a missing file all come
+    out in pair order with each slice's own size, as the serial loop would give."""
+    rng = np.random.default_rng(12)
+    paths = []
+    for z in range(14):
+        a = rng.integers(0, 256, (20 + z, 30 + 2 * z), dtype=np.uint8)
+        p = tmp_path / f"s{z}.png"
+        Image.fromarray(a).save(p)
+        paths.append(p)
+    imgs = [{"p": str(paths[z]), "q": str(paths[z + 1])} for z in range(13)]
+    imgs += [{"p": str(paths[z]), "q": str(paths[z + 4])} for z in range(0, 10, 3)]
+    imgs += [{"p": str(paths[2]), "q": str(paths[2]), "scale": 0.5},
+             {"p": str(tmp_path / "missing.png"), "q": str(paths[0])},
+             {"p": str(paths[5]), "q": str(paths[6])}]
+    cfg = {"output_dir": str(tmp_path), "scale": 1, "decode_threads": threads, "images": imgs}
+    out = run("--plan", write_cfg(tmp_path, cfg)).stdout
+    assert f"Error: {tmp_path / 'missing.png'}" in out
+    pl = {p["index"]: p for p in json.loads(out[out.index("\n[") + 1:]) if p}   # null: failed
+    assert sorted(pl) == [i for i in range(len(imgs)) if "missing" not in imgs[i]["p"]]
+    for i, p in pl.items():
+        z = int(Path(imgs[i]["p"]).stem[1:])
+        s = imgs[i].get("scale", 1)
+        assert p["size0"] == [round((30 + 2 * z) * s), round((20 + z) * s)], (i, p["size0"])
