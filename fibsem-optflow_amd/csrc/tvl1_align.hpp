@@ -486,7 +486,7 @@ static inline double reproj_err2(const double H[9], const Pt &a, const Pt &b) {
 }
 
 // cv::findHomography(src, dst, method, ransacReprojThreshold) restated: RANSAC (8) or LMEDS
-// (4), <= 2000 iterations with the 0.995-confidence stopping rule, refit on the inliers.
+// (4), iteration counts as OpenCV's registrators (below), refit on the inliers.
 // Deterministic (fixed seed).  Returns false when no model is found.
 static bool find_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, int method,
                             double thresh, double H[9]) {
@@ -499,7 +499,11 @@ static bool find_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, 
   double best[9];
   int best_in = -1;
   double best_med = 1e300;
-  int iters = 2000;
+  // RANSAC: <= 2000 iterations, cut by the 0.995-confidence rule as inliers are found.
+  // LMEDS: OpenCV's LMeDS registrator fixes its count from an assumed outlier ratio of 0.45:
+  // round(log(1 - 0.995) / log(1 - 0.55^4)) = 55 iterations.
+  int iters = lmeds ? (int)std::lround(std::log(1 - 0.995) / std::log(1 - std::pow(1 - 0.45, 4)))
+                    : 2000;
   for (int it = 0; it < iters; ++it) {
     int s[4];
     for (int k = 0; k < 4; ++k) {
