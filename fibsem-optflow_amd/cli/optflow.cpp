@@ -480,15 +480,17 @@ tvl1_align_params align_params_of(const Value &im, const Value &args) {
 // find_alignment(frame1, frame0) + warpAffine(frame1 -> frame0 size) (optflow.cpp:372-376,
 // features.cpp:46-167).  The aligned frame replaces frame1 on the device (and on the host,
 // for the random_points mask), as frame1_GPU = new_frame1 does in the reference.
-bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, ofio::Image8 &f1, const Value &im,
-                  const Value &args, float affine[6], std::string &err) {
+bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1,
+                  ofio::Image8 &aligned, const Value &im, const Value &args, float affine[6],
+                  std::string &err) {
+  const int w1 = f1.width, h1 = f1.height;   // f1 may be `aligned` itself (a second key)
   const int feature_type = im.get("features", Value(args.get("features", Value(2)).asInt())).asInt();
   if (feature_type != 1)   // SURF_TYPE (features.h:9) and anything else
     fprintf(stderr, "SURF features are not part of this build; using ORB features for the "
                     "alignment of %s.\n", im["p"].asString().c_str());
   const tvl1_align_params p = align_params_of(im, args);
   int32_t n_good = 0, outcome = 0;
-  tvl1_status s = tvl1_find_alignment(dc.ctx, dc.d1, (size_t)f1.width, f1.width, f1.height, dc.d0,
+  tvl1_status s = tvl1_find_alignment(dc.ctx, dc.d1, (size_t)w1, w1, h1, dc.d0,
                                       (size_t)f0.width, f0.width, f0.height, &p, affine, &n_good,
                                       &outcome, dc.stream);
   if (s != TVL1_OK) {
@@ -501,16 +503,16 @@ bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, ofio::Image8 &f1, const
   if (outcome == 2)
     printf("More than twenty percent variance in zoom or no homography found, this is probably "
            "an error, ignoring the transformation.\n");
-  s = tvl1_warp_affine_u8(dc.ctx, dc.d1, (size_t)f1.width, f1.width, f1.height, dc.dw,
+  s = tvl1_warp_affine_u8(dc.ctx, dc.d1, (size_t)w1, w1, h1, dc.dw,
                           (size_t)f0.width, f0.width, f0.height, affine, dc.stream);
   if (s != TVL1_OK) {
     err = std::string("warpAffine: ") + tvl1_last_error(dc.ctx);
     return false;
   }
-  f1.width = f0.width;
-  f1.height = f0.height;
-  f1.data.resize((size_t)f0.width * f0.height);
-  if (hipMemcpyAsync(f1.data.data(), dc.dw, f1.data.size(), hipMemcpyDeviceToHost, dc.stream) !=
+  aligned.width = f0.width;
+  aligned.height = f0.height;
+  aligned.data.resize((size_t)f0.width * f0.height);
+  if (hipMemcpyAsync(aligned.data.data(), dc.dw, aligned.data.size(), hipMemcpyDeviceToHost, dc.stream) !=
           hipSuccess ||
       hipStreamSynchronize(dc.stream) != hipSuccess) {
     err = "download of the aligned frame failed";
@@ -522,15 +524,17 @@ bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, ofio::Image8 &f1, const
 }
 
 // solve_rois (optflow.cpp:312-392)
-bool solve_rois(DeviceCtx &dc, ofio::Image8 f0, ofio::Image8 f1, bool f0_resident,
+bool solve_rois(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1_in, bool f0_resident,
                 bool f1_resident, const Value &rois, Value &im, const Value &args,
                 PairResult &res, std::string &err) {
+  ofio::Image8 f1_aligned;               // frame1 after find_alignment + warpAffine
+  const ofio::Image8 *f1p = &f1_in;      // the frame1 the ROIs read: the slice or f1_aligned
   bool features = resolve_features(im, args);
   const std::string otype = output_type_of(im, args);
   // cv::Mat affine(cv::Size(3,2), CV_32FC1) (optflow.cpp:319) is uninitialised until
   // find_alignment fills it; the identity stands in for that here.
   float affine[6] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f};
-  size_t img_bytes = std::max(f0.data.size(), f1.data.size());
+  size_t img_bytes = std::max(f0.data.size(), f1p->data.size());
   size_t flow_bytes = 0;
   for (auto &k : rois.memberNames()) {
     if (k == "custom_diff") {
@@ -549,7 +553,7 @@ bool solve_rois(DeviceCtx &dc, ofio::Image8 f0, ofio::Image8 f1, bool f0_residen
     err = "upload failed";
     return false;
   }
-  if (!f1_resident && hipMemcpyAsync(dc.d1, f1.data.data(), f1.data.size(), hipMemcpyHostToDevice, dc.stream) != hipSuccess) {
+  if (!f1_resident && hipMemcpyAsync(dc.d1, f1p->data.data(), f1p->data.size(), hipMemcpyHostToDevice, dc.stream) != hipSuccess) {
     err = "upload failed";
     return false;
   }
@@ -567,22 +571,23 @@ bool solve_rois(DeviceCtx &dc, ofio::Image8 f0, ofio::Image8 f1, bool f0_residen
         continue;
       }
     } else {
-      const bool size_differs = f0.width != f1.width || f0.height != f1.height;
+      const bool size_differs = f0.width != f1p->width || f0.height != f1p->height;
       if (features || size_differs || key == "default") {   // optflow.cpp:366-377
         if (size_differs || (key == "default" && !features))
           fprintf(stderr, "Rows or columns differ between frames no ROI selected, reverting to "
                           "features even though it wasn't selected.\n");
-        if (!align_frame1(dc, f0, f1, im, args, affine, err)) return false;
+        if (!align_frame1(dc, f0, *f1p, f1_aligned, im, args, affine, err)) return false;
+        f1p = &f1_aligned;
         features = true;
       }
       r0 = r1 = roi_from_array(rois[key]);
     }
-    if (!in_bounds(r0, f0) || !in_bounds(r1, f1)) {
+    if (!in_bounds(r0, f0) || !in_bounds(r1, *f1p)) {
       err = "ROI '" + key + "' is outside the image";
       ok = false;
       continue;
     }
-    if (!solve_wrapper(dc, f0, f1, r0, r1, im, args, features, affine, res, err)) ok = false;
+    if (!solve_wrapper(dc, f0, *f1p, r0, r1, im, args, features, affine, res, err)) ok = false;
   }
   if (otype == "random_points") res.pms.push_back(move_pm(im));
   return ok;
