@@ -1230,6 +1230,18 @@ __device__ __forceinline__ float div_by(float a, const Recip &R) {
   return __builtin_amdgcn_div_fixupf(q, R.d, a);
 }
 
+// Markstein's short quotient: with y = RN(1/d) (recip_of's refined reciprocal; exhaustive
+// over 15 binades in tools/div_check.hip), q0 = RN(a*y), r0 = a - d*q0 (exact) and
+// q1 = RN(q0 + r0*y) is the correctly rounded a / d whenever r0 does not underflow, i.e. for
+// |a| >= 2^-103 when d >= 1 (tools/div_check.hip: 2^32 random quotients in each of the
+// projection's and the TH step's ranges, edge numerators, no mismatch; mismatches start below
+// 2^-103).  Callers send |a| < 2^-100, zero included, through div_by instead.
+__device__ __forceinline__ float div_short(float a, const Recip &R) {
+  const float q0 = a * R.y;
+  const float r0 = __builtin_fmaf(-R.d, q0, a);
+  return __builtin_fmaf(r0, R.y, q0);
+}
+
 // estimateDualVariables for one (u, p*1, p*2) component at one px:
 // p' = (p + taut * du) / ng, du from u at (x+1) and (y+1) (clamped at the image edge).
 // EXACT: plain IEEE divisions, for taut < 0 or non-finite (k_iterate<G, true>; the host
@@ -1256,6 +1268,17 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
   if (EXACT) {
     oa = (pa + taut * ux) / ng;
     ob = (pb + taut * uy) / ng;
+  } else if (BR) {
+    // the short quotient for every lane, then the full sequence only for lanes with a tiny
+    // or zero numerator, in a branch the wavefront skips when it has none
+    const Recip R = recip_of(ng);
+    const float na = pa + taut * ux, nb = pb + taut * uy;
+    oa = div_short(na, R);
+    ob = div_short(nb, R);
+    if (__builtin_fabsf(na) < 0x1p-100f || __builtin_fabsf(nb) < 0x1p-100f) {
+      oa = div_by(na, R);
+      ob = div_by(nb, R);
+    }
   } else {
     const Recip R = recip_of(ng);
     oa = div_by(pa + taut * ux, R);
