@@ -109,7 +109,7 @@ __global__ void kb_warp(BatchWarp w) {
         return Tap3{g.x, g.y, g.z};
       },
       wx, wy, tap_floor(wx), tap_floor(wy), sum, sumx, sumy, wsum);
-  const float coeff = FM ? __builtin_amdgcn_rcpf(wsum) : 1.0f / wsum;
+  const float coeff = FM ? __builtin_amdgcn_rcpf(wsum) : recip_rn(wsum);
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;

@@ -36,6 +36,16 @@ constexpr float kFltEps = 1.1920928955078125e-07f;  // numeric_limits<float>::ep
 __device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
 __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
 
+// RN(1/d): v_rcp_f32 (1 ulp) and one Newton step.  Equal to IEEE 1.0f / d for every
+// significand of the binades 2^-23 .. 2^40 (and 2^50, 2^99, 2^100, 2^120, 2^125), checked
+// exhaustively on gfx950 by tools/div_check.hip test A.  warpBackward's coeff = 1 / wsum has
+// wsum ~ 1 (the Keys weights sum to 1), well inside.
+__device__ __forceinline__ float recip_rn(float d) {
+  const float r = __builtin_amdgcn_rcpf(d);
+  const float e = __builtin_fmaf(-d, r, 1.0f);
+  return __builtin_fmaf(e, r, r);
+}
+
 // XCD-aware tile order (speed only, never correctness).  The dispatcher deals
 // workgroups round-robin over the 8 XCDs (MI355X_MICROARCH: blocks b and b+8 share an
 // XCD), each with its own 4 MiB L2.  Give every XCD a contiguous run of tile slots and
@@ -350,7 +360,7 @@ __global__ void k_warp(const float *__restrict__ I0, const float4 *__restrict__ 
       wsum = wsum + w;
     }
   }
-  const float coeff = 1.0f / wsum;
+  const float coeff = recip_rn(wsum);
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
@@ -531,7 +541,7 @@ __global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
       warp_gather<true>(win, WW, ox, oy, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
     else
       warp_gather<false>(G, P, 0, 0, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
-    const float coeff = 1.0f / wsum;
+    const float coeff = recip_rn(wsum);
     const float I1wv = sum * coeff;
     const float I1wxv = sumx * coeff;
     const float I1wyv = sumy * coeff;
@@ -623,7 +633,7 @@ __device__ __forceinline__ void warp_roll_step(vf4 *__restrict__ ring, const War
                      [&](int cx) { return cx - (x0 - M); }, wx, wy, fx, fy, sum, sumx, sumy, wsum);
   else
     warp_gather<false>(a.G, a.P, 0, 0, a.W, a.H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
-  const float coeff = 1.0f / wsum;
+  const float coeff = recip_rn(wsum);
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
@@ -791,7 +801,7 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
   }
-  const float coeff = 1.0f / wsum;
+  const float coeff = recip_rn(wsum);
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
@@ -969,7 +979,7 @@ __global__ __launch_bounds__(256) void k_warp_img(const float *__restrict__ I0,
       warp_gather<true>(win, kWarpWW, ox, oy, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
     else
       warp_gather_img_global(I1, P, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
-    const float coeff = 1.0f / wsum;
+    const float coeff = recip_rn(wsum);
     const float I1wv = sum * coeff;
     const float I1wxv = sumx * coeff;
     const float I1wyv = sumy * coeff;
@@ -1214,11 +1224,7 @@ __device__ __forceinline__ float hypot_f(float a, float b) { return sqrt_nn<BR>(
 struct Recip {
   float d, y;
 };
-__device__ __forceinline__ Recip recip_of(float d) {
-  const float r = __builtin_amdgcn_rcpf(d);
-  const float e = __builtin_fmaf(-d, r, 1.0f);
-  return Recip{d, __builtin_fmaf(e, r, r)};
-}
+__device__ __forceinline__ Recip recip_of(float d) { return Recip{d, recip_rn(d)}; }
 __device__ __forceinline__ float div_by(float a, const Recip &R) {
   bool scaled;
   const float n = __builtin_amdgcn_div_scalef(a, R.d, true, &scaled);
@@ -2013,7 +2019,7 @@ __device__ __forceinline__ void pass_step(RollPipe<false, 2, 1> &S, float *__res
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
   }
-  const float coeff = 1.0f / wsum;
+  const float coeff = recip_rn(wsum);
   const float I1wv = sum * coeff;
   RollIn<false, 1> in;
   in.wx[0] = sumx * coeff;
@@ -2204,7 +2210,7 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
   }
-  const float coeff = FM ? __builtin_amdgcn_rcpf(wsum) : 1.0f / wsum;
+  const float coeff = FM ? __builtin_amdgcn_rcpf(wsum) : recip_rn(wsum);
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
