@@ -1083,6 +1083,8 @@ __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float
 // tests/test_gpu_parity.py.
 __device__ __forceinline__ float fm_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
+__device__ __forceinline__ float th_quot(float rho, float gradv, bool mid);
+
 // estimateU's TH step at one px: v = u^{n-1} + d from the warp constants (pointwise).
 // CPUP: profile 1 (OpenCV's CPU estimateV): rho = rho_c + (I1wx*u1 + I1wy*u2) [+ gamma*u3]
 template <bool G, bool FM = false, bool CPUP = false>
@@ -1106,7 +1108,7 @@ __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, floa
   const bool hi = rho > a.l_t * gradv;
   const bool mid = gradv > kFltEps;
   // only selected when gradv > FLT_EPSILON
-  const float fi = FM ? -rho * __builtin_amdgcn_rcpf(gradv) : -rho / gradv;
+  const float fi = FM ? -rho * __builtin_amdgcn_rcpf(gradv) : th_quot(rho, gradv, mid);
   float d1 = mid ? fi * I1wxv : 0.0f;
   float d2 = mid ? fi * I1wyv : 0.0f;
   float d3 = mid ? fi * a.gamma : 0.0f;
@@ -1246,6 +1248,19 @@ __device__ __forceinline__ float div_short(float a, const Recip &R) {
   const float q0 = a * R.y;
   const float r0 = __builtin_fmaf(-R.d, q0, a);
   return __builtin_fmaf(r0, R.y, q0);
+}
+
+// The TH step's -rho / grad (selected only where grad > FLT_EPSILON, so grad is in
+// [2^-23, 2^15]: |I1wx|, |I1wy| <= 127.5): the short quotient; the IEEE division for lanes
+// with |rho| < 2^-100 (zero included) behind a wave-uniform branch (a ballot), so the
+// compiler cannot fold it into a select that would run both.  tools/div_check.hip:
+// reciprocal exhaustive over those binades; 2^32 random TH quotients with |a| >= 2^-80 and
+// 2^32 tiny numerators against d in [2^-23, 2^40): mismatches only for |a| < 2^-104.
+__device__ __forceinline__ float th_quot(float rho, float gradv, bool mid) {
+  float fi = div_short(-rho, recip_of(gradv));
+  const bool bad = mid && __builtin_fabsf(rho) < 0x1p-100f;
+  if (__ballot(bad)) fi = bad ? -rho / gradv : fi;
+  return fi;
 }
 
 // estimateDualVariables for one (u, p*1, p*2) component at one px:
