@@ -1297,9 +1297,10 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
     const float na = pa + taut * ux, nb = pb + taut * uy;
     oa = div_short(na, R);
     ob = div_short(nb, R);
-    if (__builtin_fabsf(na) < 0x1p-100f || __builtin_fabsf(nb) < 0x1p-100f) {
-      oa = div_by(na, R);
-      ob = div_by(nb, R);
+    const bool tiny = __builtin_fabsf(na) < 0x1p-100f || __builtin_fabsf(nb) < 0x1p-100f;
+    if (__ballot(tiny)) {
+      oa = tiny ? div_by(na, R) : oa;
+      ob = tiny ? div_by(nb, R) : ob;
     }
   }
 }
