@@ -1110,9 +1110,13 @@ static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n) {
   }
   c->barena_bytes = 0;
   hipError_t e = hipMalloc((void **)&c->barena, bytes);
-  if (e != hipSuccess)
+  if (e != hipSuccess) {
+    (void)hipGetLastError();   // clear the sticky error: the caller may retry smaller
+    c->barena = nullptr;
+    c->bW = c->bH = c->bL = c->bn = 0;
     return set_err(c, TVL1_ENOMEM, "hipMalloc(%zu) for the batch arena failed: %s", bytes,
                    hipGetErrorString(e));
+  }
   c->barena_bytes = bytes;
   HIP_TRY(c, hipMemsetAsync(c->barena, 0, bytes, c->own_stream));   // finite pitch padding
   HIP_TRY(c, hipStreamSynchronize(c->own_stream));
@@ -1898,7 +1902,9 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pi
       chunk = (int)std::max(1.0, std::min((double)kBatchMax, avail / per_pair));
     }
   }
-  for (int b0 = 0; b0 < n; b0 += batched ? chunk : 1) {
+  // other contexts on the device may take memory between hipMemGetInfo and the arena's
+  // hipMalloc: a chunk whose arena does not fit is retried at half the size
+  for (int b0 = 0; b0 < n;) {
     const int m = batched ? std::min(chunk, n - b0) : 1;
     const uint8_t *i0 = I0 + (size_t)b0 * pair_stride0, *i1 = I1 + (size_t)b0 * pair_stride1;
     float *ub = reinterpret_cast<float *>(reinterpret_cast<char *>(u) + (size_t)b0 * flow_pair_stride);
@@ -1908,7 +1914,12 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pi
                                     (hipStream_t)stream)
                 : solve(c, i0, pitch0, i1, pitch1, W, H, ub, vb, fpitch, stats ? stats + b0 : nullptr,
                         (hipStream_t)stream);
+    if (s == TVL1_ENOMEM && batched && m > 1) {
+      chunk = m / 2;
+      continue;
+    }
     if (s != TVL1_OK) return s;
+    b0 += m;
   }
   return TVL1_OK;
 }
