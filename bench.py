@@ -37,13 +37,13 @@ HBM_PEAK_GBS = 8000.0
 
 
 def _traffic():
-    """HBM bytes per iteration-pass launch (k_iterate_roll / k_iterate_tb) measured with
-    rocprofv3 PMC counters (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE;
-    tools/profile.sh + tools/pmc_summary.py), committed under profiles/.  None if not
-    measured."""
+    """PMC-measured HBM bytes per iteration-pass launch (rocprofv3 FETCH_SIZE x 2 per the
+    gfx950 correction + WRITE_SIZE, separate passes, one pair alone: tools/pmc_single.sh +
+    tools/pmc_summary.py --emit-traffic) and the class's VALU utilisation, committed under
+    profiles/ for the engine build the bench runs.  None if not measured."""
     p = ROOT / "profiles" / "traffic.json"
     try:
-        return json.loads(p.read_text())["iterate_hbm_bytes_per_launch"]
+        return json.loads(p.read_text())
     except Exception:
         return None
 
@@ -98,6 +98,10 @@ def parse():
     ap.add_argument("--strides", default="1")
     ap.add_argument("--chunk", type=int, default=8,
                     help="stack: contiguous pairs per work item (slice reuse within it)")
+    ap.add_argument("--dump", default=None,
+                    help="stack: write every pair's flow, per-warp iterations and solving "
+                         "rank to DIR/pair_s<s>_z<z>.npz (tests/test_gpu_stack.py; not timed "
+                         "for the bench line)")
     args = ap.parse_args()
     if args.inflight is None:   # pairs (or strip batches) in flight per GPU
         args.inflight = 2
@@ -108,16 +112,16 @@ def cpu_baseline(I0, I1, params, sample: str):
     """Oracle (CPU restatement of OpenCV 3.4.1 CUDA TV-L1) on the benchmark pair itself (or
     a crop of it, extrapolated by pixel count, with --cpu-sample)."""
     import numpy as np
-    from optflow_amd import capi
+    from oracle import checker   # cpu_baseline leg: the oracle is timed, never the product
     sw, sh = (int(t) for t in sample.lower().split("x"))
     H, W = I0.shape
     sw, sh = min(sw, W), min(sh, H)
     a = np.ascontiguousarray(I0[:sh, :sw])
     b = np.ascontiguousarray(I1[:sh, :sw])
-    lib = capi.load_oracle()
+    lib = checker.load_oracle()
     threads = int(lib.orc_num_threads())
     t0 = time.perf_counter()
-    _, _, st, _ = capi.oracle_calc(a, b, params, warp_iters=False)
+    _, _, st, _ = checker.oracle_calc(a, b, params, warp_iters=False)
     dt = time.perf_counter() - t0
     scale = (W * H) / float(sw * sh)
     return {
@@ -195,9 +199,16 @@ def run_stack(args, rank, world, local_rank, dist):
                     sl = {z: gen.slice(z) for z in range(z0, z1 + s_)}
                 for z in range(z0, z1):
                     r = eng.calc_device(sl[z].data_ptr(), W, sl[z + s_].data_ptr(), W, W, H,
-                                        u[j].data_ptr(), v[j].data_ptr(), 4 * W, stream=st)
+                                        u[j].data_ptr(), v[j].data_ptr(), 4 * W, stream=st,
+                                        warp_iters=bool(args.dump))
                     iters[j] += r["iterations_total"]
                     done[j] += 1
+                    if args.dump:   # correctness runs only (tests/test_gpu_stack.py)
+                        import numpy as np
+                        torch_stream.synchronize()
+                        np.savez(Path(args.dump) / f"pair_s{s_}_z{z}_r{rank}_{j}.npz",
+                                 u=u[j].cpu().numpy(), v=v[j].cpu().numpy(),
+                                 warp_iters=r["warp_iters"], rank=rank, slot=j, item=i)
                 torch_stream.synchronize()
                 del sl
         except Exception as e:   # surfaced below, after the other workers finish
@@ -334,13 +345,14 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
     value = solves / elapsed
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
+        from oracle import checker   # cpu_baseline leg only
         st0 = slots[0]["stack"]
         a, c = st0[0].cpu().numpy(), st0[1].cpu().numpy()
-        lib = capi.load_oracle()
+        lib = checker.load_oracle()
         t1 = time.perf_counter()
         n_rep = 4
         for _ in range(n_rep):
-            capi.oracle_calc(a, c, params, warp_iters=False)
+            checker.oracle_calc(a, c, params, warp_iters=False)
         dt = (time.perf_counter() - t1) / n_rep
         cpu = {"value": round(1.0 / dt, 3), "unit": "strip solves/s",
                "cores": int(lib.orc_num_threads()), "kind": "port",
@@ -541,41 +553,57 @@ def main():
 
     value = world * args.steps * F / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
-    def roofline(k_bytes, k_hbm, k_ms, k_launch, wall_ms):
-        achieved = k_bytes / (k_ms * 1e-3) / 1e9
-        return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": TRAFFIC,
-                "kernel": "iteration passes: estimateU + estimateDualVariables + residual "
-                          "partials, <= 4 iterations per HBM pass (k_iterate_roll wavefront "
-                          "pipeline / k_iterate_tb blocked regions, hybrid; on levels >= 5 Mpx "
-                          "each warp's first pass is k_warp_iter, warpBackward fused in)",
-                "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
-                "algorithmic_bytes_per_launch": round(k_bytes / k_launch),
-                "algorithmic_model": "SURVEY 8(d): 64 B/px per executed iteration "
-                                     "(+ 40 B/px for a fused warpBackward)",
-                # what this kernel must move with its temporal blocking (tile loads incl.
-                # halos + interior stores): the bandwidth-efficiency figure
-                "compulsory_bytes_per_launch": round(k_hbm / k_launch),
-                "compulsory_GBs": round(k_hbm / (k_ms * 1e-3) / 1e9, 1),
-                "compulsory_frac": round(k_hbm / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "kernel_busy_share": round(k_ms / wall_ms, 4),
-                # what actually limits these passes (profiles/r1/valu_util_*):
-                # VALU issue of the exact IEEE division / sqrt sequences, except the
-                # 2-iteration passes, which stream at 3.7-4.5 TB/s
-                "measured_bound": "valu (IEEE div/sqrt sequences; 2-iteration passes hbm)"}
+    def roofline(k_bytes, k_hbm, k_ms, k_launch):
+        """The dominant kernel class (iteration passes, incl. k_warp_iter) against HBM:
+        achieved = the bytes these launches must move (the engine's per-launch accounting of
+        its tiling: tile loads with halos + interior stores, checked against the rocprofv3
+        FETCH_SIZE / WRITE_SIZE pass in profiles/, see `traffic`) / their HIP-event time.
+        SURVEY 8(d)'s one-pass-per-iteration model (64 B/px per iteration) does not describe
+        a temporally blocked kernel (it would exceed the peak), so it is reported beside
+        the fraction as `model_bytes_over_peak`, never as `frac`."""
+        achieved = k_hbm / (k_ms * 1e-3) / 1e9
+        model = k_bytes / (k_ms * 1e-3) / 1e9
+        r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+             "traffic": TRAFFIC.get("iterate_hbm_bytes_per_launch") if TRAFFIC else None,
+             "kernel": "iteration passes: estimateU + estimateDualVariables + residual "
+                       "partials, <= 4 iterations per HBM pass (k_iterate_roll wavefront "
+                       "pipeline / k_iterate_tb blocked regions; on levels >= 5 Mpx each "
+                       "warp's first pass is k_warp_iter, warpBackward fused in)",
+             "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
+             "bytes_per_launch": round(k_hbm / k_launch),
+             "bytes_basis": "engine accounting of the tiling's compulsory HBM bytes (live)",
+             "model_bytes_per_launch": round(k_bytes / k_launch),
+             "model": "SURVEY 8(d): 64 B/px per executed iteration (+ 40 B/px for a fused "
+                      "warpBackward)",
+             "model_bytes_over_peak": round(model / HBM_PEAK_GBS, 4)}
+        if TRAFFIC:
+            r["traffic_source"] = TRAFFIC.get("source")
+            r["traffic_over_bytes"] = round(TRAFFIC["iterate_hbm_bytes_per_launch"] /
+                                            (k_hbm / k_launch), 4)
+            if TRAFFIC.get("iterate_valu_frac") is not None:
+                # SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), same class,
+                # one pair alone (tools/pmc_single.sh + tools/valu_util.py)
+                r["valu_frac"] = TRAFFIC["iterate_valu_frac"]
+        return r
 
+    # the roofline is measured on ONE stream: with F > 1 in flight the launch durations
+    # interleave with the other pair's kernels, so they come from the isolated solve
+    src = iso if iso is not None else None
     roof = None
-    if k_ms > 0:
-        roof = roofline(k_bytes, k_hbm, k_ms, k_launch, 1e3 * elapsed)
-        if F > 1:
-            roof["note"] = (f"{F} pairs in flight: launch durations include interleaving "
-                            f"with the other stream; see roofline_single_stream")
-    roof_iso = None
-    if iso is not None and iso["kernel_ms"][0] > 0:
-        roof_iso = roofline(iso["kernel_bytes"][0], iso["kernel_hbm_bytes"][0],
-                            iso["kernel_ms"][0], iso["kernel_launches"][0],
-                            sum(iso["kernel_ms"][:3]))
-        roof_iso.pop("kernel_busy_share")
+    if src is not None and src["kernel_ms"][0] > 0:
+        roof = roofline(src["kernel_bytes"][0], src["kernel_hbm_bytes"][0], src["kernel_ms"][0],
+                        src["kernel_launches"][0])
+        roof["timing"] = "one pair alone on the GPU (the isolated solve after the timed steps)"
+    elif F == 1 and k_ms > 0:
+        roof = roofline(k_bytes, k_hbm, k_ms, k_launch)
+        roof["timing"] = "every iteration-pass launch of the timed steps (one stream)"
+    roof_inflight = None
+    if F > 1 and k_ms > 0:
+        roof_inflight = roofline(k_bytes, k_hbm, k_ms, k_launch)
+        roof_inflight["note"] = (f"{F} pairs in flight: launch durations overlap the other "
+                                 f"stream's kernels (busy share {k_ms / (1e3 * elapsed):.2f}), so "
+                                 f"this understates per-launch bandwidth")
     out = {
         "metric": METRIC,
         "value": round(value, 4),
@@ -613,7 +641,7 @@ def main():
             "pair_roofline_frac": round(pair_bytes * args.steps * F / elapsed / 1e9 / HBM_PEAK_GBS, 4),
         },
         "roofline": roof,
-        "roofline_single_stream": roof_iso,
+        "roofline_inflight": roof_inflight,
         # per-pair breakdown of one solve alone on the GPU (F > 1: the isolated solve;
         # F == 1: the timed steps)
         "pair_breakdown_ms": None if k_ms <= 0 else (

@@ -14,6 +14,9 @@
 
 namespace ofio {
 
+// The largest image a decoder accepts: the solver's limit (tvl1_calc: W * H <= 2^31).
+constexpr uint64_t kMaxPixels = (uint64_t)1 << 31;
+
 // ------------------------------------------------------------------ files
 bool read_file(const std::string &path, std::string &out, std::string &err, bool gunzip_if_gz) {
   out.clear();
@@ -158,13 +161,24 @@ static bool decode_png(const std::string &buf, Image8 &img, std::string &err) {
     return false;
   }
   int ch;
+  bool depth_ok;   // the PNG specification's allowed bit depths per colour type
   switch (ctype) {
-    case 0: ch = 1; break;
-    case 2: ch = 3; break;
-    case 3: ch = 1; break;
-    case 4: ch = 2; break;
-    case 6: ch = 4; break;
+    case 0: ch = 1; depth_ok = depth == 1 || depth == 2 || depth == 4 || depth == 8 || depth == 16; break;
+    case 2: ch = 3; depth_ok = depth == 8 || depth == 16; break;
+    case 3: ch = 1; depth_ok = depth == 1 || depth == 2 || depth == 4 || depth == 8; break;
+    case 4: ch = 2; depth_ok = depth == 8 || depth == 16; break;
+    case 6: ch = 4; depth_ok = depth == 8 || depth == 16; break;
     default: err = "PNG: bad colour type"; return false;
+  }
+  if (!depth_ok) {
+    err = "PNG: bit depth " + std::to_string(depth) + " is not valid for colour type " +
+          std::to_string(ctype);
+    return false;
+  }
+  // dimensions: at most 2^31 - 1 each (PNG), and an image the solver can take
+  if (W > 0x7fffffffu || H > 0x7fffffffu || (uint64_t)W * H > kMaxPixels) {
+    err = "PNG: image too large (" + std::to_string(W) + "x" + std::to_string(H) + ")";
+    return false;
   }
   const size_t rowbytes = ((size_t)W * ch * depth + 7) / 8;
   const size_t bpp = std::max<size_t>(1, (size_t)ch * depth / 8);
@@ -356,19 +370,30 @@ static bool decode_tiff(const std::string &buf, Image8 &img, std::string &err) {
   uint32_t W = 0, H = 0, bps = 8, comp = 1, photo = 1, spp = 1, rps = 0, planar = 1, pred = 1,
            fmt = 1;
   std::vector<uint32_t> offs, cnts;
+  // an entry's values; false if they do not fit in the file (a count field of up to 2^32
+  // would otherwise allocate that many values)
   auto values = [&](size_t e, std::vector<uint32_t> &v) {
     const uint16_t type = t.u16(e + 2);
     const uint32_t cnt = t.u32(e + 4);
     const size_t sz = type == 3 ? 2 : 4;
-    const size_t base = cnt * sz <= 4 ? e + 8 : t.u32(e + 8);
+    const size_t base = (size_t)cnt * sz <= 4 ? e + 8 : t.u32(e + 8);
+    if (base > t.n || (size_t)cnt * sz > t.n - base) return false;
     v.resize(cnt);
     for (uint32_t i = 0; i < cnt; ++i) v[i] = sz == 2 ? t.u16(base + i * 2) : t.u32(base + i * 4);
+    return true;
   };
+  if ((size_t)ifd + 2 + (size_t)nent * 12 > t.n) {
+    err = "TIFF: IFD out of range";
+    return false;
+  }
   for (uint16_t i = 0; i < nent; ++i) {
     const size_t e = ifd + 2 + (size_t)i * 12;
     const uint16_t tag = t.u16(e);
     std::vector<uint32_t> v;
-    values(e, v);
+    if (!values(e, v)) {
+      err = "TIFF: tag " + std::to_string(tag) + " values out of range";
+      return false;
+    }
     const uint32_t v0 = v.empty() ? 0 : v[0];
     switch (tag) {
       case 256: W = v0; break;
@@ -392,6 +417,10 @@ static bool decode_tiff(const std::string &buf, Image8 &img, std::string &err) {
   }
   if ((bps != 8 && bps != 16) || fmt == 3 || (spp != 1 && spp != 3 && spp != 4) || planar != 1) {
     err = "TIFF: only 8/16-bit integer, 1/3/4 samples, chunky layout supported";
+    return false;
+  }
+  if ((uint64_t)W * H > kMaxPixels) {
+    err = "TIFF: image too large (" + std::to_string(W) + "x" + std::to_string(H) + ")";
     return false;
   }
   if (!rps) rps = H;
@@ -458,6 +487,12 @@ static bool decode_tiff(const std::string &buf, Image8 &img, std::string &err) {
     }
     px.insert(px.end(), strip.begin(), strip.end());
   }
+  // fewer strips than ceil(H / RowsPerStrip): the rows below are missing, not zero
+  if (px.size() < rowbytes * H) {
+    err = "TIFF: strips cover " + std::to_string(rowbytes ? px.size() / rowbytes : 0) + " of " +
+          std::to_string(H) + " rows";
+    return false;
+  }
   img.width = (int)W;
   img.height = (int)H;
   img.data.assign((size_t)W * H, 0);
@@ -509,14 +544,20 @@ static bool decode_pgm(const std::string &buf, Image8 &img, std::string &err) {
         break;
       }
     }
-    int v = 0;
-    while (i < buf.size() && isdigit((unsigned char)buf[i])) v = v * 10 + (buf[i++] - '0');
-    vals[k] = v;
+    long long v = 0;
+    while (i < buf.size() && isdigit((unsigned char)buf[i])) {
+      v = v * 10 + (buf[i++] - '0');
+      if (v > 0x7fffffff) {
+        err = "PGM: header value out of range";
+        return false;
+      }
+    }
+    vals[k] = (int)v;
   }
   ++i;
   const int W = vals[0], H = vals[1], maxv = vals[2];
   const size_t bps = maxv > 255 ? 2 : 1;
-  if (W <= 0 || H <= 0 || buf.size() < i + (size_t)W * H * bps) {
+  if (W <= 0 || H <= 0 || (uint64_t)W * H > kMaxPixels || buf.size() < i + (size_t)W * H * bps) {
     err = "PGM: truncated";
     return false;
   }
@@ -527,7 +568,7 @@ static bool decode_pgm(const std::string &buf, Image8 &img, std::string &err) {
   return true;
 }
 
-bool read_gray8(const std::string &path, Image8 &img, std::string &err) {
+static bool decode_any(const std::string &path, Image8 &img, std::string &err) {
   std::string buf;
   img = Image8();
   if (!read_file(path, buf, err, false)) return false;
@@ -537,6 +578,21 @@ bool read_gray8(const std::string &path, Image8 &img, std::string &err) {
   if (buf.size() >= 2 && buf[0] == 'P' && buf[1] == '5') return decode_pgm(buf, img, err);
   err = "unsupported image format: " + path;
   return false;
+}
+
+// cv::imread returns an empty Mat for any file it cannot decode and the reference skips the
+// pair (optflow.cpp:108-112): no decode failure -- an allocation a corrupt header asks for
+// included -- may escape as an exception (on a decode-pool thread it would terminate the run).
+bool read_gray8(const std::string &path, Image8 &img, std::string &err) {
+  try {
+    const bool ok = decode_any(path, img, err);
+    if (!ok) img = Image8();
+    return ok;
+  } catch (const std::exception &e) {
+    img = Image8();
+    err = "cannot decode " + path + ": " + e.what();
+    return false;
+  }
 }
 
 // ------------------------------------------------------------------ resize

@@ -282,10 +282,25 @@ class Parser {
     if (peek() != c) fail(std::string("expected '") + c + "'");
     ++p_;
   }
+  // nesting bound: a config nested deeper than this is an error, not a stack overflow
+  static constexpr int kMaxDepth = 256;
+  struct Nest {
+    Parser &p;
+    explicit Nest(Parser &pp) : p(pp) {
+      if (++p.depth_ > kMaxDepth) p.fail("nesting deeper than 256 levels");
+    }
+    ~Nest() { --p.depth_; }
+  };
   Value value() {
     const char c = peek();
-    if (c == '{') return object();
-    if (c == '[') return array();
+    if (c == '{') {
+      Nest n(*this);
+      return object();
+    }
+    if (c == '[') {
+      Nest n(*this);
+      return array();
+    }
     if (c == '"') return Value(string());
     if (c == 't' && s_.compare(p_, 4, "true") == 0) { p_ += 4; return Value(true); }
     if (c == 'f' && s_.compare(p_, 5, "false") == 0) { p_ += 5; return Value(false); }
@@ -358,6 +373,18 @@ class Parser {
       o += (char)(0x80 | (cp & 0x3F));
     }
   }
+  unsigned hex4(size_t at) const {
+    if (at + 4 > s_.size()) fail("bad \\u escape");
+    unsigned v = 0;
+    for (size_t i = at; i < at + 4; ++i) {
+      const char h = s_[i];
+      const int d = h >= '0' && h <= '9' ? h - '0' : h >= 'a' && h <= 'f' ? h - 'a' + 10
+                  : h >= 'A' && h <= 'F' ? h - 'A' + 10 : -1;
+      if (d < 0) fail("bad \\u escape");
+      v = v * 16 + (unsigned)d;
+    }
+    return v;
+  }
   std::string string() {
     expect('"');
     std::string o;
@@ -379,12 +406,12 @@ class Parser {
         case 'r': o += '\r'; break;
         case 't': o += '\t'; break;
         case 'u': {
-          if (p_ + 4 > s_.size()) fail("bad \\u escape");
-          unsigned cp = (unsigned)std::stoul(s_.substr(p_, 4), nullptr, 16);
+          unsigned cp = hex4(p_);
           p_ += 4;
           if (cp >= 0xD800 && cp < 0xDC00 && p_ + 6 <= s_.size() && s_[p_] == '\\' &&
               s_[p_ + 1] == 'u') {
-            const unsigned lo = (unsigned)std::stoul(s_.substr(p_ + 2, 4), nullptr, 16);
+            const unsigned lo = hex4(p_ + 2);
+            if (lo < 0xDC00 || lo >= 0xE000) fail("bad \\u surrogate pair");
             p_ += 6;
             cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
           }
@@ -414,17 +441,27 @@ class Parser {
       }
     }
     const std::string t = s_.substr(b, p_ - b);
+    // the whole token must be the number ("-", "1e", "1-2" are errors, not exceptions)
+    size_t used = 0;
     try {
-      if (!real) return Value((int64_t)std::stoll(t));
-      return Value(std::stod(t));
-    } catch (...) {
-      if (!real) return Value(std::stod(t));  // out of int64 range
-      fail("bad number '" + t + "'");
+      if (!real) {
+        const long long i = std::stoll(t, &used);
+        if (used == t.size()) return Value((int64_t)i);
+      }
+    } catch (const std::out_of_range &) {   // out of int64 range: a double
+    } catch (const std::invalid_argument &) {
     }
+    try {
+      const double d = std::stod(t, &used);
+      if (used == t.size()) return Value(d);
+    } catch (const std::exception &) {
+    }
+    fail("bad number '" + t + "'");
   }
 
   const std::string &s_;
   size_t p_ = 0;
+  int depth_ = 0;
 };
 
 inline Value parse(const std::string &text) { return Parser(text).parse(); }

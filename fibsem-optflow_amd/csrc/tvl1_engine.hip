@@ -68,6 +68,9 @@ struct tvl1_ctx {
   double *pinned = nullptr;      // host-pinned residual landing slot (coherent, mapped)
   double *pinned_dev = nullptr;  // its device address: k_reduce stores the residual there
   hipEvent_t ev_check = nullptr;  // recorded after each residual copy
+  hipEvent_t ev_order = nullptr;  // stream-ordered arena release / hand-over (arena_alloc)
+  std::vector<hipStream_t> used_streams;   // streams this ctx enqueued work on since the
+                                           // last arena reallocation
   int speculate = 0;         // TVL1_SPECULATE=1 enables speculative enqueueing (measured slower)
   int iter_mode = 3;         // 0 = temporally blocked passes, 1 = one iteration per launch,
                              // 2 = wavefront-pipelined passes (k_iterate_roll),
@@ -101,6 +104,7 @@ struct tvl1_ctx {
   char *barena = nullptr;
   size_t barena_bytes = 0;
   int bW = 0, bH = 0, bL = 0, bn = 0;   // geometry it is laid out for
+  int bws[TVL1_MAX_LEVELS] = {}, bhs[TVL1_MAX_LEVELS] = {};   // ... and its level sizes
   float *bI0s[TVL1_MAX_LEVELS] = {}, *bI1s[TVL1_MAX_LEVELS] = {};
   size_t bips[TVL1_MAX_LEVELS] = {};    // pair stride of level s image planes (floats)
   float4 *bG = nullptr;
@@ -250,8 +254,54 @@ static int iterate_blocks(int W, int H) {
   return (waves + 3) / 4;
 }
 
-// Carve the arena for a geometry; grows (never shrinks) the device allocation.
-static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
+// The ctx will enqueue work on st: remember it, so a later arena reallocation orders its
+// release after that work.
+static void note_stream(tvl1_ctx *c, hipStream_t st) {
+  for (hipStream_t s : c->used_streams)
+    if (s == st) return;
+  c->used_streams.push_back(st);
+}
+
+// (Re)allocate one of the ctx's scratch arenas in stream order, zero-filled.  The old
+// allocation may still be read by work the ctx enqueued (tvl1_calc is asynchronous): its
+// release waits, on the ctx's own stream, for every stream the ctx used -- never for other
+// contexts' streams (hipDeviceSynchronize or a plain hipFree would drain the whole device,
+// stalling every other pair in flight).  The next work on `use` waits for the zero fill.
+static tvl1_status arena_alloc(tvl1_ctx *c, char **arena, size_t *have, size_t bytes,
+                               hipStream_t use) {
+  hipStream_t own = c->own_stream;
+  if (*arena) {
+    for (hipStream_t s : c->used_streams) {
+      if (s == own) continue;
+      HIP_TRY(c, hipEventRecord(c->ev_order, s));
+      HIP_TRY(c, hipStreamWaitEvent(own, c->ev_order, 0));
+    }
+    HIP_TRY(c, hipFreeAsync(*arena, own));
+    *arena = nullptr;
+    *have = 0;
+  }
+  c->used_streams.clear();
+  hipError_t e = hipMallocAsync((void **)arena, bytes, own);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();   // not sticky: the caller may retry smaller
+    *arena = nullptr;
+    return set_err(c, TVL1_ENOMEM, "hipMallocAsync(%zu) failed: %s", bytes, hipGetErrorString(e));
+  }
+  *have = bytes;
+  // zero once so pitch padding starts finite
+  HIP_TRY(c, hipMemsetAsync(*arena, 0, bytes, own));
+  if (use != own) {
+    HIP_TRY(c, hipEventRecord(c->ev_order, own));
+    HIP_TRY(c, hipStreamWaitEvent(use, c->ev_order, 0));
+  }
+  note_stream(c, use);
+  return TVL1_OK;
+}
+
+// Carve the arena for a geometry; grows (never shrinks) the device allocation.  The
+// calls's work goes to stream st.
+static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H, hipStream_t st) {
+  note_stream(c, st);
   Geometry g;
   g.W = W;
   g.H = H;
@@ -282,23 +332,9 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H) {
   bytes += 4096;                            // alignment slack
 
   if (bytes > c->arena_bytes) {
-    if (c->arena) {
-      // The old arena may still be in use by work on the caller's stream (tvl1_calc
-      // is asynchronous): drain the device before freeing it.
-      HIP_TRY(c, hipDeviceSynchronize());
-      (void)hipFree(c->arena);
-      c->arena = nullptr;
-      c->arena_bytes = 0;
-    }
-    hipError_t e = hipMalloc((void **)&c->arena, bytes);
-    if (e != hipSuccess)
-      return set_err(c, TVL1_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
-    c->arena_bytes = bytes;
-    // Zero once so pitch padding starts finite.  NOT a plain hipMemset: that runs on
-    // the legacy null stream, which does not order against the ctx's non-blocking
-    // stream or the caller's stream, and could land after the solve's kernels.
-    HIP_TRY(c, hipMemsetAsync(c->arena, 0, bytes, c->own_stream));
-    HIP_TRY(c, hipStreamSynchronize(c->own_stream));
+    c->geo_valid = false;
+    const tvl1_status r = arena_alloc(c, &c->arena, &c->arena_bytes, bytes, st);
+    if (r != TVL1_OK) return r;
   }
   char *p = c->arena;
   auto take = [&](size_t n) {
@@ -1087,9 +1123,13 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
 // a warp each pair keeps its own iteration count, stopping-rule state and u / p buffer set,
 // and a pass runs the smallest number of iterations any active pair may fuse before its
 // next check (<= kTbMax), so every pair sees exactly the single-pair schedule.
-static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n) {
+static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n, hipStream_t st) {
   const Geometry &g = c->geo;   // pyramid sizes of (W, H) (ensure_geometry ran)
-  if (c->barena && c->bW == W && c->bH == H && c->bL == g.L && c->bn >= n) return TVL1_OK;
+  // reuse only for the same level sizes: a new scaleStep with the same level count changes
+  // every level's plane stride (c->bips), and the kernels would write past each pair's slot
+  if (c->barena && c->bW == W && c->bH == H && c->bL == g.L && c->bn >= n &&
+      !memcmp(c->bws, g.ws, sizeof(int) * g.L) && !memcmp(c->bhs, g.hs, sizeof(int) * g.L))
+    return TVL1_OK;
   const size_t P0 = (size_t)g.ps[0];
   const size_t ps = align_up(P0 * H, 64);
   // residual partials per pair: blocked regions (56 x 24 px) or rolling / fused waves
@@ -1103,23 +1143,11 @@ static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n) {
   }
   bytes += (ps * n * sizeof(float) + 256) * (4 + 4 + 8 + 3);   // G (float4) + U + P + C
   bytes += (size_t)tb_blocks * n * sizeof(double) + 4096;
-  if (c->barena) {
-    HIP_TRY(c, hipDeviceSynchronize());
-    (void)hipFree(c->barena);
-    c->barena = nullptr;
+  c->bW = c->bH = c->bL = c->bn = 0;
+  {
+    const tvl1_status r = arena_alloc(c, &c->barena, &c->barena_bytes, bytes, st);
+    if (r != TVL1_OK) return r;   // TVL1_ENOMEM: the caller retries a smaller chunk
   }
-  c->barena_bytes = 0;
-  hipError_t e = hipMalloc((void **)&c->barena, bytes);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();   // clear the sticky error: the caller may retry smaller
-    c->barena = nullptr;
-    c->bW = c->bH = c->bL = c->bn = 0;
-    return set_err(c, TVL1_ENOMEM, "hipMalloc(%zu) for the batch arena failed: %s", bytes,
-                   hipGetErrorString(e));
-  }
-  c->barena_bytes = bytes;
-  HIP_TRY(c, hipMemsetAsync(c->barena, 0, bytes, c->own_stream));   // finite pitch padding
-  HIP_TRY(c, hipStreamSynchronize(c->own_stream));
   char *p = c->barena;
   auto take = [&](size_t nbytes) {
     char *r = p;
@@ -1145,6 +1173,8 @@ static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n) {
   c->bH = H;
   c->bL = g.L;
   c->bn = n;
+  memcpy(c->bws, g.ws, sizeof(int) * g.L);
+  memcpy(c->bhs, g.hs, sizeof(int) * g.L);
   return TVL1_OK;
 }
 
@@ -1157,7 +1187,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
   const Geometry &g = c->geo;
   const int L = g.L;
   {
-    const tvl1_status r = ensure_batch(c, W, H, n);
+    const tvl1_status r = ensure_batch(c, W, H, n, st);
     if (r != TVL1_OK) return r;
   }
   const size_t ps = c->bps;
@@ -1783,7 +1813,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
       hipHostMalloc((void **)&c->pinned, sizeof(double) * (8 + kBatchMax),
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&c->pinned_dev, c->pinned, 0) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_check, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_check, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return set_err(nullptr, TVL1_EHIP, "HIP initialisation failed on device %d", device);
   }
@@ -1861,7 +1892,7 @@ tvl1_status tvl1_calc(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8
   tvl1_status s = check_call(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch);
   if (s != TVL1_OK) return s;
   HIP_TRY(c, hipSetDevice(c->device));
-  s = ensure_geometry(c, W, H);
+  s = ensure_geometry(c, W, H, (hipStream_t)stream);
   if (s != TVL1_OK) return s;
   return solve(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch, stats, (hipStream_t)stream);
 }
@@ -1881,7 +1912,7 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pi
                 flow_pair_stride < fpitch * (size_t)H))
     return set_err(c, TVL1_EINVAL, "pair strides must be 0 or cover one image; the flow stride one field");
   HIP_TRY(c, hipSetDevice(c->device));
-  s = ensure_geometry(c, W, H);
+  s = ensure_geometry(c, W, H, (hipStream_t)stream);
   if (s != TVL1_OK) return s;
   const tvl1_params &prm = c->prm;
   const float taut = (float)(prm.tau / prm.theta);
@@ -1965,16 +1996,10 @@ tvl1_status tvl1_find_alignment(tvl1_ctx *c, const uint8_t *frame1, size_t pitch
   AlignCarve cv;
   const size_t need = std::max(align_carve(nullptr, g1, blur, ap->nfeatures, cv),
                                align_carve(nullptr, g0, blur, ap->nfeatures, cv));
+  note_stream(c, st);
   if (need > c->align_bytes) {
-    if (c->align_scratch) {
-      HIP_TRY(c, hipDeviceSynchronize());
-      (void)hipFree(c->align_scratch);
-      c->align_scratch = nullptr;
-      c->align_bytes = 0;
-    }
-    if (hipMalloc((void **)&c->align_scratch, need) != hipSuccess)
-      return set_err(c, TVL1_ENOMEM, "alignment: scratch allocation of %zu bytes failed", need);
-    c->align_bytes = need;
+    const tvl1_status r = arena_alloc(c, &c->align_scratch, &c->align_bytes, need, st);
+    if (r != TVL1_OK) return r;
   }
   static const bool timing = getenv("TVL1_ALIGN_TIMING") != nullptr;
   auto now = [] { return std::chrono::steady_clock::now(); };
@@ -2068,14 +2093,12 @@ tvl1_status tvl1_postprocess_affine(tvl1_ctx *c, float *u, float *v, size_t fp, 
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
   const size_t need = 2 * (size_t)W * H * sizeof(float);
+  note_stream(c, st);
   if (need > c->map_bytes) {
-    if (c->map_scratch) {
-      HIP_TRY(c, hipStreamSynchronize(st));
-      (void)hipFree(c->map_scratch);
-      c->map_scratch = nullptr;
-    }
-    HIP_TRY(c, hipMalloc((void **)&c->map_scratch, need));
-    c->map_bytes = need;
+    char *m = reinterpret_cast<char *>(c->map_scratch);
+    const tvl1_status r = arena_alloc(c, &m, &c->map_bytes, need, st);
+    c->map_scratch = reinterpret_cast<float *>(m);
+    if (r != TVL1_OK) return r;
   }
   float *m1 = c->map_scratch, *m2 = c->map_scratch + (size_t)W * H;
   Affine iM;
@@ -2093,9 +2116,9 @@ tvl1_status tvl1_calc_host(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const 
   tvl1_status s = check_call(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch);
   if (s != TVL1_OK) return s;
   HIP_TRY(c, hipSetDevice(c->device));
-  s = ensure_geometry(c, W, H);
-  if (s != TVL1_OK) return s;
   hipStream_t st = c->own_stream;
+  s = ensure_geometry(c, W, H, st);
+  if (s != TVL1_OK) return s;
   const size_t P0 = (size_t)c->geo.ps[0];
   // GpuMat::upload (optflow.cpp:315-316)
   HIP_TRY(c, hipMemcpy2DAsync(c->in0, P0, I0, pitch0, W, H, hipMemcpyHostToDevice, st));
@@ -2136,15 +2159,25 @@ void tvl1_destroy(tvl1_ctx *c) {
   if (!c) return;
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipSetDevice(c->device);
-  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-  if (c->arena) (void)hipFree(c->arena);
-  if (c->barena) (void)hipFree(c->barena);
-  if (c->map_scratch) (void)hipFree(c->map_scratch);
-  if (c->align_scratch) (void)hipFree(c->align_scratch);
+  // the arenas come from the stream-ordered allocator (arena_alloc): released after every
+  // stream this ctx used, then the ctx's stream is drained
+  if (c->own_stream) {
+    for (hipStream_t s : c->used_streams) {
+      if (s == c->own_stream || !c->ev_order) continue;
+      if (hipEventRecord(c->ev_order, s) == hipSuccess)
+        (void)hipStreamWaitEvent(c->own_stream, c->ev_order, 0);
+    }
+    if (c->arena) (void)hipFreeAsync(c->arena, c->own_stream);
+    if (c->barena) (void)hipFreeAsync(c->barena, c->own_stream);
+    if (c->align_scratch) (void)hipFreeAsync(c->align_scratch, c->own_stream);
+    if (c->map_scratch) (void)hipFreeAsync(c->map_scratch, c->own_stream);
+    (void)hipStreamSynchronize(c->own_stream);
+  }
   if (c->align_pat) (void)hipFree(c->align_pat);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->ev_check) (void)hipEventDestroy(c->ev_check);
+  if (c->ev_order) (void)hipEventDestroy(c->ev_order);
   delete c;
 }
 

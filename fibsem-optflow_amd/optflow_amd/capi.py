@@ -16,7 +16,6 @@ import numpy as np
 PKG_ROOT = Path(__file__).resolve().parent.parent          # fibsem-optflow_amd/
 REPO_ROOT = PKG_ROOT.parent
 ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
-ORACLE_SO = REPO_ROOT / "oracle" / "liboracle_tvl1.so"
 
 TVL1_MAX_LEVELS = 32
 ABI_VERSION = 4          # TVL1_ABI_VERSION of include/tvl1.h
@@ -139,27 +138,13 @@ def _f32_ptr(a: np.ndarray):
 
 
 class Library:
-    """Loads either the HIP engine or the oracle behind the same host call."""
+    """Loads the HIP engine library."""
 
     def __init__(self, path: Path):
         if not Path(path).exists():
             raise FileNotFoundError(f"{path} not built (run __graft_entry__.build())")
         self.path = Path(path)
         self.lib = C.CDLL(str(path))
-
-
-def load_oracle() -> C.CDLL:
-    """TEST INFRASTRUCTURE: the CPU restatement (oracle/).  Only tests, smoke()
-    and bench.py's cpu_baseline leg call this."""
-    lib = Library(ORACLE_SO).lib
-    lib.orc_tvl1_calc.restype = C.c_int
-    lib.orc_tvl1_calc.argtypes = [C.POINTER(TVL1Params), C.POINTER(C.c_uint8), C.c_size_t,
-                                  C.POINTER(C.c_uint8), C.c_size_t, C.c_int, C.c_int,
-                                  C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_size_t,
-                                  C.POINTER(TVL1Stats)]
-    lib.orc_num_threads.restype = C.c_int
-    lib.orc_set_num_threads.argtypes = [C.c_int]
-    return lib
 
 
 def load_engine() -> C.CDLL:
@@ -226,35 +211,6 @@ class TVL1Error(RuntimeError):
     pass
 
 
-def oracle_calc(I0: np.ndarray, I1: np.ndarray, params: TVL1Params | None = None,
-                warp_iters: bool = True, threads: int | None = None):
-    """Run the CPU restatement on host u8 images; returns (u, v, stats, warp_iters)."""
-    lib = load_oracle()
-    if threads:
-        lib.orc_set_num_threads(int(threads))
-    params = params or make_params()
-    I0 = np.ascontiguousarray(I0, dtype=np.uint8)
-    I1 = np.ascontiguousarray(I1, dtype=np.uint8)
-    h, w = I0.shape
-    u = np.zeros((h, w), np.float32)
-    v = np.zeros((h, w), np.float32)
-    st = TVL1Stats()
-    wi = None
-    if warp_iters:
-        cap = TVL1_MAX_LEVELS * max(1, params.warps)
-        wi = np.full(cap, -1, np.int32)
-        st.warp_iterations = wi.ctypes.data_as(C.POINTER(C.c_int32))
-        st.warp_iterations_capacity = cap
-    rc = lib.orc_tvl1_calc(C.byref(params), _u8_ptr(I0), w, _u8_ptr(I1), w, w, h,
-                           _f32_ptr(u), _f32_ptr(v), 4 * w, C.byref(st))
-    if rc != 0:
-        raise TVL1Error(f"oracle: {STATUS.get(rc, rc)}")
-    sd = stats_dict(st)
-    if wi is not None:
-        wi = wi[: sd["levels"] * params.warps].reshape(sd["levels"], params.warps)
-    return u, v, sd, wi
-
-
 class Engine:
     """Host-side handle on the HIP engine (one ctx per device)."""
 
@@ -308,14 +264,27 @@ class Engine:
         return u, v, sd, wi
 
     def calc_device(self, dI0: int, pitch0: int, dI1: int, pitch1: int, w: int, h: int,
-                    du: int, dv: int, flow_pitch: int, stream: int = 0, stats: bool = True):
-        st = TVL1Stats() if stats else None
+                    du: int, dv: int, flow_pitch: int, stream: int = 0, stats: bool = True,
+                    warp_iters: bool = False):
+        st = TVL1Stats() if stats or warp_iters else None
+        wi = None
+        if warp_iters:
+            cap = TVL1_MAX_LEVELS * max(1, self.params.warps)
+            wi = np.full(cap, -1, np.int32)
+            st.warp_iterations = wi.ctypes.data_as(C.POINTER(C.c_int32))
+            st.warp_iterations_capacity = cap
         rc = self.lib.tvl1_calc(self.ctx, C.c_void_p(dI0), pitch0, C.c_void_p(dI1), pitch1,
                                 w, h, C.c_void_p(du), C.c_void_p(dv), flow_pitch,
                                 C.byref(st) if st is not None else None,
                                 C.c_void_p(stream) if stream else None)
         self._check(rc, "tvl1_calc")
-        return stats_dict(st) if st is not None else None
+        if st is None:
+            return None
+        sd = stats_dict(st)
+        if wi is not None:
+            sd["warp_iters"] = wi[: sd["levels"] * self.params.warps].reshape(sd["levels"],
+                                                                              self.params.warps)
+        return sd
 
     def calc_batch_device(self, n: int, dI0: int, pitch0: int, stride0: int, dI1: int,
                           pitch1: int, stride1: int, w: int, h: int, du: int, dv: int,

@@ -16,7 +16,8 @@ def pytest_configure(config):
 def built():
     """Ensure native artefacts exist (build once per session if missing)."""
     from optflow_amd import capi
-    if not capi.ENGINE_SO.exists() or not capi.ORACLE_SO.exists():
+    from oracle import checker
+    if not capi.ENGINE_SO.exists() or not checker.ORACLE_SO.exists():
         import __graft_entry__
         __graft_entry__.build()
     return True

@@ -18,7 +18,9 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "fibsem-optflow_amd"))
-from optflow_amd import capi, synth  # noqa: E402
+sys.path.insert(0, str(ROOT))
+from optflow_amd import capi, synth
+from oracle import checker  # noqa: E402
 
 CASES = {
     "pair_64x48_s5w3": (64, 48, 101, dict(nscales=5, warps=3)),
@@ -35,7 +37,7 @@ def main():
     for name, (W, H, seed, kw) in CASES.items():
         I0, I1 = synth.gen_pair(W, H, seed=seed)
         p = capi.make_params(**kw)
-        u, v, st, wi = capi.oracle_calc(I0, I1, p)
+        u, v, st, wi = checker.oracle_calc(I0, I1, p)
         params = {f: getattr(p, f) for f, _ in capi.TVL1Params._fields_}
         np.savez_compressed(out / f"{name}.npz", I0=I0, I1=I1, u=u, v=v,
                             warp_iters=wi.astype(np.int32), levels=st["levels"],

@@ -10,6 +10,7 @@ import pytest
 from PIL import Image
 
 from optflow_amd import capi, synth
+from oracle import checker
 
 pytestmark = pytest.mark.gpu
 OPTFLOW = capi.PKG_ROOT / "bin" / "optflow"
@@ -24,8 +25,8 @@ def run_cli(cfg, tmp_path, name="cfg.json"):
 
 
 def oracle_post(I0, I1, params, mode):
-    u, v, _, _ = capi.oracle_calc(I0, I1, params, warp_iters=False)
-    lib = capi.load_oracle()
+    u, v, _, _ = checker.oracle_calc(I0, I1, params, warp_iters=False)
+    lib = checker.load_oracle()
     lib.orc_postprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                     C.c_int, C.c_int, C.c_int]
     H, W = I0.shape

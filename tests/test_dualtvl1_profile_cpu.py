@@ -8,13 +8,14 @@ import numpy as np
 import pytest
 
 from optflow_amd import capi, synth
+from oracle import checker
 
 F32P = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
 
 
 @pytest.fixture(scope="module")
 def oracle(built):
-    lib = capi.load_oracle()
+    lib = checker.load_oracle()
     lib.orc_resize_hp.restype = None
     lib.orc_resize_hp.argtypes = [F32P, C.c_int, C.c_int, F32P, C.c_int, C.c_int, C.c_double,
                                   C.c_double, C.c_int]
@@ -85,7 +86,7 @@ def test_remap_outside_is_zero(oracle):
 def test_identity_pair_one_iteration_per_warp(built):
     I0, _ = synth.gen_pair(96, 80, seed=5)
     p = capi.make_params(profile=1, nscales=4, warps=3)
-    u, v, st, wi = capi.oracle_calc(I0, I0, p)
+    u, v, st, wi = checker.oracle_calc(I0, I0, p)
     assert np.all(u == 0) and np.all(v == 0)
     assert np.all(wi == 1)          # the residual is checked at every inner iteration
     assert st["iterations_total"] == st["checks_total"]
@@ -100,7 +101,7 @@ def test_translation_recovered(built):
                                                 mode="nearest")), 0, 255).astype(np.uint8)
     # cv::DualTVL1OpticalFlow defaults: lambda 0.15, nscales 5, warps 5, median 5
     p = capi.make_params(profile=1, nscales=5, warps=5, lambda_=0.15, median_filtering=5)
-    u, v, st, wi = capi.oracle_calc(A, B, p)
+    u, v, st, wi = checker.oracle_calc(A, B, p)
     c = (slice(20, -20), slice(20, -20))
     assert abs(float(np.median(u[c])) - 0.7) < 0.05
     assert abs(float(np.median(v[c])) + 0.4) < 0.05
@@ -111,11 +112,11 @@ def test_schedule_bounds(built):
     I0, I1 = synth.gen_pair(64, 48, seed=7)
     p = capi.make_params(profile=1, nscales=2, warps=2, epsilon=0.0, inner_iterations=3,
                          outer_iterations=2)
-    _, _, st, wi = capi.oracle_calc(I0, I1, p)
+    _, _, st, wi = checker.oracle_calc(I0, I1, p)
     assert np.all(wi == 6)
 
 
 def test_bad_profile_rejected(built):
     I0, I1 = synth.gen_pair(32, 32, seed=1)
     with pytest.raises(Exception):
-        capi.oracle_calc(I0, I1, capi.make_params(profile=3))
+        checker.oracle_calc(I0, I1, capi.make_params(profile=3))

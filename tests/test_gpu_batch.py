@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 from optflow_amd import capi, synth
+from oracle import checker
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -32,7 +33,7 @@ def run_batch(eng, I0s, I1s):
 
 def check_against_oracle(p, I0s, I1s, u, v, st):
     for b in range(I0s.shape[0]):
-        ur, vr, sr, wr = capi.oracle_calc(I0s[b], I1s[b], p)
+        ur, vr, sr, wr = checker.oracle_calc(I0s[b], I1s[b], p)
         assert st[b]["levels"] == sr["levels"]
         np.testing.assert_array_equal(st[b]["warp_iters"], wr, err_msg=f"pair {b}")
         assert bits_equal(u[b], ur) and bits_equal(v[b], vr), f"pair {b} not bit-exact"
@@ -121,7 +122,7 @@ def test_batch_fast_math_within_tolerance(built):
     eng.close()
     p = capi.make_params(**kw)
     for b in range(4):
-        ur, vr, sr, wr = capi.oracle_calc(I0s[b], I1s[b], p)
+        ur, vr, sr, wr = checker.oracle_calc(I0s[b], I1s[b], p)
         np.testing.assert_array_equal(st[b]["warp_iters"], wr)
         e = capi.epe(u[b], v[b], ur, vr)
         assert float(e.mean()) <= 1e-3 and float((e > 1e-2).mean()) <= 1e-3
@@ -201,3 +202,57 @@ def test_batch_shared_reference_frame(built):
     torch.cuda.synchronize()
     eng.close()
     check_against_oracle(p, np.stack([I0] * n), I1s, du.cpu().numpy(), dv.cpu().numpy(), st)
+
+
+def test_batch_arena_relaid_after_scale_step_change(built):
+    """set_params with a new scaleStep but the same level count must
+    re-lay the batch arena -- the level planes grow (0.5 -> 0.8), and a reused arena would
+    let each pair's pyramid spill into its neighbour's planes."""
+    w, h, n = 256, 192, 3
+    I0s, I1s = pairs(n, w, h, seed=91)
+    p05 = capi.make_params(nscales=4, warps=3, scale_step=0.5)
+    p08 = capi.make_params(nscales=4, warps=3, scale_step=0.8)
+    eng = capi.Engine(p05)
+    u, v, st = run_batch(eng, I0s, I1s)
+    check_against_oracle(p05, I0s, I1s, u, v, st)
+    eng.set_params(p08)
+    u, v, st = run_batch(eng, I0s, I1s)
+    assert st[0]["levels"] == 4
+    check_against_oracle(p08, I0s, I1s, u, v, st)
+    for b in range(n):   # and the single-pair path on the same ctx agrees
+        us, vs, ss, ws = eng.calc_host(I0s[b], I1s[b])
+        np.testing.assert_array_equal(st[b]["warp_iters"], ws)
+        assert bits_equal(u[b], us) and bits_equal(v[b], vs)
+    eng.close()
+
+
+def test_arena_growth_keeps_other_contexts_running(built):
+    """Arena growth is stream-ordered (no device-wide drain): a ctx whose arena grows while
+    another ctx's solve is in flight on its own stream leaves both results exact."""
+    pa = capi.make_params(nscales=5, warps=5)
+    ea, eb = capi.Engine(pa), capi.Engine(pa)
+    dev = torch.device("cuda", 0)
+    big0, big1 = synth.gen_pair(1536, 1024, seed=5, z=1)
+    sm0, sm1 = synth.gen_pair(200, 120, seed=6, z=2)
+    lg0, lg1 = synth.gen_pair(700, 500, seed=7, z=3)
+    tb0, tb1 = torch.from_numpy(big0).to(dev), torch.from_numpy(big1).to(dev)
+    ub = torch.zeros((1024, 1536), dtype=torch.float32, device=dev)
+    vb = torch.zeros_like(ub)
+    torch.cuda.synchronize()
+    # ctx b: small solve first (small arena), then grow while ctx a runs the big pair
+    eb.calc_host(sm0, sm1)
+    import threading
+    res = {}
+    t = threading.Thread(target=lambda: res.setdefault(
+        "a", ea.calc_device(tb0.data_ptr(), 1536, tb1.data_ptr(), 1536, 1536, 1024,
+                            ub.data_ptr(), vb.data_ptr(), 4 * 1536, stream=ea.stream)))
+    t.start()
+    ul, vl, sl, wl = eb.calc_host(lg0, lg1)   # grows ctx b's arena
+    t.join()
+    torch.cuda.synchronize()
+    ur, vr, sr, wr = checker.oracle_calc(lg0, lg1, pa)
+    assert bits_equal(ul, ur) and bits_equal(vl, vr)
+    us, vs, ss, ws = ea.calc_host(big0, big1)
+    assert bits_equal(ub.cpu().numpy(), us) and bits_equal(vb.cpu().numpy(), vs)
+    ea.close()
+    eb.close()

@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from optflow_amd import capi, synth
+from oracle import checker
 
 pytestmark = pytest.mark.gpu
 
@@ -46,7 +47,7 @@ def test_engine_matches_oracle(engine, W, H, seed, kw):
     p = capi.make_params(**kw)
     engine.set_params(p)
     u, v, st, wi = engine.calc_host(I0, I1)
-    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    ur, vr, sr, wr = checker.oracle_calc(I0, I1, p)
     assert st["levels"] == sr["levels"]
     assert st["sizes"] == sr["sizes"]
     np.testing.assert_array_equal(wi, wr)
@@ -65,7 +66,7 @@ def test_negative_taut_takes_exact_division_path(engine, tau, theta):
     p = capi.make_params(nscales=3, warps=2, iterations=12, tau=tau, theta=theta)
     engine.set_params(p)
     u, v, _, wi = engine.calc_host(I0, I1)
-    ur, vr, _, wr = capi.oracle_calc(I0, I1, p)
+    ur, vr, _, wr = checker.oracle_calc(I0, I1, p)
     np.testing.assert_array_equal(wi, wr)
     fin = np.isfinite(ur) & np.isfinite(vr)
     assert np.array_equal(fin, np.isfinite(u) & np.isfinite(v))
@@ -138,7 +139,7 @@ def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
     I0, I1 = synth.gen_pair(W, H, seed=seed)
     u, v, st, wi = eng.calc_host(I0, I1)
     eng.close()
-    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    ur, vr, sr, wr = checker.oracle_calc(I0, I1, p)
     np.testing.assert_array_equal(wi, wr)
     assert bits_equal(u, ur) and bits_equal(v, vr)
 
@@ -182,7 +183,7 @@ def test_large_flow_uses_global_gather_fallback(built, monkeypatch, env):
     engine.set_params(p)
     u, v, st, wi = engine.calc_host(I0, I1)
     engine.close()
-    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    ur, vr, sr, wr = checker.oracle_calc(I0, I1, p)
     assert float(np.abs(ur).max()) > 5.0   # the case really leaves the window
     np.testing.assert_array_equal(wi, wr)
     assert bits_equal(u, ur) and bits_equal(v, vr)
@@ -195,7 +196,7 @@ def test_benchmark_pair_bit_exact(engine):
     p = capi.make_params(nscales=5, warps=30)
     engine.set_params(p)
     u, v, st, wi = engine.calc_host(I0, I1)
-    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    ur, vr, sr, wr = checker.oracle_calc(I0, I1, p)
     assert st["levels"] == sr["levels"] == 5
     np.testing.assert_array_equal(wi, wr)
     assert bits_equal(u, ur) and bits_equal(v, vr)
@@ -222,7 +223,7 @@ def test_dualtvl1_profile_matches_oracle(engine, W, H, seed, kw):
     p = capi.make_params(profile=1, **kw)
     engine.set_params(p)
     u, v, st, wi = engine.calc_host(I0, I1)
-    ur, vr, sr, wr = capi.oracle_calc(I0, I1, p)
+    ur, vr, sr, wr = checker.oracle_calc(I0, I1, p)
     assert st["levels"] == sr["levels"]
     np.testing.assert_array_equal(wi, wr)
     fin = np.isfinite(ur) & np.isfinite(vr)

@@ -1,0 +1,225 @@
+"""Malformed-input tests for the host decoders the CLI ships (cli/imageio.cpp PNG / TIFF /
+PGM, cli/json.hpp): every corrupt or hostile file must give an error message and a clean
+non-zero exit from `optflow --decode`, never a crash, a hang or an unbounded allocation.
+The reference's cv::imread returns an empty Mat and the pair is skipped
+(/root/reference/src/optflow.cpp:108-112); a bad config is reported with its position.
+The same suite runs under ASan + UBSan with `make -C fibsem-optflow_amd asan`
+(OPTFLOW_BIN=fibsem-optflow_amd/bin/optflow_asan)."""
+import os
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from optflow_amd import capi
+
+BINS = {"release": capi.PKG_ROOT / "bin" / "optflow",
+        "asan": capi.PKG_ROOT / "bin" / "optflow_asan"}   # make -C fibsem-optflow_amd asan
+_bin = [str(BINS["release"])]
+
+
+@pytest.fixture(autouse=True, params=["release", "asan"])
+def optflow_bin(request, built):
+    path = BINS[request.param]
+    if request.param == "asan" and not path.exists():
+        r = subprocess.run(["make", "-C", str(capi.PKG_ROOT), "asan"], capture_output=True, text=True)
+        if r.returncode != 0:
+            pytest.skip("ASan/UBSan build unavailable: " + r.stderr[-300:])
+    _bin[0] = os.environ.get("OPTFLOW_BIN", str(path))
+    yield
+
+
+def run(*args):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=99",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=98")
+    r = subprocess.run([_bin[0], *map(str, args)], capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode not in (98, 99), r.stderr
+    assert r.returncode >= 0, f"optflow killed by signal {-r.returncode}: {r.stderr}"
+    assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr
+    return r
+
+
+def decode_fails(tmp_path, data, expect=None, name="bad.bin"):
+    src = tmp_path / name
+    src.write_bytes(data)
+    r = run("--decode", src, tmp_path / "out.tif")
+    assert r.returncode == 1, (r.returncode, r.stderr)
+    if expect:
+        assert expect in r.stderr, r.stderr
+    return r
+
+
+def chunk(t, d):
+    return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+
+
+def png(w, h, depth, ctype, raw=None, interlace=0):
+    ihdr = struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, interlace)
+    if raw is None:
+        raw = b"\0" * ((w * depth + 7) // 8 + 1) * min(h, 4)
+    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", zlib.compress(raw))
+            + chunk(b"IEND", b""))
+
+
+@pytest.fixture
+def good_png(tmp_path, built):
+    a = np.random.default_rng(1).integers(0, 256, (40, 50), dtype=np.uint8)
+    p = tmp_path / "good.png"
+    Image.fromarray(a).save(p)
+    return p.read_bytes()
+
+
+@pytest.mark.parametrize("depth,ctype", [(0, 0), (3, 0), (32, 0), (4, 2), (16, 3), (1, 4), (2, 6)])
+def test_png_illegal_bit_depth(tmp_path, built, depth, ctype):
+    """Depth 0 on gray used to divide by zero; other illegal depths shifted by negative
+    amounts."""
+    decode_fails(tmp_path, png(8, 8, depth, ctype), "bit depth")
+
+
+@pytest.mark.parametrize("w,h", [(0x7fffffff, 0x7fffffff), (0xffffffff, 1), (1 << 20, 1 << 20)])
+def test_png_huge_dimensions(tmp_path, built, w, h):
+    """(rowbytes + 1) * H could wrap; W * H beyond the solver's limit is refused up front."""
+    decode_fails(tmp_path, png(w, h, 8, 0), "too large")
+
+
+def test_png_truncated_file(tmp_path, good_png):
+    for cut in (len(good_png) // 2, 40, 20, 9):
+        decode_fails(tmp_path, good_png[:cut])
+
+
+def test_png_corrupt_idat(tmp_path, good_png):
+    b = bytearray(good_png)
+    i = b.index(b"IDAT") + 8
+    for k in range(i, min(i + 40, len(b) - 16)):
+        b[k] ^= 0x5A
+    src = tmp_path / "c.png"
+    src.write_bytes(bytes(b))
+    r = run("--decode", src, tmp_path / "o.tif")
+    assert r.returncode in (0, 1)   # zlib may or may not detect it; no crash either way
+
+
+def test_png_bad_filter_and_palette(tmp_path, built):
+    raw = b"".join(b"\x07" + b"\0" * 8 for _ in range(8))   # filter type 7
+    decode_fails(tmp_path, png(8, 8, 8, 0, raw=raw), "filter")
+    raw = b"".join(b"\0" + bytes(range(200, 208)) for _ in range(8))   # no PLTE chunk
+    decode_fails(tmp_path, png(8, 8, 8, 3, raw=raw), "palette")
+
+
+def test_png_missing_ihdr_and_interlace(tmp_path, built):
+    decode_fails(tmp_path, b"\x89PNG\r\n\x1a\n" + chunk(b"IEND", b""), "IHDR")
+    decode_fails(tmp_path, png(8, 8, 8, 0, interlace=1), "interlaced")
+
+
+def tiff(w, h, rows_per_strip, strips, bps=8, comp=1, count_override=None, extra=()):
+    """A little-endian baseline TIFF: one IFD, the strips' data after it."""
+    entries = []
+    data = b"".join(strips)
+    n_ent = 9 + len(extra)
+    ifd_off = 8
+    data_off = ifd_off + 2 + 12 * n_ent + 4
+    offs_arr = data_off + len(data)
+    cnts_arr = offs_arr + 4 * len(strips)
+    offs, o = [], data_off
+    for s in strips:
+        offs.append(o)
+        o += len(s)
+
+    def ent(tag, typ, cnt, val):
+        entries.append(struct.pack("<HHII", tag, typ, cnt, val))
+
+    ent(256, 4, 1, w)
+    ent(257, 4, 1, h)
+    ent(258, 3, 1, bps)
+    ent(259, 3, 1, comp)
+    ent(262, 3, 1, 1)
+    ns = len(strips)
+    ent(273, 4, count_override or ns, offs[0] if ns == 1 else offs_arr)
+    ent(277, 3, 1, 1)
+    ent(278, 4, 1, rows_per_strip)
+    ent(279, 4, ns, len(strips[0]) if ns == 1 else cnts_arr)
+    for e in extra:
+        ent(*e)
+    out = b"II*\0" + struct.pack("<I", ifd_off) + struct.pack("<H", n_ent) + b"".join(entries)
+    out += b"\0\0\0\0" + data
+    if ns > 1:
+        out += struct.pack(f"<{ns}I", *offs) + struct.pack(f"<{ns}I", *[len(s) for s in strips])
+    return out
+
+
+def test_tiff_valid_multi_strip_decodes(tmp_path, built):
+    a = np.random.default_rng(2).integers(0, 256, (12, 10), dtype=np.uint8)
+    strips = [a[i:i + 4].tobytes() for i in range(0, 12, 4)]
+    src = tmp_path / "ok.tif"
+    src.write_bytes(tiff(10, 12, 4, strips))
+    r = run("--decode", src, tmp_path / "o.tif")
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(np.array(Image.open(tmp_path / "o.tif")), a)
+
+
+def test_tiff_fewer_strips_than_rows(tmp_path, built):
+    """2 strips of 4 rows for a 12-row image used to read past the strip buffer."""
+    a = np.zeros((12, 10), np.uint8)
+    decode_fails(tmp_path, tiff(10, 12, 4, [a[:4].tobytes(), a[4:8].tobytes()]), "strips cover")
+
+
+def test_tiff_huge_count_field(tmp_path, built):
+    """A StripOffsets count of 2^32 - 1 used to allocate that many values (bad_alloc on a
+    decode thread -> std::terminate)."""
+    a = np.zeros((4, 4), np.uint8)
+    decode_fails(tmp_path, tiff(4, 4, 4, [a.tobytes()], count_override=0xFFFFFFFF), "out of range")
+
+
+def test_tiff_strip_out_of_range_and_bad_ifd(tmp_path, built):
+    a = np.zeros((4, 4), np.uint8)
+    t = bytearray(tiff(4, 4, 4, [a.tobytes()]))
+    t = t[:-8]   # the strip runs past the end of the file
+    decode_fails(tmp_path, bytes(t))
+    decode_fails(tmp_path, b"II*\0" + struct.pack("<I", 0x7FFFFFF0) + b"\0" * 8, "IFD")
+
+
+def test_tiff_huge_dimensions(tmp_path, built):
+    decode_fails(tmp_path, tiff(1 << 20, 1 << 20, 1, [b"\0" * 16]), "too large")
+
+
+@pytest.mark.parametrize("comp", [5, 8, 32773])
+def test_tiff_corrupt_compressed_strip(tmp_path, built, comp):
+    """Garbage LZW / deflate / PackBits data: an error or a clean (zero-filled) decode."""
+    junk = bytes(np.random.default_rng(comp).integers(0, 256, 64, dtype=np.uint8))
+    src = tmp_path / "j.tif"
+    src.write_bytes(tiff(16, 16, 16, [junk], comp=comp))
+    r = run("--decode", src, tmp_path / "o.tif")
+    assert r.returncode in (0, 1), r.stderr
+
+
+def test_pgm_malformed(tmp_path, built):
+    decode_fails(tmp_path, b"P5\n99999999999999999999 2\n255\n", "out of range")
+    decode_fails(tmp_path, b"P5\n100 100\n255\n" + b"\0" * 10, "truncated")
+    decode_fails(tmp_path, b"P5\n65536 65536\n255\n" + b"\0" * 10)
+
+
+def write_cfg(tmp_path, text):
+    p = tmp_path / "cfg.json"
+    p.write_text(text)
+    return p
+
+
+@pytest.mark.parametrize("text,what", [
+    ("[" * 5000 + "]" * 5000, "nesting"),
+    ('{"a": "\\uZZZZ"}', "escape"),
+    ('{"a": "\\u12"}', "escape"),
+    ('{"a": -}', "bad number"),
+    ('{"a": 1e}', "bad number"),
+    ('{"a": 1-2}', "bad number"),
+    ('{"a": "unterminated', "unterminated"),
+    ('{"a": 1 /* open comment', "comment"),
+    ('{"a": "\\ud800\\u0041"}', "surrogate"),
+    ("", "unexpected"),
+], ids=["deep", "hex", "short-hex", "minus", "exp", "minus-mid", "unterminated", "comment",
+        "surrogate", "empty"])
+def test_malformed_json_configs(tmp_path, built, text, what):
+    r = run(write_cfg(tmp_path, text))
+    assert r.returncode == 2 and what in r.stderr, (r.returncode, r.stderr)

@@ -12,13 +12,14 @@ import numpy as np
 import pytest
 
 from optflow_amd import capi, synth
+from oracle import checker
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
 
 
 @pytest.fixture(scope="module")
 def oracle(built):
-    lib = capi.load_oracle()
+    lib = checker.load_oracle()
     lib.orc_pyramid_sizes.restype = C.c_int
     lib.orc_pyramid_sizes.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double,
                                       C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -54,7 +55,7 @@ def test_pyramid_sizes_512_and_stop_rule(oracle):
 
 def test_identity_pair_is_exactly_zero(built):
     I0, _ = synth.gen_pair(72, 50, seed=5)
-    u, v, st, wi = capi.oracle_calc(I0, I0, capi.make_params(nscales=4, warps=3))
+    u, v, st, wi = checker.oracle_calc(I0, I0, capi.make_params(nscales=4, warps=3))
     assert np.all(u == 0) and np.all(v == 0)
     assert np.all(wi == 2)      # n = 0 no check, n = 1 check -> error 0 -> stop
 
@@ -62,7 +63,7 @@ def test_identity_pair_is_exactly_zero(built):
 def test_constant_images_zero_flow(built):
     I0 = np.full((33, 47), 90, np.uint8)
     I1 = np.full((33, 47), 130, np.uint8)
-    u, v, _, _ = capi.oracle_calc(I0, I1, capi.make_params(nscales=3, warps=2))
+    u, v, _, _ = checker.oracle_calc(I0, I1, capi.make_params(nscales=3, warps=2))
     assert np.all(u == 0) and np.all(v == 0)
 
 
@@ -75,7 +76,7 @@ def test_recovers_known_translation(built, dx, dy):
     I0 = np.clip(np.rint(base), 0, 255).astype(np.uint8)
     I1 = np.clip(np.rint(ndimage.map_coordinates(base, [ys - dy, xs - dx], order=3,
                                                  mode="nearest")), 0, 255).astype(np.uint8)
-    u, v, _, _ = capi.oracle_calc(I0, I1, capi.make_params(nscales=5, warps=5))
+    u, v, _, _ = checker.oracle_calc(I0, I1, capi.make_params(nscales=5, warps=5))
     c = np.s_[16:-16, 16:-16]
     assert abs(float(np.median(u[c])) - dx) < 0.05
     assert abs(float(np.median(v[c])) - dy) < 0.05
@@ -83,13 +84,13 @@ def test_recovers_known_translation(built, dx, dy):
 
 def test_fixed_work_mode_runs_exact_iteration_count(built):
     I0, I1 = synth.gen_pair(64, 48, seed=2)
-    _, _, st, wi = capi.oracle_calc(I0, I1, capi.make_params(nscales=3, warps=2, epsilon=0.0,
+    _, _, st, wi = checker.oracle_calc(I0, I1, capi.make_params(nscales=3, warps=2, epsilon=0.0,
                                                              iterations=7))
     assert np.all(wi == 7) and st["checks_total"] == 0
 
 
 def test_invalid_params_rejected(built):
-    lib = capi.load_oracle()
+    lib = checker.load_oracle()
     I0 = np.zeros((8, 8), np.uint8)
     u = np.zeros((8, 8), np.float32)
     p = capi.make_params(nscales=0)
@@ -101,8 +102,8 @@ def test_invalid_params_rejected(built):
 def test_thread_count_does_not_change_results(built):
     I0, I1 = synth.gen_pair(96, 80, seed=12)
     p = capi.make_params(nscales=4, warps=4)
-    a = capi.oracle_calc(I0, I1, p, threads=1)
-    b = capi.oracle_calc(I0, I1, p, threads=4)
+    a = checker.oracle_calc(I0, I1, p, threads=1)
+    b = checker.oracle_calc(I0, I1, p, threads=4)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
     assert np.array_equal(a[3], b[3])
 
@@ -111,7 +112,7 @@ def test_thread_count_does_not_change_results(built):
 def test_oracle_reproduces_golden(built, path):
     g = np.load(path, allow_pickle=False)
     params = capi.make_params(**json.loads(str(g["params"])))
-    u, v, st, wi = capi.oracle_calc(g["I0"], g["I1"], params)
+    u, v, st, wi = checker.oracle_calc(g["I0"], g["I1"], params)
     assert st["levels"] == int(g["levels"])
     np.testing.assert_array_equal(wi, g["warp_iters"])
     assert np.array_equal(u, g["u"]) and np.array_equal(v, g["v"])
@@ -119,7 +120,7 @@ def test_oracle_reproduces_golden(built, path):
 
 def test_postprocess_semantics(built):
     """solve_wrapper post-ops: map adds the pixel grid, mask zeroes where I1 <= 1."""
-    lib = capi.load_oracle()
+    lib = checker.load_oracle()
     lib.orc_postprocess.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                     C.c_int, C.c_int, C.c_int]
     H, W = 5, 7
@@ -135,3 +136,17 @@ def test_postprocess_semantics(built):
     exp_u[I1 <= 1] = 0
     exp_v[I1 <= 1] = 0
     assert np.array_equal(u, exp_u) and np.array_equal(v, exp_v)
+
+
+def test_oracle_under_asan_ubsan():
+    """The restatement itself under ASan + UBSan (`make -C oracle asan`): every path --
+    both profiles, gamma, median, fixed work, a 1x1 and a bottomed-out pyramid."""
+    import subprocess
+    root = Path(__file__).resolve().parent.parent / "oracle"
+    r = subprocess.run(["make", "-C", str(root), "asan"], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("ASan/UBSan build unavailable: " + r.stderr[-300:])
+    r = subprocess.run([str(root / "_asan" / "orc_asan")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "0 failures" in r.stdout, r.stdout + r.stderr
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr

@@ -80,6 +80,12 @@ def main():
             hb = sum(out[k]["hbm_bytes_per_dispatch"] * out[k]["dispatches"] for k in ks) / n
             res["hbm_bytes_per_dispatch"] = round(hb)
             res["hbm_GBs_at_trace_avg"] = round(hb / (tot_ns / max(1, ndur)), 1)
+            res["hbm_frac_of_8TBs"] = round(hb / (tot_ns / max(1, ndur)) / 8000.0, 4)
+        # VALU issue utilisation: SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+        if all("SQ_INSTS_VALU" in ctr[k] and "GRBM_GUI_ACTIVE" in ctr[k] for k in ks):
+            valu = sum(ctr[k]["SQ_INSTS_VALU"] for k in ks)
+            gui = sum(ctr[k]["GRBM_GUI_ACTIVE"] for k in ks) / 8.0
+            res["valu_frac"] = round(valu * 2 / (1024 * gui), 4) if gui else None
         classes[cls] = res
     out["classes"] = classes
     print(json.dumps(out, indent=1))
@@ -88,10 +94,14 @@ def main():
     if "--emit-traffic" in sys.argv and "hbm_bytes_per_dispatch" in it:
         path = sys.argv[sys.argv.index("--emit-traffic") + 1]
         json.dump({"iterate_hbm_bytes_per_launch": it["hbm_bytes_per_dispatch"],
+                   "iterate_avg_us_trace": it["avg_us_trace"],
+                   "iterate_hbm_frac_of_8TBs": it.get("hbm_frac_of_8TBs"),
+                   "iterate_valu_frac": it.get("valu_frac"),
                    "iterate_kernels": it["kernels"], "dispatches": it["dispatches"],
                    "warp_hbm_bytes_per_launch": classes.get("warp", {}).get("hbm_bytes_per_dispatch"),
                    "source": d, "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
-                   "separate passes, average over every iteration-pass dispatch of the bench run"},
+                   "separate passes, average over every iteration-pass dispatch of one pair "
+                   "alone (tools/pmc_single.sh); valu_frac from the SQ_INSTS_VALU pass"},
                   open(path, "w"), indent=1)
 
 
