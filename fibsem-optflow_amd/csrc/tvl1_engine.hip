@@ -68,9 +68,8 @@ struct tvl1_ctx {
   double *pinned = nullptr;      // host-pinned residual landing slot (coherent, mapped)
   double *pinned_dev = nullptr;  // its device address: k_reduce stores the residual there
   hipEvent_t ev_check = nullptr;  // recorded after each residual copy
-  hipEvent_t ev_order = nullptr;  // stream-ordered arena release / hand-over (arena_alloc)
-  std::vector<hipStream_t> used_streams;   // streams this ctx enqueued work on since the
-                                           // last arena reallocation
+  hipEvent_t ev_order = nullptr;  // orders work on the caller's stream after a zero fill
+  std::vector<char *> retired;    // arenas outgrown while possibly in use (arena_alloc)
   int speculate = 0;         // TVL1_SPECULATE=1 enables speculative enqueueing (measured slower)
   int iter_mode = 3;         // 0 = temporally blocked passes, 1 = one iteration per launch,
                              // 2 = wavefront-pipelined passes (k_iterate_roll),
@@ -254,54 +253,50 @@ static int iterate_blocks(int W, int H) {
   return (waves + 3) / 4;
 }
 
-// The ctx will enqueue work on st: remember it, so a later arena reallocation orders its
-// release after that work.
-static void note_stream(tvl1_ctx *c, hipStream_t st) {
-  for (hipStream_t s : c->used_streams)
-    if (s == st) return;
-  c->used_streams.push_back(st);
-}
-
-// (Re)allocate one of the ctx's scratch arenas in stream order, zero-filled.  The old
-// allocation may still be read by work the ctx enqueued (tvl1_calc is asynchronous): its
-// release waits, on the ctx's own stream, for every stream the ctx used -- never for other
-// contexts' streams (hipDeviceSynchronize or a plain hipFree would drain the whole device,
-// stalling every other pair in flight).  The next work on `use` waits for the zero fill.
+// (Re)allocate one of the ctx's scratch arenas, zero-filled, for work on stream `use`.
+// The old allocation may still be read by work the ctx enqueued (tvl1_calc is
+// asynchronous), and hipFree would wait for every stream on the device -- every other
+// context's pair in flight.  So the old arena is retired, not freed: it is released at
+// tvl1_destroy.  Growth therefore never drains the device; a ctx holds at most the sizes it
+// grew through (one growth in the usual fixed-size workloads).  The work on `use` is
+// ordered after the zero fill by an event, not by a host wait.  (The stream-ordered
+// allocator, hipMallocAsync / hipFreeAsync, would release in stream order too, but it
+// deadlocked against a concurrent hipStreamDestroy on this ROCm, so it is not used.)
 static tvl1_status arena_alloc(tvl1_ctx *c, char **arena, size_t *have, size_t bytes,
                                hipStream_t use) {
-  hipStream_t own = c->own_stream;
   if (*arena) {
-    for (hipStream_t s : c->used_streams) {
-      if (s == own) continue;
-      HIP_TRY(c, hipEventRecord(c->ev_order, s));
-      HIP_TRY(c, hipStreamWaitEvent(own, c->ev_order, 0));
-    }
-    HIP_TRY(c, hipFreeAsync(*arena, own));
+    c->retired.push_back(*arena);
     *arena = nullptr;
     *have = 0;
   }
-  c->used_streams.clear();
-  hipError_t e = hipMallocAsync((void **)arena, bytes, own);
+  hipError_t e = hipMalloc((void **)arena, bytes);
+  if (e != hipSuccess && !c->retired.empty()) {
+    // out of memory with outgrown arenas held: release them (hipFree waits for the device;
+    // a rare path, better than failing) and try once more
+    (void)hipGetLastError();
+    for (char *r : c->retired) (void)hipFree(r);
+    c->retired.clear();
+    e = hipMalloc((void **)arena, bytes);
+  }
   if (e != hipSuccess) {
     (void)hipGetLastError();   // not sticky: the caller may retry smaller
     *arena = nullptr;
-    return set_err(c, TVL1_ENOMEM, "hipMallocAsync(%zu) failed: %s", bytes, hipGetErrorString(e));
+    return set_err(c, TVL1_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
   }
   *have = bytes;
-  // zero once so pitch padding starts finite
-  HIP_TRY(c, hipMemsetAsync(*arena, 0, bytes, own));
-  if (use != own) {
-    HIP_TRY(c, hipEventRecord(c->ev_order, own));
+  // zero once so pitch padding starts finite (hipMemsetAsync on the ctx's stream: a plain
+  // hipMemset runs on the legacy null stream, unordered with non-blocking streams)
+  HIP_TRY(c, hipMemsetAsync(*arena, 0, bytes, c->own_stream));
+  if (use != c->own_stream) {
+    HIP_TRY(c, hipEventRecord(c->ev_order, c->own_stream));
     HIP_TRY(c, hipStreamWaitEvent(use, c->ev_order, 0));
   }
-  note_stream(c, use);
   return TVL1_OK;
 }
 
 // Carve the arena for a geometry; grows (never shrinks) the device allocation.  The
 // calls's work goes to stream st.
 static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H, hipStream_t st) {
-  note_stream(c, st);
   Geometry g;
   g.W = W;
   g.H = H;
@@ -1996,7 +1991,6 @@ tvl1_status tvl1_find_alignment(tvl1_ctx *c, const uint8_t *frame1, size_t pitch
   AlignCarve cv;
   const size_t need = std::max(align_carve(nullptr, g1, blur, ap->nfeatures, cv),
                                align_carve(nullptr, g0, blur, ap->nfeatures, cv));
-  note_stream(c, st);
   if (need > c->align_bytes) {
     const tvl1_status r = arena_alloc(c, &c->align_scratch, &c->align_bytes, need, st);
     if (r != TVL1_OK) return r;
@@ -2093,7 +2087,6 @@ tvl1_status tvl1_postprocess_affine(tvl1_ctx *c, float *u, float *v, size_t fp, 
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
   const size_t need = 2 * (size_t)W * H * sizeof(float);
-  note_stream(c, st);
   if (need > c->map_bytes) {
     char *m = reinterpret_cast<char *>(c->map_scratch);
     const tvl1_status r = arena_alloc(c, &m, &c->map_bytes, need, st);
@@ -2159,20 +2152,13 @@ void tvl1_destroy(tvl1_ctx *c) {
   if (!c) return;
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipSetDevice(c->device);
-  // the arenas come from the stream-ordered allocator (arena_alloc): released after every
-  // stream this ctx used, then the ctx's stream is drained
-  if (c->own_stream) {
-    for (hipStream_t s : c->used_streams) {
-      if (s == c->own_stream || !c->ev_order) continue;
-      if (hipEventRecord(c->ev_order, s) == hipSuccess)
-        (void)hipStreamWaitEvent(c->own_stream, c->ev_order, 0);
-    }
-    if (c->arena) (void)hipFreeAsync(c->arena, c->own_stream);
-    if (c->barena) (void)hipFreeAsync(c->barena, c->own_stream);
-    if (c->align_scratch) (void)hipFreeAsync(c->align_scratch, c->own_stream);
-    if (c->map_scratch) (void)hipFreeAsync(c->map_scratch, c->own_stream);
-    (void)hipStreamSynchronize(c->own_stream);
-  }
+  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+  // hipFree waits for the device: callers' streams included
+  if (c->arena) (void)hipFree(c->arena);
+  if (c->barena) (void)hipFree(c->barena);
+  if (c->align_scratch) (void)hipFree(c->align_scratch);
+  if (c->map_scratch) (void)hipFree(c->map_scratch);
+  for (char *r : c->retired) (void)hipFree(r);
   if (c->align_pat) (void)hipFree(c->align_pat);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
