@@ -50,6 +50,8 @@ def _traffic():
 
 TRAFFIC = _traffic()
 RED_CPU = False   # reductions on CPU tensors (gloo rehearsal, BENCH_DIST_BACKEND=gloo)
+MATH = {0: "IEEE (bit-identical to oracle/)", 1: "fast (CUDA_FAST_MATH semantics)",
+        2: "fma (nvcc -fmad=true contraction, IEEE division; bit-identical to oracle/'s fma mode)"}
 METRIC = "slice-pairs/sec (6k×4k, 5 scales, 30 warps) at 1/2/4/8 GPUs; % HBM roofline"
 
 
@@ -65,11 +67,12 @@ def parse():
     ap.add_argument("--iterations", type=int, default=300)
     ap.add_argument("--epsilon", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--fast-math", action="store_true",
-                    help="headline run in fast-math mode (tvl1_params.fast_math = 1: the "
-                         "reference build's CUDA_FAST_MATH semantics; tolerance parity, not "
-                         "bit-identical). Default: IEEE (bit-identical to oracle/), with a "
-                         "secondary fast-math measurement reported under \"fast_math\"")
+    ap.add_argument("--fast-math", type=int, default=0, choices=(0, 1, 2), nargs="?", const=1,
+                    help="headline arithmetic mode (tvl1_params.fast_math): 0 = IEEE, bit-identical "
+                         "to oracle/ (default); 1 = the reference build's CUDA_FAST_MATH semantics "
+                         "(tolerance parity); 2 = nvcc's -fmad=true contraction alone (bit-identical "
+                         "to oracle/'s fma mode).  The other modes are measured after the headline "
+                         "and reported under \"math_modes\" with their EPE against it")
     ap.add_argument("--profile", type=int, default=0, choices=(0, 1),
                     help="1 = OpenCV's CPU DualTVL1OpticalFlow schedule (SURVEY 8(f) N3; "
                          "BASELINE configs[0]), with --inner / --outer iterations")
@@ -80,7 +83,7 @@ def parse():
     ap.add_argument("--no-strips-line", action="store_true",
                     help="skip the production ROI-strip measurement reported beside C2")
     ap.add_argument("--no-fast-math-line", action="store_true",
-                    help="skip the secondary fast-math measurement")
+                    help="skip the other arithmetic modes' measurement (math_modes)")
     ap.add_argument("--cpu-sample", default="6144x4096",
                     help="WxH crop of the benchmark pair the CPU baseline solves (default: all of it)")
     ap.add_argument("--inflight", type=int, default=None,
@@ -257,7 +260,7 @@ def run_stack(args, rank, world, local_rank, dist):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "math": "fast (CUDA_FAST_MATH semantics)" if args.fast_math else "IEEE (bit-identical to oracle/)",
+        "math": MATH[args.fast_math],
         "data": "synthetic (slices generated on the device)",
         "config": {
             "workload": (f"{name}: {npairs} pairs (z, z+s), s in {strides}, of a {Z}-slice "
@@ -362,8 +365,7 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "math": ("fast (CUDA_FAST_MATH semantics)" if args.fast_math
-                 else "IEEE (bit-identical to oracle/)"),
+        "math": MATH[args.fast_math],
         "data": "synthetic (slice 0 vs slices 1..B of a device-generated stack)",
         "config": {"workload": (f"production ROI strips (SURVEY 3.2): {W}x{H} pairs, nscales "
                                 f"{args.nscales}, warps {args.warps}, epsilon {args.epsilon}; "
@@ -508,27 +510,36 @@ def main():
 
     # secondary measurement in the other math mode (same pairs, same K): the IEEE run is
     # the headline unless --fast-math; its flow is the reference for the EPE figures
-    alt = None
+    # the other arithmetic modes on the same pairs and K: pairs/s and the
+    # per-pixel EPE of pair 0 against the headline run's flow -- the tolerance table
+    modes = None
     if not args.no_fast_math_line:
         u_ref, v_ref = slots[0]["u"].clone(), slots[0]["v"].clone()
-        alt_params = capi.make_params(nscales=args.nscales, warps=args.warps,
-                                      iterations=args.iterations, epsilon=args.epsilon,
-                                      fast_math=0 if args.fast_math else 1,
-                                      lambda_=args.lam, median_filtering=args.median)
-        for sl in slots:
-            sl["eng"].set_params(alt_params)
-            sl["eng"].set_profiling(False)
-        alt_elapsed, alt_stats = timed(1, args.steps)
-        solve(slots[0])
-        torch.cuda.synchronize(dev)
-        e = torch.sqrt((slots[0]["u"] - u_ref) ** 2 + (slots[0]["v"] - v_ref) ** 2)
-        alt = {"math": "IEEE" if args.fast_math else "fast (CUDA_FAST_MATH semantics)",
-               "value": round(world * args.steps * F / alt_elapsed, 4),
-               "ms_per_step": round(1e3 * alt_elapsed / args.steps, 3),
-               "iterations_per_pair": alt_stats[0]["iterations_total"],
-               "same_iterations": alt_stats[0]["iterations_total"] == stats[0]["iterations_total"],
-               "mean_epe_vs_headline_px": float(e.mean()),
-               "max_epe_vs_headline_px": float(e.max())}
+        modes = {}
+        names = {0: "ieee", 1: "fast", 2: "fma"}
+        for m in (0, 1, 2):
+            if m == args.fast_math:
+                continue
+            mp = capi.make_params(nscales=args.nscales, warps=args.warps,
+                                  iterations=args.iterations, epsilon=args.epsilon,
+                                  fast_math=m, lambda_=args.lam, median_filtering=args.median)
+            for sl in slots:
+                sl["eng"].set_params(mp)
+                sl["eng"].set_profiling(False)
+            m_elapsed, m_stats = timed(1, args.steps)
+            solve(slots[0])
+            torch.cuda.synchronize(dev)
+            e = torch.sqrt((slots[0]["u"] - u_ref) ** 2 + (slots[0]["v"] - v_ref) ** 2).flatten()
+            k = max(1, int(round(0.001 * e.numel())))
+            modes[names[m]] = {
+                "fast_math": m,
+                "value": round(world * args.steps * F / m_elapsed, 4),
+                "ms_per_step": round(1e3 * m_elapsed / args.steps, 3),
+                "iterations_per_pair": m_stats[0]["iterations_total"],
+                "same_iterations": m_stats[0]["iterations_total"] == stats[0]["iterations_total"],
+                "epe_vs_headline_px": {"mean": float(e.mean()),
+                                       "p99.9": float(torch.topk(e, k).values.min()),
+                                       "max": float(e.max())}}
 
     # aggregate per-kernel timing of this rank (rank 0 reports its own kernel roofline)
     k_ms = sum(s["kernel_ms"][0] for s in stats)
@@ -617,7 +628,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "math": "fast (CUDA_FAST_MATH semantics)" if args.fast_math else "IEEE (bit-identical to oracle/)",
+        "math": MATH[args.fast_math],
         "data": "synthetic",
         "config": {
             "workload": ((("C2" if (W, H, args.nscales, args.warps) == (6144, 4096, 5, 30)
@@ -653,7 +664,7 @@ def main():
              "other_kernels": round(cls_ms[2], 2),
              "host_sync_and_gaps": round(ms_per_step - sum(cls_ms), 2)}),
         "cpu_baseline": None,
-        "fast_math" if not args.fast_math else "ieee_math": alt,
+        "math_modes": modes,
         "production_strips": strips,
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -11,7 +11,7 @@
 // in a residual check and whether p is still 0 are per-pair bits in the kernel arguments
 // (BatchSel), because pairs leave a warp's iteration loop at different iterations.
 //
-// The arithmetic is the single-pair kernels' (warp_gather_fn, tb_iterate_store,
+// The arithmetic is the single-pair kernels' (warp_ring_body, warp_iter_body, roll_body,
 // resize_px), so every pair's flow is bit-identical to oracle/.
 #pragma once
 
@@ -52,6 +52,7 @@ __global__ void kb_convert(const uint8_t *__restrict__ I0, size_t p0, size_t s0,
 }
 
 // K2 pyramid step for both frames of every pair (blockIdx.z = 2 * pair + frame).
+template <bool C>
 __global__ void kb_resize_down2(const float *__restrict__ a0, const float *__restrict__ a1,
                                 int sw, int sh, int sp, size_t sps, float *__restrict__ b0,
                                 float *__restrict__ b1, int dw, int dh, int dp, size_t dps,
@@ -62,62 +63,7 @@ __global__ void kb_resize_down2(const float *__restrict__ a0, const float *__res
   const int b = blockIdx.z >> 1;
   const float *src = ((blockIdx.z & 1) == 0 ? a0 : a1) + b * sps;
   float *dst = ((blockIdx.z & 1) == 0 ? b0 : b1) + b * dps;
-  dst[(size_t)y * dp + x] = resize_px(src, sw, sh, sp, x, y, fx, fy);
-}
-
-// K3 centeredGradient of every pair's I1 into its G plane (blockIdx.z = pair).
-__global__ void kb_gradient(const float *__restrict__ I, size_t ips, int W, int H, int P,
-                            float4 *__restrict__ G, size_t gps) {
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  if (x >= W || y >= H) return;
-  const float *Ib = I + blockIdx.z * ips;
-  const float *row = Ib + (size_t)y * P;
-  const float c = row[x];
-  const float gx = 0.5f * (row[imin(x + 1, W - 1)] - row[imax(x - 1, 0)]);
-  const float gy = 0.5f * (Ib[(size_t)imin(y + 1, H - 1) * P + x] - Ib[(size_t)imax(y - 1, 0) * P + x]);
-  G[blockIdx.z * gps + (size_t)y * P + x] = make_float4(c, gx, gy, 0.0f);
-}
-
-// K5 warpBackward of the selected pairs (blockIdx.z = entry of sel): the fixed 4x4 Keys
-// gather of k_warp_lds's global path from G, weight-normalised; I1wx, I1wy, rho_c.
-struct BatchWarp {
-  const float *I0;           // level s of pair 0 (pair stride ips)
-  const float4 *G;           // pair stride gps
-  const float *U[2][2];      // u sets (pair stride ps)
-  float *C[3];               // I1wx, I1wy, rho (pair stride ps)
-  size_t ips, gps, ps;
-  int W, H, P;
-  BatchSel sel;
-};
-template <bool FM>
-__global__ void kb_warp(BatchWarp w) {
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  if (x >= w.W || y >= w.H) return;
-  const int b = w.sel.idx[blockIdx.z];
-  const int us = bsel_bit(w.sel.ubit, b);
-  const size_t i = (size_t)y * w.P + x, o = b * w.ps;
-  const float u1v = w.U[us][0][o + i], u2v = w.U[us][1][o + i];
-  const float4 *G = w.G + b * w.gps;
-  const float wx = (float)x + u1v;
-  const float wy = (float)y + u2v;
-  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
-  warp_gather_fn<FM>(
-      [&](int cy, int cx) {
-        const float4 g = G[(size_t)imin(imax(cy, 0), w.H - 1) * w.P + imin(imax(cx, 0), w.W - 1)];
-        return Tap3{g.x, g.y, g.z};
-      },
-      wx, wy, tap_floor(wx), tap_floor(wy), sum, sumx, sumy, wsum);
-  const float coeff = FM ? __builtin_amdgcn_rcpf(wsum) : recip_rn(wsum);
-  const float I1wv = sum * coeff;
-  const float I1wxv = sumx * coeff;
-  const float I1wyv = sumy * coeff;
-  const float i0 = w.I0[b * w.ips + i];
-  w.C[0][o + i] = I1wxv;
-  w.C[1][o + i] = I1wyv;
-  w.C[2][o + i] = FM ? __builtin_fmaf(-I1wyv, u2v, __builtin_fmaf(-I1wxv, u1v, I1wv)) - i0
-                     : I1wv - I1wxv * u1v - I1wyv * u2v - i0;
+  dst[(size_t)y * dp + x] = resize_px<C>(src, sw, sh, sp, x, y, fx, fy);
 }
 
 // K5 as k_warp_ring's streaming gather (64-px bands, LDS window ring of I1 / I1x / I1y
@@ -130,7 +76,7 @@ struct BatchRing {
   size_t ips, ps;
   BatchSel sel;
 };
-template <int M, int NW>
+template <int M, int NW, int FM>
 __global__ __launch_bounds__(64 * NW) void kb_warp_ring(BatchRing br) {
   __shared__ float ring[3 * warp_ring_rows<M, NW>() * (64 + 2 * M)];
   const int b = br.sel.idx[blockIdx.y];
@@ -145,7 +91,7 @@ __global__ __launch_bounds__(64 * NW) void kb_warp_ring(BatchRing br) {
   a.rho = br.C[2] + b * br.ps;
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= a.waves) return;
-  warp_ring_body<M, NW>(a, wid, ring);
+  warp_ring_body<M, NW, FM>(a, wid, ring);
 }
 
 // K5 + the warp's first pass (2 iterations ending in the first check) fused, as
@@ -162,7 +108,7 @@ struct BatchWI {
   int nblk;
   BatchSel sel;
 };
-template <int M, bool FM>
+template <int M, int FM>
 __global__ __launch_bounds__(192) void kb_warp_iter(BatchWI bw) {
   __shared__ float ring[kWiRows * 3 * wi_ww<M, 128>()];
   __shared__ float cring[2 * 5 * 128];
@@ -199,76 +145,12 @@ __global__ __launch_bounds__(192) void kb_warp_iter(BatchWI bw) {
   warp_iter_body<M, FM, 128>(w, wid, ring, cring);
 }
 
-// K6+K8(+K7 partials): one temporally blocked pass of t.niter iterations on each selected
-// pair (blockIdx.y = entry of sel, blockIdx.x = region) -- k_iterate_tb's body on the
-// pair's planes.  Residual partials of pair b at partials + b * nblk.
-struct BatchTB {
-  TBArgs t;                  // geometry, l_t, theta, gamma, taut (plane pointers unused)
-  float *U[2][2];            // u sets (pair stride ps)
-  float *Pp[2][4];           // p sets
-  const float *C[3];         // warp constants
-  size_t ps;
-  double *partials;
-  int nblk;                  // regions per pair
-  BatchSel sel;
-};
-template <int RH, int NG, int PX, bool FM>
-__global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void kb_iterate_tb(BatchTB bt) {
-  constexpr int LPR = 64 / PX;
-  constexpr int HALF = RH / NG;
-  __shared__ typename VecT<PX>::type lds[4 * RH * LPR];
-  const int b = bt.sel.idx[blockIdx.y];
-  TBArgs t = bt.t;
-  IterArgs &a = t.it;
-  {
-    const size_t o = b * bt.ps;
-    const int us = bsel_bit(bt.sel.ubit, b), qs = bsel_bit(bt.sel.pbit, b);
-    a.u1s = bt.U[us][0] + o;
-    a.u2s = bt.U[us][1] + o;
-    a.u1d = bt.U[us ^ 1][0] + o;
-    a.u2d = bt.U[us ^ 1][1] + o;
-    a.p11s = bt.Pp[qs][0] + o;
-    a.p12s = bt.Pp[qs][1] + o;
-    a.p21s = bt.Pp[qs][2] + o;
-    a.p22s = bt.Pp[qs][3] + o;
-    a.p11d = bt.Pp[qs ^ 1][0] + o;
-    a.p12d = bt.Pp[qs ^ 1][1] + o;
-    a.p21d = bt.Pp[qs ^ 1][2] + o;
-    a.p22d = bt.Pp[qs ^ 1][3] + o;
-    a.I1wx = bt.C[0] + o;
-    a.I1wy = bt.C[1] + o;
-    a.rho = bt.C[2] + o;
-    a.calc_err = bsel_bit(bt.sel.cerr, b);
-    a.p_zero = bsel_bit(bt.sel.pzero, b);
-    a.partials = bt.partials + (size_t)b * bt.nblk;
-  }
-  const int tid = threadIdx.x;
-  const int c4 = tid % LPR;
-  const int rr = tid / LPR;
-  int bx, by;
-  tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
-  const int K = t.niter;
-  const int xr0 = bx * 56 - 4;
-  const int yr0 = by * t.out_h - K;
-  const int X = xr0 + PX * c4;
-  const int xa = imin(imax(X, 0), a.P - PX);
-  Row<false, PX> r[NG];
-  int Y[NG];
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    Y[g] = yr0 + rr + g * HALF;
-    const int ya = imin(imax(Y[g], 0), a.H - 1);
-    load_row<false, PX>(r[g], a, (size_t)ya * a.P + xa);
-  }
-  tb_iterate_store<false, RH, NG, PX, FM>(t, lds, r, Y, X, c4, rr);
-}
-
-// The same pass as a k_iterate_roll<false, K, PX> wavefront pipeline (blockIdx.y = entry of
-// sel, 4 wavefronts per block): for strips the column bands walk all rows of the level in
-// one segment, so the halo recompute is 2K rows and 2 halo px per band, against 64x32
-// regions' 1.5-1.8x.  Residual partials of pair b at partials + b * nblk (one per wave).
+// K6+K8(+K7 partials): one pass of K iterations as a k_iterate_roll<false, K, PX> wavefront
+// pipeline on each selected pair (blockIdx.y = entry of sel, 4 wavefronts per block): for
+// strips the column bands walk all rows of the level in one segment, so the halo recompute
+// is 2K rows and 2 halo px per band (64x32 blocked regions recomputed 1.5-1.8x).  Residual partials of pair b at partials + b * nblk (one per wave).
 struct BatchRoll {
-  RollArgs ra;
+  RollArgs ra;               // geometry, l_t, theta, taut (plane pointers set per pair)
   float *U[2][2];
   float *Pp[2][4];
   const float *C[3];
@@ -277,7 +159,7 @@ struct BatchRoll {
   int nblk;
   BatchSel sel;
 };
-template <int K, int PX, bool FM>
+template <int K, int PX, int FM>
 __global__ __launch_bounds__(256) void kb_iterate_roll(BatchRoll br) {
   const int b = br.sel.idx[blockIdx.y];
   RollArgs ra = br.ra;
@@ -369,6 +251,7 @@ struct BatchUp {
   float fx, fy, mul;
   BatchSel sel;
 };
+template <bool C>
 __global__ void kb_upsample(BatchUp w) {
   const int x = blockIdx.x * 64 + threadIdx.x;
   const int y = blockIdx.y * 4 + threadIdx.y;
@@ -377,7 +260,7 @@ __global__ void kb_upsample(BatchUp w) {
   const int us = bsel_bit(w.sel.ubit, b);
   const float *src = w.U[us][c] + b * w.ps;
   float *dst = w.U[us ^ 1][c] + b * w.ps;
-  dst[(size_t)y * w.dp + x] = resize_px(src, w.sw, w.sh, w.sp, x, y, w.fx, w.fy) * w.mul;
+  dst[(size_t)y * w.dp + x] = resize_px<C>(src, w.sw, w.sh, w.sp, x, y, w.fx, w.fy) * w.mul;
 }
 
 // K10: every pair's final u set to the caller's flow (pair b at u + b * fstride bytes).

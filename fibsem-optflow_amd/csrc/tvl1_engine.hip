@@ -70,35 +70,22 @@ struct tvl1_ctx {
   hipEvent_t ev_check = nullptr;  // recorded after each residual copy
   hipEvent_t ev_order = nullptr;  // orders work on the caller's stream after a zero fill
   std::vector<char *> retired;    // arenas outgrown while possibly in use (arena_alloc)
-  int speculate = 0;         // TVL1_SPECULATE=1 enables speculative enqueueing (measured slower)
-  int iter_mode = 3;         // 0 = temporally blocked passes, 1 = one iteration per launch,
-                             // 2 = wavefront-pipelined passes (k_iterate_roll),
-                             // 3 = hybrid: roll for passes of >= 3 iterations on large levels
-  int roll_seg = 0;          // k_iterate_roll rows per segment (0 = auto, see roll_segment)
-  int roll_px = 2;           // px per lane of k_iterate_roll (1 or 2)
-  int roll_px_short = 4;     // px per lane of k_iterate_roll for passes of <= 2 iterations (1, 2, 4)
-  long roll_px4_min = 5000000;   // ... on levels of at least this many px (2 px below: more waves)
+  // dispatch: the defaults are the measured best; the environment knobs are
+  // for tests (named in tests/test_gpu_parity.py) and diagnostics
+  int roll_seg = 0;          // TVL1_ROLL_SEG: k_iterate_roll rows per segment (0 = auto)
+  long roll_px4_min = 5000000;   // TVL1_ROLL_PX4_MIN: 2-iteration passes take 4 px per lane on
+                                 // levels of at least this many px (2 px below: more waves)
   int roll_slots[kRollMax + 1][2][5] = {};   // resident k_iterate_roll<G, K, PX> wavefronts
-  int roll_lds = 0;          // experiment: dummy dynamic LDS per k_iterate_roll block (bytes)
-  int roll_fill = 100;       // % of the resident slots one streaming launch is sized for
-  int warp_fill = 100;
-  int warp_lds = 0;          // experiment: dummy dynamic LDS per k_warp_lds block (bytes)
-  int warp_margin = 6;       // k_warp_lds window margin (px): flows |u| < margin - 1 gather from LDS
-  int warp_mode = 4;         // 2 = k_warp_lds (LDS-staged G window per 64 x 16 tile),
-                             // 3 = k_warp_roll (streaming bands, LDS row ring of G),
-                             // 4 = k_warp_ring (streaming bands, ring built from I1; no G),
-                             // 0 = k_warp_img (gradient built in LDS from I1), 1 = k_warp (global)
-  int warp_roll_slots[8][5] = {};   // resident k_warp_roll<M, NW> blocks per device
-  int warp_ring_slots[8][5] = {};   // resident k_warp_ring<M, NW> blocks per device
-  size_t buf_limit = ((size_t)1 << 31) - 4096;   // plane bytes the buffer-addressed kernels take
-  int fuse_first = 2;        // warpBackward fused into each warp's first pass: 1 = k_warp_pass
-                             // (opt-in: slower), 2 = k_warp_iter (levels >= fuse_min px)
-  long fuse_min = 5000000;   // smaller levels: k_warp_ring + the pass (as fast, and their
-                             // warps mostly run past the first check)
-  int fuse_slots[8] = {};    // resident k_warp_pass<M> wavefronts per device
-  int witer_slots[8][2] = {};   // resident k_warp_iter<M, -, BW> blocks per device [M][BW == 64]
-  int witer_bw = 128;           // TVL1_WITER_BW: k_warp_iter band width (128: 2 producers, 64: 1)
-  int fuse_store = 0;        // TVL1_FUSE_STORE=1: k_warp_iter always stores the constants
+  long roll_long_min = 0;    // >= 3-iteration passes stream (k_iterate_roll) on levels of at
+                             // least this many 56 x 32 tiles, else k_iterate_tb
+  int warp_ring_slots = 0;   // resident k_warp_ring<6, 2> blocks per device
+  size_t buf_limit = ((size_t)1 << 31) - 4096;   // TVL1_BUF_LIMIT: plane bytes the
+                             // buffer-addressed kernels take (tests force the fallbacks)
+  int fuse = 1;              // TVL1_FUSE=0: no k_warp_iter (warp + first pass as two kernels)
+  long fuse_min = 5000000;   // TVL1_FUSE_MIN: k_warp_iter on levels of >= this many px; smaller
+                             // levels: k_warp_ring + the pass (as fast, and their warps mostly
+                             // run past the first check)
+  int witer_slots = 0;       // resident k_warp_iter<6, -, 128> blocks per device
   // batch arena (tvl1_calc_batch): per logical plane, kBatchMax pairs' copies
   char *barena = nullptr;
   size_t barena_bytes = 0;
@@ -106,12 +93,9 @@ struct tvl1_ctx {
   int bws[TVL1_MAX_LEVELS] = {}, bhs[TVL1_MAX_LEVELS] = {};   // ... and its level sizes
   float *bI0s[TVL1_MAX_LEVELS] = {}, *bI1s[TVL1_MAX_LEVELS] = {};
   size_t bips[TVL1_MAX_LEVELS] = {};    // pair stride of level s image planes (floats)
-  float4 *bG = nullptr;
   float *bU[2][2] = {}, *bP[2][4] = {}, *bC[3] = {};
   size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
   double *bpartials = nullptr;
-  int batch_tb = 0;                     // TVL1_BATCH_TB=1: blocked regions for batch passes
-  int batch_warp = 0;                   // TVL1_BATCH_WARP=1: per-px global gather (kb_warp)
   int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
   size_t map_bytes = 0;
@@ -119,13 +103,7 @@ struct tvl1_ctx {
   size_t align_bytes = 0;
   int4 *align_pat = nullptr;            // the rBRIEF pair pattern (device, set once)
   int bnblk = 0;                        // partials per pair
-  int warp_nw = 2;           // wavefronts per k_warp_roll block (1, 2 or 4)
   int check = 0;             // TVL1_CHECK=1: synchronise + check after every launch (diagnostics)
-  int warp_th = 16;          // k_warp_lds tile height (8, 16, 32)
-  // k_iterate_tb shape (0 = 64x32/512 thr, 1 = 64x32/256 thr, 2 = 64x64/1024 thr,
-  // 3 = 64x32/1024 thr 2 px each) for passes of <= 2 iterations (HBM-bound: 0 is
-  // fastest) and of >= 3 iterations (VALU-bound: 3 is fastest); TVL1_TB_CFG sets both
-  int tb_cfg = 0, tb_cfg_long = 3;
 
   // optional per-kernel-class HIP-event timing (tvl1_set_profiling)
   bool profiling = false;
@@ -195,8 +173,9 @@ static tvl1_status check_params(tvl1_ctx *c, const tvl1_params *p) {
     return set_err(c, TVL1_EINVAL, "scaleStep must be in (0, 1]");
   if (p->median_filtering > 1 && p->median_filtering != 3 && p->median_filtering != 5)
     return set_err(c, TVL1_EINVAL, "medianFiltering must be 1 (off), 3 or 5");
-  if (p->fast_math != 0 && p->fast_math != 1)
-    return set_err(c, TVL1_EINVAL, "fastMath must be 0 or 1 (got %d)", p->fast_math);
+  if (p->fast_math < 0 || p->fast_math > 2)
+    return set_err(c, TVL1_EINVAL, "fastMath must be 0 (IEEE), 1 (fast) or 2 (fma) (got %d)",
+                   p->fast_math);
   if (p->profile != 0 && p->profile != 1)
     return set_err(c, TVL1_EINVAL, "profile must be 0 (CUDA OpticalFlowDual_TVL1) or 1 (CPU DualTVL1) (got %d)",
                    p->profile);
@@ -220,9 +199,14 @@ static int pyramid_sizes(int w, int h, int nscales, double step, int *ws, int *h
   return L;
 }
 
-// region height of k_iterate_tb for a tb_cfg (0: 64x32/512 threads 4 px each,
-// 1: 64x32/256 threads 2x4 px, 2: 64x64/1024 threads 4 px, 3: 64x32/1024 threads 2 px)
-static int tb_region_h(int cfg, int) { return cfg == 2 ? 64 : 32; }
+// Arithmetic mode of a solve (kIEEE / kFast / kFma, tvl1_kernels.hpp): tvl1_params.fast_math
+// for the gamma = 0 path with 0 <= tau/theta < inf; gamma != 0 and taut < 0 solves run the
+// IEEE kernels.
+static int math_of(const tvl1_params &p) {
+  const float taut = (float)(p.tau / p.theta);
+  const bool exact_div = !(taut >= 0.0f && taut <= FLT_MAX);
+  return p.gamma != 0.0 || exact_div ? kIEEE : p.fast_math;
+}
 
 // Rows per k_iterate_roll segment.  Every wavefront runs (rows + 2K) steps, so the pass
 // takes about rounds x (rows + 2K) step times, rounds = ceil(wavefronts / resident slots):
@@ -373,6 +357,17 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H, hipStream_t st) {
                        (int)(lev), (int)(warp), (int)(it), hipGetErrorString(e_));         \
     }                                                                                      \
   } while (0)
+
+// Launch the kernel instance of a runtime arithmetic mode (tvl1_params.fast_math):
+// LAUNCH(FM) expands to the launch of the FM instantiation.
+#define MATH_SWITCH(m, LAUNCH) \
+  if ((m) == kFast) {          \
+    LAUNCH(kFast)              \
+  } else if ((m) == kFma) {    \
+    LAUNCH(kFma)               \
+  } else {                     \
+    LAUNCH(kIEEE)              \
+  }
 
 static inline dim3 grid2(int w, int h, int z = 1) {
   return dim3((unsigned)((w + 63) / 64), (unsigned)((h + 3) / 4), (unsigned)z);
@@ -576,10 +571,17 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 2), kBlk2, 0, st, I0, pitch0, I1, pitch1,
                      c->I0s[0], c->I1s[0], W, H, g.ps[0]);
   const float fdown = (float)(1.0 / prm.scale_step);
-  for (int s = 1; s < L; ++s)
-    hipLaunchKernelGGL(k_resize_down2, grid2(g.ws[s], g.hs[s], 2), kBlk2, 0, st, c->I0s[s - 1],
-                       c->I1s[s - 1], g.ws[s - 1], g.hs[s - 1], g.ps[s - 1], c->I0s[s],
-                       c->I1s[s], g.ws[s], g.hs[s], g.ps[s], fdown, fdown);
+  const bool contract_pyr = contracts(math_of(prm));
+  for (int s = 1; s < L; ++s) {
+    if (contract_pyr)
+      hipLaunchKernelGGL(k_resize_down2<true>, grid2(g.ws[s], g.hs[s], 2), kBlk2, 0, st,
+                         c->I0s[s - 1], c->I1s[s - 1], g.ws[s - 1], g.hs[s - 1], g.ps[s - 1],
+                         c->I0s[s], c->I1s[s], g.ws[s], g.hs[s], g.ps[s], fdown, fdown);
+    else
+      hipLaunchKernelGGL(k_resize_down2<false>, grid2(g.ws[s], g.hs[s], 2), kBlk2, 0, st,
+                         c->I0s[s - 1], c->I1s[s - 1], g.ws[s - 1], g.hs[s - 1], g.ps[s - 1],
+                         c->I0s[s], c->I1s[s], g.ws[s], g.hs[s], g.ps[s], fdown, fdown);
+  }
   {
     double b = (double)W * H * (2 + 8);
     for (int s = 1; s < L; ++s) b += (double)g.ws[s] * g.hs[s] * 8 + (double)g.ws[s - 1] * g.hs[s - 1] * 8;
@@ -602,72 +604,35 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
   // The projection's shared-reciprocal division (dual_px) needs ng = 1 + taut*|grad u| >= 1;
   // other parameters take the one-iteration kernel with plain IEEE divisions.
   const bool exact_div = !(taut >= 0.0f && taut <= FLT_MAX);
-  // fast-math kernels (FM template argument) for the gamma = 0 iteration passes
-  const bool fm = prm.fast_math != 0 && !gam;
+  // arithmetic mode of the gamma = 0 kernels (kIEEE / kFast / kFma, tvl1_kernels.hpp);
+  // gamma != 0 and taut < 0 solves run IEEE
+  const int math = math_of(prm);
   const float theta_f = (float)prm.theta;
   const float gamma_f = (float)prm.gamma;
   const float upmul = (float)(1.0 / prm.scale_step);
-  const bool speculate = c->speculate && !median;
 
   int64_t level_iters[TVL1_MAX_LEVELS] = {};
-  int64_t checks = 0, spec_miss = 0;
+  int64_t checks = 0;
 
   // ---- launch helpers
-  // Buffer-addressed kernels (k_iterate_roll, k_warp_ring, k_warp_pass) take 32-bit byte
-  // offsets: a level whose planes reach c->buf_limit bytes uses the 64-bit-addressed ones.
+  // The streaming kernels (k_iterate_roll, k_warp_ring, k_warp_iter) take 32-bit buffer
+  // byte offsets: a level whose planes reach c->buf_limit bytes uses the 64-bit-addressed
+  // ones (k_warp_img, k_iterate_tb).
   auto buffer_ok = [&](int s) {
     return (size_t)g.ps[s] * g.hs[s] * sizeof(float) < c->buf_limit;
-  };
-  auto warp_mode_of = [&](int s) { return c->warp_mode == 4 && !buffer_ok(s) ? 2 : c->warp_mode; };
-  auto gradient = [&](int s) -> tvl1_status {  // interleaved G plane for warp modes 1, 2, 3
-    const int wm = warp_mode_of(s);
-    if (wm == 0 || wm == 4) return TVL1_OK;     // derived from I1 in LDS
-    const int lw = g.ws[s], lh = g.hs[s];
-    size_t t0 = prof_begin(c, st);
-    hipLaunchKernelGGL(k_gradient, grid2(lw, lh), kBlk2, 0, st, c->I1s[s], lw, lh, g.ps[s], c->G);
-    prof_end(c, st, t0, 2, (double)lw * lh * (4 + 16));
-    DIAG(c, st, "k_gradient", s, -1, -1);
-    return TVL1_OK;
   };
   auto gather = [&](int s, int uset, int cbuf, int wp) -> tvl1_status {  // K5 warpBackward
     const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
     size_t t0 = prof_begin(c, st);
-    const int wm = warp_mode_of(s);
-    if (wm == 0) {
+    if (!buffer_ok(s)) {
       const int tx = (lw + kWarpTW - 1) / kWarpTW, ty = (lh + kWarpTH - 1) / kWarpTH;
-      hipLaunchKernelGGL(k_warp_img, dim3(tx * ty), dim3(256), 0, st, c->I0s[s], c->I1s[s],
-                         c->U[uset][0], c->U[uset][1], lw, lh, P, tx, c->C[cbuf][0],
-                         c->C[cbuf][1], c->C[cbuf][2]);
-    } else if (wm == 3) {
-      WarpRollArgs wa;
-      wa.I0 = c->I0s[s];
-      wa.G = c->G;
-      wa.u1 = c->U[uset][0];
-      wa.u2 = c->U[uset][1];
-      wa.I1wx = c->C[cbuf][0];
-      wa.I1wy = c->C[cbuf][1];
-      wa.rho = c->C[cbuf][2];
-      wa.W = lw;
-      wa.H = lh;
-      wa.P = P;
-      wa.bands = (lw + 63) / 64;
-      const int M = c->warp_margin == 4 ? 4 : c->warp_margin == 5 ? 5 : 6;
-      const int NW = c->warp_nw == 1 ? 1 : c->warp_nw == 4 ? 4 : 2;
-      // every block streams its rows + a 2M-row ring prologue
-      wa.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                    : roll_segment(wa.bands, lh, M, c->warp_roll_slots[M][NW]);
-      wa.waves = wa.bands * ((lh + wa.seg_rows - 1) / wa.seg_rows);
-#define WARP_ROLL(MM, NN)                                                                      \
-  hipLaunchKernelGGL((k_warp_roll<MM, NN>), dim3(wa.waves), dim3(64 * NN), c->warp_lds, st, wa);
-      if (M == 4) {
-        if (NW == 1) WARP_ROLL(4, 1) else if (NW == 4) WARP_ROLL(4, 4) else WARP_ROLL(4, 2)
-      } else if (M == 5) {
-        if (NW == 1) WARP_ROLL(5, 1) else if (NW == 4) WARP_ROLL(5, 4) else WARP_ROLL(5, 2)
-      } else {
-        if (NW == 1) WARP_ROLL(6, 1) else if (NW == 4) WARP_ROLL(6, 4) else WARP_ROLL(6, 2)
-      }
-#undef WARP_ROLL
-    } else if (wm == 4) {
+#define WARP_IMG(FM)                                                                           \
+  hipLaunchKernelGGL(k_warp_img<FM>, dim3(tx * ty), dim3(256), 0, st, c->I0s[s], c->I1s[s],    \
+                     c->U[uset][0], c->U[uset][1], lw, lh, P, tx, c->C[cbuf][0], c->C[cbuf][1], \
+                     c->C[cbuf][2]);
+      MATH_SWITCH(math, WARP_IMG)
+#undef WARP_IMG
+    } else {
       WarpRingArgs wa;
       wa.I0 = c->I0s[s];
       wa.I1 = c->I1s[s];
@@ -680,42 +645,16 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       wa.H = lh;
       wa.P = P;
       wa.bands = (lw + 63) / 64;
-      const int M = c->warp_margin == 4 ? 4 : c->warp_margin == 5 ? 5 : 6;
-      const int NW = c->warp_nw == 1 ? 1 : c->warp_nw == 4 ? 4 : 2;
       wa.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                    : roll_segment(wa.bands, lh, M, c->warp_ring_slots[M][NW] * c->warp_fill / 100);
+                                    : roll_segment(wa.bands, lh, 6, c->warp_ring_slots);
       wa.waves = wa.bands * ((lh + wa.seg_rows - 1) / wa.seg_rows);
-#define WARP_RING(MM, NN)                                                                      \
-  hipLaunchKernelGGL((k_warp_ring<MM, NN>), dim3(wa.waves), dim3(64 * NN), c->warp_lds, st, wa);
-      if (M == 4) {
-        if (NW == 1) WARP_RING(4, 1) else if (NW == 4) WARP_RING(4, 4) else WARP_RING(4, 2)
-      } else if (M == 5) {
-        if (NW == 1) WARP_RING(5, 1) else if (NW == 4) WARP_RING(5, 4) else WARP_RING(5, 2)
-      } else {
-        if (NW == 1) WARP_RING(6, 1) else if (NW == 4) WARP_RING(6, 4) else WARP_RING(6, 2)
-      }
+#define WARP_RING(FM) \
+  hipLaunchKernelGGL((k_warp_ring<6, 2, FM>), dim3(wa.waves), dim3(128), 0, st, wa);
+      MATH_SWITCH(math, WARP_RING)
 #undef WARP_RING
-    } else if (wm == 1) {
-      hipLaunchKernelGGL(k_warp, grid2(lw, lh), kBlk2, 0, st, c->I0s[s], c->G, c->U[uset][0],
-                         c->U[uset][1], lw, lh, P, c->C[cbuf][0], c->C[cbuf][1], c->C[cbuf][2]);
-    } else {
-#define WARP_LDS(TH, M)                                                                         \
-  {                                                                                             \
-    const int tx = (lw + kWarpTW - 1) / kWarpTW, ty = (lh + TH - 1) / TH;                       \
-    hipLaunchKernelGGL((k_warp_lds<TH, M>), dim3(tx * ty), dim3(256), c->warp_lds, st,          \
-                       c->I0s[s], c->G, c->U[uset][0], c->U[uset][1], lw, lh, P, tx,            \
-                       c->C[cbuf][0], c->C[cbuf][1], c->C[cbuf][2]);                            \
-  }
-      if (c->warp_th == 8) WARP_LDS(8, 6)
-      else if (c->warp_th == 32) WARP_LDS(32, 6)
-      else if (c->warp_margin == 4) WARP_LDS(16, 4)
-      else if (c->warp_margin == 5) WARP_LDS(16, 5)
-      else WARP_LDS(16, 6)
-#undef WARP_LDS
     }
-    // algorithmic: 40 B/px per warp
-    prof_end(c, st, t0, 1, (double)lw * lh * 40.0,
-             (double)lw * lh * (wm == 0 || wm == 4 ? 28.0 : 40.0));
+    // algorithmic: 40 B/px per warp; compulsory here ~28 B/px (I1 x 1 + 2M/64)
+    prof_end(c, st, t0, 1, (double)lw * lh * 40.0, (double)lw * lh * 28.0);
     DIAG(c, st, "warp kernel", s, wp, -1);
     return TVL1_OK;
   };
@@ -725,9 +664,14 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     const float fxu = (float)(1.0 / ((double)dw / lw));
     const float fyu = (float)(1.0 / ((double)dh / lh));
     size_t t0 = prof_begin(c, st);
-    hipLaunchKernelGGL(k_upsample, grid2(dw, dh, gam ? 3 : 2), kBlk2, 0, st, c->U[uset][0],
-                       c->U[uset][1], c->U[uset][2], lw, lh, g.ps[s], c->U[uset ^ 1][0],
-                       c->U[uset ^ 1][1], c->U[uset ^ 1][2], dw, dh, g.ps[s - 1], fxu, fyu, upmul);
+    if (contracts(math))
+      hipLaunchKernelGGL(k_upsample<true>, grid2(dw, dh, gam ? 3 : 2), kBlk2, 0, st, c->U[uset][0],
+                         c->U[uset][1], c->U[uset][2], lw, lh, g.ps[s], c->U[uset ^ 1][0],
+                         c->U[uset ^ 1][1], c->U[uset ^ 1][2], dw, dh, g.ps[s - 1], fxu, fyu, upmul);
+    else
+      hipLaunchKernelGGL(k_upsample<false>, grid2(dw, dh, gam ? 3 : 2), kBlk2, 0, st, c->U[uset][0],
+                         c->U[uset][1], c->U[uset][2], lw, lh, g.ps[s], c->U[uset ^ 1][0],
+                         c->U[uset ^ 1][1], c->U[uset ^ 1][2], dw, dh, g.ps[s - 1], fxu, fyu, upmul);
     prof_end(c, st, t0, 2, (double)lw * lh * 8.0 + (double)dw * dh * 8.0);
     DIAG(c, st, "k_upsample", s, -1, -1);
     return TVL1_OK;
@@ -738,14 +682,10 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     if (r_ != TVL1_OK) return r_;      \
   } while (0)
 
-  bool have_level = false;   // level s's gradient (+ u upsample) already enqueued speculatively
-  bool have_gather = false;  // the next warp's constants already enqueued speculatively
   for (int s = L - 1; s >= 0; --s) {
     const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
     const double Nl = (double)lw * lh;
     const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
-    if (!have_level) TRY(gradient(s));
-    have_level = false;
     bool p_zero = true;  // p = 0 at the start of every level (setTo(0) in procOneScale)
 
     IterArgs a{};
@@ -760,16 +700,13 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     a.taut = taut;
     a.partials = c->partials;
     const int nblk = iterate_blocks(lw, lh);
-    // k_iterate_roll addresses a plane with 32-bit buffer offsets (< 2 GiB per plane).
-    // Hybrid (3): 2-iteration passes (HBM-bound) stream best through k_iterate_roll's
-    // x-only halo; passes of >= 3 iterations are VALU-bound, where the roll kernel wins
-    // only while the level has enough rows for one round of >= 32-row segments (short
-    // segments repeat the 2K-row halo) and k_iterate_tb (64 x 32, 2 px/lane) wins below.
+    // Pass kernels: 2-iteration passes (HBM-bound) stream through k_iterate_roll's x-only
+    // halo; passes of >= 3 iterations are VALU-bound, where the streaming kernel wins only
+    // while the level has enough rows for one round of >= 32-row segments (short segments
+    // repeat the 2K-row halo) and k_iterate_tb (64 x 32 regions, 2 px/lane) wins below.
+    // Planes beyond 32-bit buffer offsets take k_iterate_tb for every pass.
     const bool roll_ok = buffer_ok(s);
-    const bool roll_all = roll_ok && c->iter_mode == 2;
-    const bool roll_short = roll_ok && c->iter_mode == 3;
-    const bool roll_long = roll_short &&
-                           (long)((lw + 55) / 56) * ((lh + 31) / 32) >= c->roll_slots[4][gam][1];
+    const bool roll_long = roll_ok && (long)((lw + 55) / 56) * ((lh + 31) / 32) >= c->roll_long_min;
 
     int last_warp_n = -1;   // iterations of the level's previous warp
     for (int wp = 0; wp < prm.warps; ++wp) {
@@ -784,12 +721,10 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       }
       // warpBackward fused into the warp's first pass (2 iterations ending in the first
       // check) when that pass would stream through k_iterate_roll anyway
-      const bool fuse = c->fuse_first && !gam && !exact_div && !have_gather && roll_short &&
-                        prm.epsilon > 0 && prm.iterations >= 2 &&
-                        (c->fuse_first == 1 || (long)lw * lh >= c->fuse_min);
+      const bool fuse = c->fuse && !gam && !exact_div && roll_ok && prm.epsilon > 0 &&
+                        prm.iterations >= 2 && (long)lw * lh >= c->fuse_min;
       bool fused_nostore = false;   // k_warp_iter ran without storing the constants
-      if (!have_gather && !fuse) TRY(gather(s, ui, cb, wp));
-      have_gather = false;
+      if (!fuse) TRY(gather(s, ui, cb, wp));
       a.I1wx = c->C[cb][0];
       a.I1wy = c->C[cb][1];
       a.rho = c->C[cb][2];
@@ -800,7 +735,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         int k = 0;
         bool calc_end = false;
         double prev_sim = prevError;
-        const int kmax = c->iter_mode == 1 || exact_div ? 1 : (roll_all || roll_short) ? kRollMax : kTbMax;
+        const int kmax = exact_div ? 1 : roll_ok ? kRollMax : kTbMax;
         while (k < kmax && n + k < prm.iterations) {
           const bool calcError = (prm.epsilon > 0) && ((n + k) & 1) && (prev_sim < scaledEps);
           ++k;
@@ -824,7 +759,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         const int nu = gam ? 3 : 2, np = gam ? 6 : 4;
         const double ld_planes = 3 + nu + (p_zero ? 0 : np), st_planes = nu + np;
         double alg_extra = 0.0;   // the fused warpBackward's algorithmic bytes
-        if (fuse && c->fuse_first == 2 && n == 0 && k == 2 && calc_end) {
+        if (fuse && n == 0 && k == 2 && calc_end) {
           WarpIterArgs w;
           w.ra.it = a;
           w.ra.it.I1wx = c->C[cb][0];
@@ -835,14 +770,12 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           // the constants go to HBM only when the warp may run further passes: always for
           // a level's first warp, else when the previous warp did not stop at its first
           // check (a wrong guess recomputes them with the warp kernel after the check)
-          w.store_c = c->fuse_store || wp == 0 || last_warp_n != 2;
+          w.store_c = wp == 0 || last_warp_n != 2;
           fused_nostore = !w.store_c;
-          const int M = c->warp_margin == 4 ? 4 : 6;
-          const int BW = c->witer_bw;
+          constexpr int M = 6, BW = 128;
           w.ra.bands = (lw + BW - 5) / (BW - 4);
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                          : roll_segment(w.ra.bands, lh, 2 + M,
-                                                         c->witer_slots[M][BW == 64]);
+                                          : roll_segment(w.ra.bands, lh, 2 + M, c->witer_slots);
           w.ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           w.ra.waves = w.ra.bands * segs;
@@ -850,21 +783,10 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
                            c->partials_cap);
-#define WITER_LAUNCH(MM, BB)                                                                   \
-  if (fm)                                                                                      \
-    hipLaunchKernelGGL((k_warp_iter<MM, true, BB>), dim3(w.ra.waves), dim3(64 + BB), 0, st, w); \
-  else                                                                                         \
-    hipLaunchKernelGGL((k_warp_iter<MM, false, BB>), dim3(w.ra.waves), dim3(64 + BB), 0, st, w);
-          if (M == 4 && BW == 64) {
-            WITER_LAUNCH(4, 64)
-          } else if (M == 4) {
-            WITER_LAUNCH(4, 128)
-          } else if (BW == 64) {
-            WITER_LAUNCH(6, 64)
-          } else {
-            WITER_LAUNCH(6, 128)
-          }
-#undef WITER_LAUNCH
+#define WITER(FM) \
+  hipLaunchKernelGGL((k_warp_iter<M, FM, BW>), dim3(w.ra.waves), dim3(64 + BW), 0, st, w);
+          MATH_SWITCH(math, WITER)
+#undef WITER
           // compulsory: p, u, I0 and the I1 window (x 1 + 2M/BW) per band column and row;
           // u, p (+ the constants) stored
           double rows = 0.0;
@@ -875,60 +797,21 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           hbm = (double)w.ra.bands * BW * rows * 4.0 * ((p_zero ? 3 : 7) + (double)(BW + 2 * M) / BW) +
                 Nl * 4.0 * (6.0 + (w.store_c ? 3.0 : 0.0));
           alg_extra = Nl * 40.0;   // 40 B/px per warp
-        } else if (fuse && n == 0 && k == 2 && calc_end) {
-          WarpPassArgs w;
-          w.ra.it = a;
-          w.ra.it.I1wx = c->C[cb][0];
-          w.ra.it.I1wy = c->C[cb][1];
-          w.ra.it.rho = c->C[cb][2];
-          w.I0 = c->I0s[s];
-          w.I1 = c->I1s[s];
-          const int M = c->warp_margin == 4 ? 4 : 6;
-          w.ra.bands = (lw + 59) / 60;
-          const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                          : roll_segment(w.ra.bands, lh, 2 + M, c->fuse_slots[M]);
-          w.ra.seg_rows = seg;
-          const int segs = (lh + seg - 1) / seg;
-          w.ra.waves = w.ra.bands * segs;
-          blocks = w.ra.waves;
-          if (blocks > c->partials_cap)
-            return set_err(c, TVL1_EHIP, "internal: %d wavefronts > partials capacity %d", blocks,
-                           c->partials_cap);
-          if (M == 4)
-            hipLaunchKernelGGL(k_warp_pass<4>, dim3(w.ra.waves), dim3(64), 0, st, w);
-          else
-            hipLaunchKernelGGL(k_warp_pass<6>, dim3(w.ra.waves), dim3(64), 0, st, w);
-          // compulsory: u, p, I0 and the I1 window (x 1 + 2M/64) per band lane and row,
-          // u, p and the constants stored
-          double rows = 0.0;
-          for (int sg = 0; sg < segs; ++sg) {
-            const int ys = sg * seg, ye = std::min(ys + seg, lh);
-            rows += std::min(ye - 1 + 2, lh - 1) - std::max(ys - 2, 0) + 1;
-          }
-          hbm = (double)w.ra.bands * 64.0 * rows * 4.0 * ((p_zero ? 3 : 7) + (64.0 + 2 * M) / 64.0) +
-                Nl * 4.0 * 9.0;
-          alg_extra = Nl * 40.0;   // 40 B/px per warp
-        } else if (c->iter_mode == 1 || exact_div) {
-          if (gam && exact_div)
+        } else if (exact_div) {   // taut < 0 or not finite: one iteration per launch, IEEE
+          if (gam)
             hipLaunchKernelGGL((k_iterate<true, true>), dim3(nblk), dim3(kBlock), 0, st, a);
-          else if (exact_div)
-            hipLaunchKernelGGL((k_iterate<false, true>), dim3(nblk), dim3(kBlock), 0, st, a);
-          else if (gam)
-            hipLaunchKernelGGL(k_iterate<true>, dim3(nblk), dim3(kBlock), 0, st, a);
           else
-            hipLaunchKernelGGL(k_iterate<false>, dim3(nblk), dim3(kBlock), 0, st, a);
+            hipLaunchKernelGGL((k_iterate<false, true>), dim3(nblk), dim3(kBlock), 0, st, a);
           hbm = Nl * 4.0 * (ld_planes + st_planes) * k;
-        } else if (roll_all || (roll_short && k <= 2) || (roll_long && k >= 3)) {
+        } else if (roll_ok && (k <= 2 || roll_long)) {
           RollArgs ra;
           ra.it = a;
-          const int px = k > 2 ? c->roll_px
-                         : c->roll_px_short == 4 && (long)lw * lh < c->roll_px4_min ? 2
-                                                                                   : c->roll_px_short;
+          const int px = k <= 2 && (long)lw * lh >= c->roll_px4_min ? 4 : 2;
           const int halo = (k + px - 1) / px * px;   // roll_halo<K, PX>
           const int out_w = 64 * px - 2 * halo;
           ra.bands = (lw + out_w - 1) / out_w;
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px] * c->roll_fill / 100);
+                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px]);
           ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           ra.waves = ra.bands * segs;
@@ -936,38 +819,38 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d wavefronts > partials capacity %d", blocks,
                            c->partials_cap);
-#define ROLL_LAUNCH(K, PX)                                                                     \
-  if (gam)                                                                                     \
-    hipLaunchKernelGGL((k_iterate_roll<true, K, PX>), dim3((ra.waves + 3) / 4), dim3(256),     \
-                       c->roll_lds, st, ra);                                                   \
-  else if (fm)                                                                                 \
-    hipLaunchKernelGGL((k_iterate_roll<false, K, PX, true>), dim3((ra.waves + 3) / 4),         \
-                       dim3(256), c->roll_lds, st, ra);                                        \
-  else                                                                                         \
-    hipLaunchKernelGGL((k_iterate_roll<false, K, PX>), dim3((ra.waves + 3) / 4), dim3(256),    \
-                       c->roll_lds, st, ra);
+          const dim3 grid((ra.waves + 3) / 4);
+#define ROLL_G(K, PX) \
+  hipLaunchKernelGGL((k_iterate_roll<true, K, PX>), grid, dim3(256), 0, st, ra);
+#define ROLL_M(FM, K, PX) \
+  hipLaunchKernelGGL((k_iterate_roll<false, K, PX, FM>), grid, dim3(256), 0, st, ra);
+#define ROLL(K, PX)                     \
+  if (gam) {                            \
+    ROLL_G(K, PX)                       \
+  } else if (math == kFast) {           \
+    ROLL_M(kFast, K, PX)                \
+  } else if (math == kFma) {            \
+    ROLL_M(kFma, K, PX)                 \
+  } else {                              \
+    ROLL_M(kIEEE, K, PX)                \
+  }
           if (px == 4) {   // k <= 2
             if (k == 1) {
-              ROLL_LAUNCH(1, 4)
+              ROLL(1, 4)
             } else {
-              ROLL_LAUNCH(2, 4)
-            }
-          } else if (px == 1) {
-            switch (k) {
-              case 1: ROLL_LAUNCH(1, 1) break;
-              case 2: ROLL_LAUNCH(2, 1) break;
-              case 3: ROLL_LAUNCH(3, 1) break;
-              default: ROLL_LAUNCH(4, 1) break;
+              ROLL(2, 4)
             }
           } else {
             switch (k) {
-              case 1: ROLL_LAUNCH(1, 2) break;
-              case 2: ROLL_LAUNCH(2, 2) break;
-              case 3: ROLL_LAUNCH(3, 2) break;
-              default: ROLL_LAUNCH(4, 2) break;
+              case 1: ROLL(1, 2) break;
+              case 2: ROLL(2, 2) break;
+              case 3: ROLL(3, 2) break;
+              default: ROLL(4, 2) break;
             }
           }
-#undef ROLL_LAUNCH
+#undef ROLL
+#undef ROLL_M
+#undef ROLL_G
           // compulsory: every band lane loads its column over the segment's rows + halo
           double rows = 0.0;
           for (int sg = 0; sg < segs; ++sg) {
@@ -975,35 +858,27 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
             rows += std::min(ye - 1 + k, lh - 1) - std::max(ys - k, 0) + 1;
           }
           hbm = (double)ra.bands * 64.0 * px * rows * 4.0 * ld_planes + Nl * 4.0 * st_planes;
-        } else {
+        } else {   // 64 x 32 regions, 2 px per lane
           TBArgs t;
           t.it = a;
           t.niter = k;
           t.tiles_x = (lw + 55) / 56;
-          const int cfg = k >= 3 ? c->tb_cfg_long : c->tb_cfg;
-          const int rh = tb_region_h(cfg, k);
+          constexpr int rh = 32;
           t.out_h = rh - 2 * k;
           blocks = t.tiles_x * ((lh + t.out_h - 1) / t.out_h);
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
                            c->partials_cap);
-#define TB_LAUNCH(RH, NG, PX)                                                                  \
-  if (gam)                                                                                     \
-    hipLaunchKernelGGL((k_iterate_tb<true, RH, NG, PX>), dim3(blocks),                         \
-                       dim3((64 / PX) * RH / NG), 0, st, t);                                   \
-  else if (fm)                                                                                 \
-    hipLaunchKernelGGL((k_iterate_tb<false, RH, NG, PX, true>), dim3(blocks),                  \
-                       dim3((64 / PX) * RH / NG), 0, st, t);                                   \
-  else                                                                                         \
-    hipLaunchKernelGGL((k_iterate_tb<false, RH, NG, PX>), dim3(blocks),                        \
-                       dim3((64 / PX) * RH / NG), 0, st, t);
-          switch (cfg) {
-            case 1: TB_LAUNCH(32, 2, 4) break;
-            case 2: TB_LAUNCH(64, 1, 4) break;
-            case 3: TB_LAUNCH(32, 1, 2) break;
-            default: TB_LAUNCH(32, 1, 4) break;
+#define TB(G, FM) \
+  hipLaunchKernelGGL((k_iterate_tb<G, rh, 1, 2, FM>), dim3(blocks), dim3(32 * rh), 0, st, t);
+#define TB_M(FM) TB(false, FM)
+          if (gam) {
+            TB(true, kIEEE)
+          } else {
+            MATH_SWITCH(math, TB_M)
           }
-#undef TB_LAUNCH
+#undef TB_M
+#undef TB
           // compulsory for this tiling: every staged region cell loads I1wx, I1wy, rho,
           // u (+p unless p == 0), every px stores u and p once per pass
           hbm = (double)blocks * 64.0 * rh * 4.0 * ld_planes + Nl * 4.0 * st_planes;
@@ -1022,21 +897,6 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, blocks,
                              c->pinned_dev);
           HIP_TRY(c, hipEventRecord(c->ev_check, st));
-          // enqueue what follows if this check ends the warp (see the comment above)
-          int spec = 0;  // 1 = next warp's gather, 2 = next level's upsample/gradient/gather
-          // only where a check nearly always ends the warp: the first check of a warp
-          // that is not the level's first (those run 2 iterations almost always)
-          if (speculate && n < prm.iterations && wp > 0 && n == k) {
-            if (wp + 1 < prm.warps) {
-              TRY(gather(s, ui, cb ^ 1, wp + 1));
-              spec = 1;
-            } else if (s > 0) {
-              TRY(upsample(s, ui));
-              TRY(gradient(s - 1));
-              TRY(gather(s - 1, ui ^ 1, cb ^ 1, 0));
-              spec = 2;
-            }
-          }
           HIP_TRY(c, hipEventSynchronize(c->ev_check));  // the cuda::sum -> host read
           error = *c->pinned;
           prevError = error;
@@ -1046,9 +906,6 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           // constants (from its input u, the set the pass just read) before the next pass
           if (fused_nostore && !ends) TRY(gather(s, ui ^ 1, cb, wp));
           fused_nostore = false;
-          if (spec && !ends) ++spec_miss;
-          if (spec == 1 && ends) have_gather = true;
-          if (spec == 2 && ends) have_level = have_gather = true;
         } else {
           error = DBL_MAX;
           prevError = prev_sim;
@@ -1062,7 +919,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     }
     HIP_TRY(c, hipGetLastError());
     if (s == 0) break;
-    if (!have_level) TRY(upsample(s, ui));  // zoom the flow to level s-1, scale by 1/scaleStep
+    TRY(upsample(s, ui));  // zoom the flow to level s-1, scale by 1/scaleStep
     ui ^= 1;
   }
 #undef TRY
@@ -1105,7 +962,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
     }
     stats->iterations_total = tot;
     stats->checks_total = checks;
-    stats->speculation_misses = (int32_t)spec_miss;
+    stats->speculation_misses = 0;
     stats->algorithmic_bytes = survey_bytes(g, prm.warps, level_iters);
   }
   return TVL1_OK;
@@ -1136,7 +993,7 @@ static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n, hipStream_t st
     ips[s] = align_up((size_t)g.ps[s] * g.hs[s], 64);
     bytes += 2 * ips[s] * n * sizeof(float) + 512;
   }
-  bytes += (ps * n * sizeof(float) + 256) * (4 + 4 + 8 + 3);   // G (float4) + U + P + C
+  bytes += (ps * n * sizeof(float) + 256) * (4 + 8 + 3);   // U + P + C
   bytes += (size_t)tb_blocks * n * sizeof(double) + 4096;
   c->bW = c->bH = c->bL = c->bn = 0;
   {
@@ -1156,7 +1013,6 @@ static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n, hipStream_t st
     c->bI1s[s] = (float *)take(ips[s] * n * sizeof(float));
   }
   c->bps = ps;
-  c->bG = (float4 *)take(4 * ps * n * sizeof(float));
   for (int k = 0; k < 2; ++k)
     for (int j = 0; j < 2; ++j) c->bU[k][j] = (float *)take(ps * n * sizeof(float));
   for (int k = 0; k < 2; ++k)
@@ -1194,11 +1050,20 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
   hipLaunchKernelGGL(kb_convert, grid2(W, H, 2 * n), kBlk2, 0, st, I0, pitch0, stride0, I1,
                      pitch1, stride1, c->bI0s[0], c->bI1s[0], W, H, g.ps[0], c->bips[0]);
   const float fdown = (float)(1.0 / prm.scale_step);
-  for (int s = 1; s < L; ++s)
-    hipLaunchKernelGGL(kb_resize_down2, grid2(g.ws[s], g.hs[s], 2 * n), kBlk2, 0, st,
-                       c->bI0s[s - 1], c->bI1s[s - 1], g.ws[s - 1], g.hs[s - 1], g.ps[s - 1],
-                       c->bips[s - 1], c->bI0s[s], c->bI1s[s], g.ws[s], g.hs[s], g.ps[s],
-                       c->bips[s], fdown, fdown);
+  const int math = math_of(prm);
+  for (int s = 1; s < L; ++s) {
+#define KB_DOWN(C)                                                                             \
+  hipLaunchKernelGGL(kb_resize_down2<C>, grid2(g.ws[s], g.hs[s], 2 * n), kBlk2, 0, st,         \
+                     c->bI0s[s - 1], c->bI1s[s - 1], g.ws[s - 1], g.hs[s - 1], g.ps[s - 1],    \
+                     c->bips[s - 1], c->bI0s[s], c->bI1s[s], g.ws[s], g.hs[s], g.ps[s],       \
+                     c->bips[s], fdown, fdown);
+    if (contracts(math)) {
+      KB_DOWN(true)
+    } else {
+      KB_DOWN(false)
+    }
+#undef KB_DOWN
+  }
   // u = 0 at the coarsest level, set 0 of every pair
   for (int k = 0; k < 2; ++k)
     HIP_TRY(c, hipMemsetAsync(c->bU[0][k], 0, ps * n * sizeof(float), st));
@@ -1207,7 +1072,6 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
   const float l_t = (float)(prm.lambda * prm.theta);
   const float taut = (float)(prm.tau / prm.theta);
   const float upmul = (float)(1.0 / prm.scale_step);
-  const bool fm = prm.fast_math != 0;
   BatchMask ubit{}, pbit{};
   std::vector<int64_t> level_iters((size_t)n * TVL1_MAX_LEVELS, 0), checks(n, 0);
   std::vector<int> nit(n);
@@ -1216,39 +1080,17 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
   for (int s = L - 1; s >= 0; --s) {
     const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
     const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
-    hipLaunchKernelGGL(kb_gradient, grid2(lw, lh, n), kBlk2, 0, st, c->bI1s[s], c->bips[s], lw,
-                       lh, P, c->bG, ps);
     BatchMask pzero{};   // p = 0 at every level start
     for (int b = 0; b < n; ++b) pzero.set(b);
-    BatchTB bt{};
-    bt.t.it.W = lw;
-    bt.t.it.H = lh;
-    bt.t.it.P = P;
-    bt.t.it.l_t = l_t;
-    bt.t.it.theta = (float)prm.theta;
-    bt.t.it.gamma = 0.0f;
-    bt.t.it.taut = taut;
-    bt.t.tiles_x = (lw + 55) / 56;
-    for (int k = 0; k < 2; ++k)
-      for (int j = 0; j < 2; ++j) bt.U[k][j] = c->bU[k][j];
-    for (int k = 0; k < 2; ++k)
-      for (int j = 0; j < 4; ++j) bt.Pp[k][j] = c->bP[k][j];
-    for (int j = 0; j < 3; ++j) bt.C[j] = c->bC[j];
-    bt.ps = ps;
-    bt.partials = c->bpartials;
+    IterArgs it{};   // pass geometry and scalars (plane pointers are set per pair)
+    it.W = lw;
+    it.H = lh;
+    it.P = P;
+    it.l_t = l_t;
+    it.theta = (float)prm.theta;
+    it.gamma = 0.0f;
+    it.taut = taut;
     for (int wp = 0; wp < prm.warps; ++wp) {
-      BatchWarp bw{};
-      bw.I0 = c->bI0s[s];
-      bw.G = c->bG;
-      for (int k = 0; k < 2; ++k)
-        for (int j = 0; j < 2; ++j) bw.U[k][j] = c->bU[k][j];
-      for (int j = 0; j < 3; ++j) bw.C[j] = c->bC[j];
-      bw.ips = c->bips[s];
-      bw.gps = ps;
-      bw.ps = ps;
-      bw.W = lw;
-      bw.H = lh;
-      bw.P = P;
       if (prm.median_filtering > 1) {   // build-only median of u before each warp
         BatchMedian md{};
         for (int k = 0; k < 2; ++k)
@@ -1263,16 +1105,14 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         hipLaunchKernelGGL(kb_median, grid2(lw, lh, 2 * n), kBlk2, 0, st, md);
         for (int b = 0; b < n; ++b) ubit.flip(b);
       }
-      bw.sel = all;
-      bw.sel.ubit = ubit;
       // warpBackward fused with the warp's first pass, which is 2 iterations ending in the
       // first check for every pair (procOneScale with epsilon > 0, iterations >= 2)
       const bool fuse = c->batch_fuse && prm.epsilon > 0 && prm.iterations >= 2;
       if (fuse) {
         BatchWI wi{};
-        wi.w.ra.it = bt.t.it;
+        wi.w.ra.it = it;
         wi.w.ra.bands = (lw + 123) / 124;
-        wi.w.ra.seg_rows = roll_segment(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots[6][0]);
+        wi.w.ra.seg_rows = roll_segment(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots);
         wi.w.ra.waves = wi.w.ra.bands * ((lh + wi.w.ra.seg_rows - 1) / wi.w.ra.seg_rows);
         if (wi.w.ra.waves > c->bnblk)
           return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", wi.w.ra.waves, c->bnblk);
@@ -1291,25 +1131,20 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         wi.sel.ubit = ubit;
         wi.sel.pbit = pbit;
         wi.sel.pzero = pzero;
-        if (fm)
-          hipLaunchKernelGGL((kb_warp_iter<6, true>), dim3(wi.w.ra.waves, n), dim3(192), 0, st, wi);
-        else
-          hipLaunchKernelGGL((kb_warp_iter<6, false>), dim3(wi.w.ra.waves, n), dim3(192), 0, st, wi);
+#define KB_WITER(FM) \
+  hipLaunchKernelGGL((kb_warp_iter<6, FM>), dim3(wi.w.ra.waves, n), dim3(192), 0, st, wi);
+        MATH_SWITCH(math, KB_WITER)
+#undef KB_WITER
         hipLaunchKernelGGL(kb_reduce, dim3(n), dim3(kBlock), 0, st, c->bpartials, wi.w.ra.waves,
                            all, c->pinned_dev + 8);
         HIP_TRY(c, hipEventRecord(c->ev_check, st));
-      } else if (fm || c->batch_warp == 1) {   // per-px global gather from G
-        if (fm)
-          hipLaunchKernelGGL(kb_warp<true>, grid2(lw, lh, n), kBlk2, 0, st, bw);
-        else
-          hipLaunchKernelGGL(kb_warp<false>, grid2(lw, lh, n), kBlk2, 0, st, bw);
       } else {   // k_warp_ring's streaming LDS-ring gather, per pair
         BatchRing br{};
         br.wa.W = lw;
         br.wa.H = lh;
         br.wa.P = P;
         br.wa.bands = (lw + 63) / 64;
-        br.wa.seg_rows = roll_segment(br.wa.bands * n, lh, 6, c->warp_ring_slots[6][2]);
+        br.wa.seg_rows = roll_segment(br.wa.bands * n, lh, 6, c->warp_ring_slots);
         br.wa.waves = br.wa.bands * ((lh + br.wa.seg_rows - 1) / br.wa.seg_rows);
         br.I0 = c->bI0s[s];
         br.I1 = c->bI1s[s];
@@ -1320,7 +1155,10 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         br.ps = ps;
         br.sel = all;
         br.sel.ubit = ubit;
-        hipLaunchKernelGGL((kb_warp_ring<6, 2>), dim3(br.wa.waves, n), dim3(128), 0, st, br);
+#define KB_RING(FM) \
+  hipLaunchKernelGGL((kb_warp_ring<6, 2, FM>), dim3(br.wa.waves, n), dim3(128), 0, st, br);
+        MATH_SWITCH(math, KB_RING)
+#undef KB_RING
       }
       int nact = 0;
       for (int b = 0; b < n; ++b) {
@@ -1380,21 +1218,9 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         sel.pbit = pbit;
         sel.pzero = pzero;
         int blocks;   // residual partials per pair
-        if (c->batch_tb) {   // 64x32 blocked regions (TVL1_BATCH_TB=1)
-          bt.t.niter = K;
-          bt.t.out_h = 32 - 2 * K;
-          blocks = bt.t.tiles_x * ((lh + bt.t.out_h - 1) / bt.t.out_h);
-          if (blocks > c->bnblk)
-            return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", blocks, c->bnblk);
-          bt.nblk = blocks;
-          bt.sel = sel;
-          if (fm)
-            hipLaunchKernelGGL((kb_iterate_tb<32, 1, 2, true>), dim3(blocks, sel.n), dim3(32 * 32), 0, st, bt);
-          else
-            hipLaunchKernelGGL((kb_iterate_tb<32, 1, 2, false>), dim3(blocks, sel.n), dim3(32 * 32), 0, st, bt);
-        } else {   // wavefront pipelines: 128-px bands down the whole level, one per wave
+        {   // wavefront pipelines: 128-px bands down the whole level, one per wave
           BatchRoll br{};
-          br.ra.it = bt.t.it;
+          br.ra.it = it;
           const int halo = (K + 1) / 2 * 2;   // roll_halo<K, 2>
           br.ra.bands = (lw + 128 - 2 * halo - 1) / (128 - 2 * halo);
           // segments sized so the batch's wavefronts fill whole rounds of resident slots
@@ -1415,11 +1241,12 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           br.nblk = blocks;
           br.sel = sel;
           const dim3 grid((br.ra.waves + 3) / 4, sel.n);
-#define KB_ROLL(KK)                                                                            \
-  if (fm)                                                                                      \
-    hipLaunchKernelGGL((kb_iterate_roll<KK, 2, true>), grid, dim3(256), 0, st, br);            \
-  else                                                                                         \
-    hipLaunchKernelGGL((kb_iterate_roll<KK, 2, false>), grid, dim3(256), 0, st, br);
+#define KB_ROLL_M(FM) hipLaunchKernelGGL((kb_iterate_roll<KK, 2, FM>), grid, dim3(256), 0, st, br);
+#define KB_ROLL(K_)                 \
+  {                                 \
+    constexpr int KK = K_;          \
+    MATH_SWITCH(math, KB_ROLL_M)    \
+  }
           switch (K) {
             case 1: KB_ROLL(1) break;
             case 2: KB_ROLL(2) break;
@@ -1427,6 +1254,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
             default: KB_ROLL(4) break;
           }
 #undef KB_ROLL
+#undef KB_ROLL_M
         }
         for (int j = 0; j < sel.n; ++j) {
           const int b = sel.idx[j];
@@ -1481,7 +1309,10 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
     up.mul = upmul;
     up.sel = all;
     up.sel.ubit = ubit;
-    hipLaunchKernelGGL(kb_upsample, grid2(up.dw, up.dh, 2 * n), kBlk2, 0, st, up);
+    if (contracts(math))
+      hipLaunchKernelGGL(kb_upsample<true>, grid2(up.dw, up.dh, 2 * n), kBlk2, 0, st, up);
+    else
+      hipLaunchKernelGGL(kb_upsample<false>, grid2(up.dw, up.dh, 2 * n), kBlk2, 0, st, up);
     for (int b = 0; b < n; ++b) ubit.flip(b);
   }
   BatchOut bo{};
@@ -1771,38 +1602,15 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (!c) return set_err(nullptr, TVL1_ENOMEM, "out of host memory");
   c->device = device;
   c->prm = *params;
-  if (const char *m = getenv("TVL1_ITER_MODE")) {
-    const int v = atoi(m);
-    c->iter_mode = v >= 0 && v <= 3 ? v : 3;
-  }
+  // test / diagnostic knobs (tests/test_gpu_parity.py names what each one reaches)
   if (const char *m = getenv("TVL1_ROLL_SEG")) c->roll_seg = atoi(m);
-  if (const char *m = getenv("TVL1_ROLL_LDS")) c->roll_lds = std::max(0, atoi(m));
-  if (const char *m = getenv("TVL1_ROLL_PX")) c->roll_px = c->roll_px_short = atoi(m) == 1 ? 1 : 2;
-  if (const char *m = getenv("TVL1_ROLL_PX_SHORT")) {
-    const int v = atoi(m);
-    c->roll_px_short = v == 1 ? 1 : v == 4 ? 4 : 2;
-  }
   if (const char *m = getenv("TVL1_ROLL_PX4_MIN")) c->roll_px4_min = atol(m);
-  if (const char *m = getenv("TVL1_ROLL_FILL")) c->roll_fill = std::max(10, atoi(m));
-  if (const char *m = getenv("TVL1_WARP_FILL")) c->warp_fill = std::max(10, atoi(m));
-  if (const char *m = getenv("TVL1_WARP_LDS")) c->warp_lds = std::max(0, atoi(m));
-  if (const char *m = getenv("TVL1_WARP_MARGIN")) c->warp_margin = atoi(m);
-  if (const char *m = getenv("TVL1_WARP_NW")) c->warp_nw = atoi(m);
-  if (const char *m = getenv("TVL1_FUSE_STORE")) c->fuse_store = atoi(m) != 0;
-  if (const char *m = getenv("TVL1_WITER_BW")) c->witer_bw = atoi(m) == 64 ? 64 : 128;
-  if (const char *m = getenv("TVL1_BATCH_TB")) c->batch_tb = atoi(m) != 0;
-  if (const char *m = getenv("TVL1_BATCH_WARP")) c->batch_warp = atoi(m);
-  if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_FUSE")) c->fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
-  if (const char *m = getenv("TVL1_FUSE")) c->fuse_first = atoi(m) == 1 ? 1 : atoi(m) == 2 ? 2 : 0;
-  if (const char *m = getenv("TVL1_BUF_LIMIT"))   // tests: force the 64-bit-addressed kernels
+  if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
-  if (const char *m = getenv("TVL1_TB_CFG")) c->tb_cfg = c->tb_cfg_long = atoi(m);
-  if (const char *m = getenv("TVL1_TB_CFG_LONG")) c->tb_cfg_long = atoi(m);
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
-  if (const char *m = getenv("TVL1_WARP_TH")) c->warp_th = atoi(m);
-  if (const char *m = getenv("TVL1_SPECULATE")) c->speculate = atoi(m) != 0;
-  if (const char *m = getenv("TVL1_WARP_MODE")) c->warp_mode = atoi(m);
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void **)&c->pinned, sizeof(double) * (8 + kBatchMax),
@@ -1813,46 +1621,25 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     delete c;
     return set_err(nullptr, TVL1_EHIP, "HIP initialisation failed on device %d", device);
   }
-  // resident wavefronts of each k_iterate_roll instance (4 per 256-thread block)
+  // resident wavefronts / blocks of the streaming kernels, for their segment sizing
   {
-    auto slots = [&](const void *fn) {
+    auto blocks_of = [&](const void *fn, int threads) {
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, c->roll_lds) != hipSuccess)
-        nb = 0;
-      return nb * 4 * prop.multiProcessorCount;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, 0) != hipSuccess) nb = 0;
+      return nb * prop.multiProcessorCount;
     };
 #define ROLL_SLOTS(G, K, PX) \
-  c->roll_slots[K][G][PX] = slots((const void *)k_iterate_roll<G, K, PX>);
-    ROLL_SLOTS(false, 1, 1) ROLL_SLOTS(false, 2, 1) ROLL_SLOTS(false, 3, 1) ROLL_SLOTS(false, 4, 1)
-    ROLL_SLOTS(true, 1, 1) ROLL_SLOTS(true, 2, 1) ROLL_SLOTS(true, 3, 1) ROLL_SLOTS(true, 4, 1)
+  c->roll_slots[K][G][PX] = 4 * blocks_of((const void *)k_iterate_roll<G, K, PX>, 256);
     ROLL_SLOTS(false, 1, 2) ROLL_SLOTS(false, 2, 2) ROLL_SLOTS(false, 3, 2) ROLL_SLOTS(false, 4, 2)
     ROLL_SLOTS(true, 1, 2) ROLL_SLOTS(true, 2, 2) ROLL_SLOTS(true, 3, 2) ROLL_SLOTS(true, 4, 2)
     ROLL_SLOTS(false, 1, 4) ROLL_SLOTS(false, 2, 4) ROLL_SLOTS(true, 1, 4) ROLL_SLOTS(true, 2, 4)
 #undef ROLL_SLOTS
-    auto blocks_of = [&](const void *fn, int threads) {
-      int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, c->warp_lds) != hipSuccess)
-        nb = 0;
-      return nb * prop.multiProcessorCount;
-    };
-#define WARP_SLOTS(MM, NN) \
-  c->warp_roll_slots[MM][NN] = blocks_of((const void *)k_warp_roll<MM, NN>, 64 * NN);
-    WARP_SLOTS(4, 1) WARP_SLOTS(4, 2) WARP_SLOTS(4, 4)
-    WARP_SLOTS(5, 1) WARP_SLOTS(5, 2) WARP_SLOTS(5, 4)
-    WARP_SLOTS(6, 1) WARP_SLOTS(6, 2) WARP_SLOTS(6, 4)
-#undef WARP_SLOTS
-#define RING_SLOTS(MM, NN) \
-  c->warp_ring_slots[MM][NN] = blocks_of((const void *)k_warp_ring<MM, NN>, 64 * NN);
-    RING_SLOTS(4, 1) RING_SLOTS(4, 2) RING_SLOTS(4, 4)
-    RING_SLOTS(5, 1) RING_SLOTS(5, 2) RING_SLOTS(5, 4)
-    RING_SLOTS(6, 1) RING_SLOTS(6, 2) RING_SLOTS(6, 4)
-#undef RING_SLOTS
-    c->fuse_slots[4] = blocks_of((const void *)k_warp_pass<4>, 64);
-    c->fuse_slots[6] = blocks_of((const void *)k_warp_pass<6>, 64);
-    c->witer_slots[4][0] = blocks_of((const void *)k_warp_iter<4>, 192);
-    c->witer_slots[6][0] = blocks_of((const void *)k_warp_iter<6>, 192);
-    c->witer_slots[4][1] = blocks_of((const void *)k_warp_iter<4, false, 64>, 128);
-    c->witer_slots[6][1] = blocks_of((const void *)k_warp_iter<6, false, 64>, 128);
+    c->warp_ring_slots = blocks_of((const void *)k_warp_ring<6, 2>, 128);
+    c->witer_slots = blocks_of((const void *)k_warp_iter<6>, 192);
+    // >= 3-iteration passes stream when the level has at least 4 wavefronts' worth of 56 x 32
+    // tiles per SIMD (the measured crossover against 64 x 32 blocked regions)
+    c->roll_long_min = 16L * prop.multiProcessorCount;
+    if (const char *m = getenv("TVL1_ROLL_LONG_MIN")) c->roll_long_min = atol(m);   // tests
     (void)hipGetLastError();
   }
   *out = c;

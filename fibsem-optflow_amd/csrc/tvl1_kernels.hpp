@@ -2,25 +2,28 @@
 //
 // Each kernel restates one stage of the solver the reference calls at
 // /root/reference/src/optflow.cpp:518-519 (OpenCV 3.4.1 cv::cuda::OpticalFlowDual_TVL1,
-// semantics in SURVEY.md Appendix A; kernel inventory SURVEY 2.1 K1..K12).
-// The arithmetic (float32, expression order, no FMA contraction: the library is
-// compiled with -ffp-contract=off) is identical to oracle/tvl1_oracle.c so the
-// two agree bit for bit; the data layout and fusion are MI355X-first:
+// semantics in SURVEY.md Appendix A; kernel inventory SURVEY 2.1 K1..K12).  In the default
+// arithmetic mode (kIEEE: float32, OpenCV's expression order, no FMA contraction -- the
+// library is compiled with -ffp-contract=off) the results are identical to oracle/tvl1_oracle.c
+// bit for bit.  The data layout and fusion are MI355X-first:
 //
 //   * every f32 plane is pitched to a multiple of 64 floats (256 B rows);
-//   * the gradient of I1 is stored interleaved as float4 (I1, I1x, I1y, 0) so each
-//     bicubic tap of warpBackward is ONE 16-byte gather instead of three;
-//   * estimateU (K6) and estimateDualVariables (K8) are FUSED into one pass
-//     (k_iterate): a wave owns a 248-px-wide column segment (62 lanes x float4, plus
-//     one halo lane on each side) and rolls down a strip of rows, so the
-//     backward-difference divergence and forward-difference gradient stencils are
-//     wavefront shuffles (x) and register rotation (y); no LDS, one HBM pass;
-//   * the state (u, p) ping-pongs between two buffer sets (Jacobi), so strips and
-//     segments never race on their halos;
-//   * grad = I1wx^2 + I1wy^2 is recomputed from I1wx, I1wy (same IEEE ops as K5)
-//     instead of being stored and re-read every iteration (-4 B/px/iteration);
-//   * the residual sum (K7) is fused into the iteration as per-block double partials
-//     reduced by one tiny kernel in a fixed order (deterministic).
+//   * estimateU (K6) and estimateDualVariables (K8) are fused, and up to 4 iterations run
+//     in ONE HBM pass: k_iterate_roll is a wavefront pipeline down a 128- or 256-px column
+//     band (x neighbours by DPP, y neighbours in registers, no LDS); k_iterate_tb runs
+//     64 x 32 regions in LDS for long passes on small levels;
+//   * warpBackward (K5) builds the (I1, I1x, I1y) window from I1 in an LDS ring
+//     (k_warp_ring; centeredGradient, K3, per slot), and on large levels it is fused with
+//     the warp's first 2-iteration pass (k_warp_iter: producer and consumer wavefronts);
+//   * the state (u, p) ping-pongs between two buffer sets (Jacobi), so bands and regions
+//     never race on their halos;
+//   * grad = I1wx^2 + I1wy^2 is recomputed from I1wx, I1wy (same operations as K5) instead
+//     of being stored and re-read every iteration;
+//   * the residual sum (K7) is fused into the iteration as per-wavefront / per-block double
+//     partials reduced by one tiny kernel in a fixed order (deterministic).
+//   * k_iterate (one iteration per launch) and k_warp_img (tiled, 64-bit addressing) serve
+//     the parameter sets and plane sizes the streaming kernels do not take (taut < 0,
+//     profile 1, planes >= 2 GiB).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -45,6 +48,20 @@ __device__ __forceinline__ float recip_rn(float d) {
   const float e = __builtin_fmaf(-d, r, 1.0f);
   return __builtin_fmaf(e, r, r);
 }
+
+// Arithmetic mode of the solver kernels (tvl1_params.fast_math; the FM template argument):
+//   kIEEE (0)  IEEE float32, no contraction: bit-identical to oracle/ (the default);
+//   kFast (1)  the reference build's CUDA_FAST_MATH (singularity/optflow.def:33-34): a*b + c
+//              contracted as nvcc does, division and sqrt approximated (v_rcp_f32 /
+//              v_sqrt_f32, 1 ulp);
+//   kFma  (2)  nvcc's default -fmad=true contraction alone, IEEE division and sqrt:
+//              bit-identical to oracle/'s fma mode.
+// The contraction rule (NVPTX's DAG combine, which fuses aggressively): an add or subtract
+// with a multiply operand becomes one fma, the LEFT operand's product when both are
+// products (a*b + c*d -> fma(a, b, c*d)).  Each site below says which expression it fuses.
+constexpr int kIEEE = 0, kFast = 1, kFma = 2;
+__host__ __device__ constexpr bool contracts(int m) { return m != kIEEE; }
+__host__ __device__ constexpr bool approx(int m) { return m == kFast; }
 
 // XCD-aware tile order (speed only, never correctness).  The dispatcher deals
 // workgroups round-robin over the 8 XCDs (MI355X_MICROARCH: blocks b and b+8 share an
@@ -139,25 +156,44 @@ __global__ void k_convert_u8(const uint8_t *__restrict__ s0, size_t sp0,
 
 // ---------------------------------------------------------------- K2 / K9 resize
 // cuda::resize INTER_LINEAR: corner-aligned, src = dst * f, +1 taps clamped.
+// C (contracting modes): the tap weights' differences take the product src_x = dst_x * fx
+// unrounded (x2 - src_x -> fma(-dst_x, fx, x2), src_x - x1 -> fma(dst_x, fx, -x1); the floor
+// uses the rounded product) and out + src * w -> fma(src, w, out).
+template <bool C = false>
 __device__ __forceinline__ float resize_px(const float *__restrict__ src, int sw, int sh,
                                            int sp, int dx, int dy, float fx, float fy) {
-  const float src_x = (float)dx * fx;
-  const float src_y = (float)dy * fy;
+  const float dxf = (float)dx, dyf = (float)dy;
+  const float src_x = dxf * fx;
+  const float src_y = dyf * fy;
   const int x1 = (int)floorf(src_x);
   const int y1 = (int)floorf(src_y);
   const int x2 = x1 + 1;
   const int y2 = y1 + 1;
   const int x2r = imin(x2, sw - 1);
   const int y2r = imin(y2, sh - 1);
+  const float ax = C ? __builtin_fmaf(-dxf, fx, (float)x2) : (float)x2 - src_x;
+  const float bx = C ? __builtin_fmaf(dxf, fx, -(float)x1) : src_x - (float)x1;
+  const float ay = C ? __builtin_fmaf(-dyf, fy, (float)y2) : (float)y2 - src_y;
+  const float by = C ? __builtin_fmaf(dyf, fy, -(float)y1) : src_y - (float)y1;
+  const float t00 = src[(size_t)y1 * sp + x1], t01 = src[(size_t)y1 * sp + x2r];
+  const float t10 = src[(size_t)y2r * sp + x1], t11 = src[(size_t)y2r * sp + x2r];
   float out = 0.0f;
-  out = out + src[(size_t)y1 * sp + x1] * (((float)x2 - src_x) * ((float)y2 - src_y));
-  out = out + src[(size_t)y1 * sp + x2r] * ((src_x - (float)x1) * ((float)y2 - src_y));
-  out = out + src[(size_t)y2r * sp + x1] * (((float)x2 - src_x) * (src_y - (float)y1));
-  out = out + src[(size_t)y2r * sp + x2r] * ((src_x - (float)x1) * (src_y - (float)y1));
+  if (C) {
+    out = __builtin_fmaf(t00, ax * ay, out);
+    out = __builtin_fmaf(t01, bx * ay, out);
+    out = __builtin_fmaf(t10, ax * by, out);
+    out = __builtin_fmaf(t11, bx * by, out);
+  } else {
+    out = out + t00 * (ax * ay);
+    out = out + t01 * (bx * ay);
+    out = out + t10 * (ax * by);
+    out = out + t11 * (bx * by);
+  }
   return out;
 }
 
 // Pyramid step for both frames at once (blockIdx.z selects the frame).
+template <bool C>
 __global__ void k_resize_down2(const float *__restrict__ a0, const float *__restrict__ a1,
                                int sw, int sh, int sp, float *__restrict__ b0,
                                float *__restrict__ b1, int dw, int dh, int dp, float fx,
@@ -167,11 +203,12 @@ __global__ void k_resize_down2(const float *__restrict__ a0, const float *__rest
   if (x >= dw || y >= dh) return;
   const float *src = blockIdx.z == 0 ? a0 : a1;
   float *dst = blockIdx.z == 0 ? b0 : b1;
-  dst[(size_t)y * dp + x] = resize_px(src, sw, sh, sp, x, y, fx, fy);
+  dst[(size_t)y * dp + x] = resize_px<C>(src, sw, sh, sp, x, y, fx, fy);
 }
 
 // Flow upsample to the next finer level + cuda::multiply(1/scaleStep) on u1, u2
 // (u3 is resized but not scaled, as in calcImpl).  blockIdx.z = component.
+template <bool C>
 __global__ void k_upsample(const float *__restrict__ s1, const float *__restrict__ s2,
                            const float *__restrict__ s3, int sw, int sh, int sp,
                            float *__restrict__ d1, float *__restrict__ d2,
@@ -183,7 +220,7 @@ __global__ void k_upsample(const float *__restrict__ s1, const float *__restrict
   const int c = blockIdx.z;
   const float *src = c == 0 ? s1 : (c == 1 ? s2 : s3);
   float *dst = c == 0 ? d1 : (c == 1 ? d2 : d3);
-  const float r = resize_px(src, sw, sh, sp, x, y, fx, fy);
+  const float r = resize_px<C>(src, sw, sh, sp, x, y, fx, fy);
   dst[(size_t)y * dp + x] = c < 2 ? r * mul : r;
 }
 
@@ -321,58 +358,9 @@ __global__ void k_remap_cubic(const float *__restrict__ I0, const float4 *__rest
 }
 
 // ---------------------------------------------------------------- K5 warp
-__device__ __forceinline__ float cubic(float x) {
-  x = fabsf(x);
-  if (x <= 1.0f) return x * x * (1.5f * x - 2.5f) + 1.0f;
-  if (x < 2.0f) return x * (x * (-0.5f * x + 2.5f) - 4.0f) + 2.0f;
-  return 0.0f;
-}
-
-// warpBackward: Keys-cubic (a=-0.5) gather at (x+u1, y+u2), texture clamp,
-// weight-normalised.  Writes I1wx, I1wy, rho_c (I1w and grad are not stored).
-__global__ void k_warp(const float *__restrict__ I0, const float4 *__restrict__ G,
-                       const float *__restrict__ u1, const float *__restrict__ u2, int W,
-                       int H, int P, float *__restrict__ I1wx, float *__restrict__ I1wy,
-                       float *__restrict__ rho) {
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  if (x >= W || y >= H) return;
-  const size_t i = (size_t)y * P + x;
-  const float u1v = u1[i];
-  const float u2v = u2[i];
-  const float wx = (float)x + u1v;
-  const float wy = (float)y + u2v;
-  const int xmin = (int)ceilf(wx - 2.0f);
-  const int xmax = (int)floorf(wx + 2.0f);
-  const int ymin = (int)ceilf(wy - 2.0f);
-  const int ymax = (int)floorf(wy + 2.0f);
-  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
-  for (int cy = ymin; cy <= ymax; ++cy) {
-    const int ry = imin(imax(cy, 0), H - 1);
-    const float wyk = cubic(wy - (float)cy);
-    for (int cx = xmin; cx <= xmax; ++cx) {
-      const int rx = imin(imax(cx, 0), W - 1);
-      const float w = cubic(wx - (float)cx) * wyk;
-      const float4 g = G[(size_t)ry * P + rx];
-      sum = sum + w * g.x;
-      sumx = sumx + w * g.y;
-      sumy = sumy + w * g.z;
-      wsum = wsum + w;
-    }
-  }
-  const float coeff = recip_rn(wsum);
-  const float I1wv = sum * coeff;
-  const float I1wxv = sumx * coeff;
-  const float I1wyv = sumy * coeff;
-  I1wx[i] = I1wxv;
-  I1wy[i] = I1wyv;
-  rho[i] = I1wv - I1wxv * u1v - I1wyv * u2v - I0[i];
-}
-
-// warpBackward, LDS-staged: a 64 x 16 px tile stages the (I1, I1x, I1y) window it can
-// reach with |u| <= kWarpHalo - 2 (clamped coordinates, exactly the texture-clamp
-// values) and gathers every bicubic tap from LDS; a pixel whose taps leave the
-// window takes the global-memory path.  Same arithmetic and order as k_warp.
+// Window geometry of k_warp_img (the tiled, 64-bit-addressed warpBackward for planes the
+// 32-bit buffer offsets of the streaming kernels cannot address): a 64 x 16 px tile and
+// the (I1, I1x, I1y) window it can reach with |u| <= kWarpHalo - 2.
 constexpr int kWarpTW = 64, kWarpTH = 16, kWarpHalo = 6;
 constexpr int kWarpWW = kWarpTW + 2 * kWarpHalo, kWarpWH = kWarpTH + 2 * kWarpHalo;
 
@@ -406,7 +394,8 @@ __device__ __forceinline__ float cubic_out(float x) {
 struct Tap3 {
   float x, y, z;
 };
-// FM (fast-math mode, see th_px): the polynomial and the accumulation contracted to fma.
+// Contracting modes: cubic's polynomials (x*x*t + 1 -> fma(x*x, t, 1), t = 1.5x - 2.5 ->
+// fma(1.5, x, -2.5); likewise the outer piece) and the accumulations sum + w*I -> fma.
 __device__ __forceinline__ float cubic_in_fm(float x) {
   x = fabsf(x);
   return __builtin_fmaf(x * x, __builtin_fmaf(1.5f, x, -2.5f), 1.0f);
@@ -415,14 +404,14 @@ __device__ __forceinline__ float cubic_out_fm(float x) {
   x = fabsf(x);
   return __builtin_fmaf(x, __builtin_fmaf(x, __builtin_fmaf(-0.5f, x, 2.5f), -4.0f), 2.0f);
 }
-template <bool FM = false, class TapF>
+template <int FM = 0, class TapF>
 __device__ __forceinline__ void warp_gather_fn(TapF tap, float wx, float wy, int fx, int fy,
                                                float &sum, float &sumx, float &sumy, float &wsum) {
   // (float)(fx + k) == (float)fx + k exactly: |fx| <= 2^24 (tap_floor), and both round
   // the same integer once
   const float fxf = (float)fx, fyf = (float)fy;
   float kx[4], ky[4];
-  if (FM) {
+  if (contracts(FM)) {
     kx[0] = cubic_out_fm(wx - (fxf - 1.0f));
     kx[1] = cubic_in_fm(wx - fxf);
     kx[2] = cubic_in_fm(wx - (fxf + 1.0f));
@@ -467,136 +456,31 @@ __device__ __forceinline__ void warp_gather_fn(TapF tap, float wx, float wy, int
   }
 }
 
-// The taps from a float4 (I1, I1x, I1y, -) plane: row(cy) -> the row, col(cx) -> index.
-template <class RowF, class ColF>
-__device__ __forceinline__ void warp_gather_taps(RowF row, ColF col, float wx, float wy, int fx,
-                                                 int fy, float &sum, float &sumx, float &sumy,
-                                                 float &wsum) {
-  warp_gather_fn(
-      [&](int cy, int cx) {
-        const float4 g = row(cy)[col(cx)];
-        return Tap3{g.x, g.y, g.z};
-      },
-      wx, wy, fx, fy, sum, sumx, sumy, wsum);
-}
-
-template <bool LDSPATH>
-__device__ __forceinline__ void warp_gather(const float4 *__restrict__ src, int sp, int ox, int oy,
-                                            int W, int H, float wx, float wy, int fx, int fy,
-                                            float &sum, float &sumx, float &sumy, float &wsum) {
-  warp_gather_taps(
-      [&](int cy) { return src + (size_t)(LDSPATH ? cy - oy : imin(imax(cy, 0), H - 1)) * sp; },
-      [&](int cx) { return LDSPATH ? cx - ox : imin(imax(cx, 0), W - 1); }, wx, wy, fx, fy, sum,
-      sumx, sumy, wsum);
-}
-
-template <int TH, int M = kWarpHalo>
-__global__ __launch_bounds__(256) void k_warp_lds(const float *__restrict__ I0,
-                                                  const float4 *__restrict__ G,
-                                                  const float *__restrict__ u1,
-                                                  const float *__restrict__ u2, int W, int H,
-                                                  int P, int tiles_x, float *__restrict__ I1wx,
-                                                  float *__restrict__ I1wy,
-                                                  float *__restrict__ rho) {
-  constexpr int WW = kWarpTW + 2 * M, WH = TH + 2 * M;   // window (margin M: |u| < M - 1 fits)
-  __shared__ float4 win[WH * WW];
-  int bx, by;
-  tile_of_block(blockIdx.x, gridDim.x, tiles_x, gridDim.x / tiles_x, bx, by);
-  const int x0 = bx * kWarpTW, y0 = by * TH;
-  const int ox = x0 - M, oy = y0 - M;   // window origin (unclamped coords)
-  // Issue this thread's own loads (u1, u2, I0 of its 4 rows) before the window fill so
-  // their latency overlaps it.
-  constexpr int R = TH / 4;
-  const int x = x0 + (threadIdx.x & 63);
-  const int xc = imin(x, W - 1);
-  float u1v[R], u2v[R], i0v[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int y = imin(y0 + (threadIdx.x >> 6) + 4 * j, H - 1);
-    const size_t i = (size_t)y * P + xc;
-    u1v[j] = u1[i];
-    u2v[j] = u2[i];
-    i0v[j] = I0[i];
-  }
-  for (int i = threadIdx.x; i < WH * WW; i += 256) {
-    const int wy = i / WW, wx = i - wy * WW;
-    const int cx = imin(imax(ox + wx, 0), W - 1);
-    const int cy = imin(imax(oy + wy, 0), H - 1);
-    win[i] = G[(size_t)cy * P + cx];
-  }
-  __syncthreads();
-  if (x >= W) return;
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int y = y0 + (threadIdx.x >> 6) + 4 * j;
-    if (y >= H) break;
-    const size_t i = (size_t)y * P + x;
-    const float wx = (float)x + u1v[j];
-    const float wy = (float)y + u2v[j];
-    const int fx = tap_floor(wx);
-    const int fy = tap_floor(wy);
-    float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
-    const bool inwin = fx - 1 >= ox && fx + 2 < ox + WW && fy - 1 >= oy && fy + 2 < oy + WH;
-    if (inwin)
-      warp_gather<true>(win, WW, ox, oy, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
-    else
-      warp_gather<false>(G, P, 0, 0, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
-    const float coeff = recip_rn(wsum);
-    const float I1wv = sum * coeff;
-    const float I1wxv = sumx * coeff;
-    const float I1wyv = sumy * coeff;
-    I1wx[i] = I1wxv;
-    I1wy[i] = I1wyv;
-    rho[i] = I1wv - I1wxv * u1v[j] - I1wyv * u2v[j] - i0v[j];
-  }
-}
-
-// warpBackward, streaming: a block of NW wavefronts owns a 64-px column band of a row
-// segment and walks down it, NW output rows per step (one row per wavefront, one px per
-// lane).  The block's LDS holds a ring of R rows of the (I1, I1x, I1y) window, (64 + 2M)
-// columns wide (clamped coordinates, exactly the texture-clamp values; ring row = image
-// row mod R): at step s the rows y0-M .. y0+NW-1+M are resident (y0 = first row of the
-// step), so a px whose taps stay within M - 1 px of it gathers from LDS; any other px
-// takes the global-memory path (same taps, same order).  Each wavefront loads one new
-// window row and its own u1 / u2 / I0 row kWarpAhead steps ahead into registers and writes
-// the window row when its step comes, so loads are in flight while earlier rows compute;
-// a row of G is read from HBM once per band (x 1 + 2M/64).  One LDS-only barrier per step
-// (NW > 1): rows written at step s+1 are >= 1 and < 2NW + 2M <= R rows past any row a
-// slower wavefront still reads at step s, so they never land on a slot in use.  The
-// register rings are unrolled (kWarpAhead + 1 steps per loop trip), so no register
-// holding a load in flight is copied.
+// Streaming warpBackward (k_warp_ring, and the producers of k_warp_iter): a block of NW
+// wavefronts owns a 64-px column band of a row segment and walks down it, NW output rows
+// per step (one row per wavefront, one px per lane).  The block's LDS holds a ring of R rows
+// of the (I1, I1x, I1y) window, (64 + 2M) columns wide (clamped coordinates, exactly the
+// texture-clamp values; ring row = image row mod R): at step s the rows y0-M .. y0+NW-1+M
+// are resident (y0 = first row of the step), so a px whose taps stay within M - 1 px of it
+// gathers from LDS; any other px takes the global-memory path (same taps, same order).
+// Each wavefront loads one new window row and its own u1 / u2 / I0 row kWarpAhead steps
+// ahead into registers and writes the window row when its step comes, so loads are in
+// flight while earlier rows compute.  One LDS-only barrier per step (NW > 1): rows written
+// at step s+1 are >= 1 and < 2NW + 2M <= R rows past any row a slower wavefront still reads
+// at step s, so they never land on a slot in use.  The register rings are unrolled
+// (kWarpAhead + 1 steps per loop trip), so no register holding a load in flight is copied.
 constexpr int kWarpAhead = 2;
-constexpr int kWarpRing16 = 16;   // k_warp_pass ring rows
 
 template <int M, int NW>
 constexpr int warp_ring_rows() { return 2 * NW + 2 * M <= 16 ? 16 : 32; }
 
-struct WarpRollArgs {
-  const float *I0;
-  const float4 *G;
-  const float *u1, *u2;
-  float *I1wx, *I1wy, *rho;
-  int W, H, P;
-  int bands, seg_rows, waves;   // waves = blocks (bands x segments)
-};
-
-typedef float vf4 __attribute__((ext_vector_type(4)));   // native vector: stays in VGPRs
-
-struct WarpRow {   // this lane's share of one window row (2 slots) and of one flow row
-  vf4 g0, g1;
-  float u1, u2, i0;
-};
-
-template <int M>
-__device__ __forceinline__ void warp_row_load(WarpRow &v, const WarpRollArgs &a, int gy, int fy,
-                                              int xg0, int xg1, int xc) {
-  const vf4 *Gr = reinterpret_cast<const vf4 *>(a.G) + (size_t)imin(imax(gy, 0), a.H - 1) * a.P;
-  v.g0 = Gr[xg0];
-  v.g1 = Gr[xg1];
-  const size_t o = (size_t)imin(fy, a.H - 1) * a.P + xc;
-  v.u1 = a.u1[o];
-  v.u2 = a.u2[o];
-  v.i0 = a.I0[o];
+// warpBackward's rho_c = I1w - I1wx*u1 - I1wy*u2 - I0 (contracted: the two products
+// fused into the running difference, fma(-I1wy, u2, fma(-I1wx, u1, I1w)) - I0).
+template <int FM>
+__device__ __forceinline__ float rho_c(float I1w, float I1wx, float I1wy, float u1, float u2,
+                                       float i0) {
+  return contracts(FM) ? __builtin_fmaf(-I1wy, u2, __builtin_fmaf(-I1wx, u1, I1w)) - i0
+                       : I1w - I1wx * u1 - I1wy * u2 - i0;
 }
 
 // LDS-only workgroup barrier: waits for this wave's LDS writes, not for its global loads
@@ -607,95 +491,7 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <int M, int NW>
-__device__ __forceinline__ void warp_roll_step(vf4 *__restrict__ ring, const WarpRow &cur,
-                                               WarpRow &ahead, const WarpRollArgs &a, int y0,
-                                               int ye, int w, int lane, int x0, int xg0, int xg1,
-                                               int xc) {
-  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>();
-  // loads for step + A: window row y0 + NW*A + M + w, flow row y0 + NW*A + w
-  warp_row_load<M>(ahead, a, y0 + NW * kWarpAhead + M + w, y0 + NW * kWarpAhead + w, xg0, xg1, xc);
-  __builtin_amdgcn_sched_barrier(0);
-  // window row y0 + M + w enters the ring
-  vf4 *dst = ring + ((y0 + M + w) & (R - 1)) * WW;
-  dst[lane] = cur.g0;
-  if (lane < 2 * M) dst[64 + lane] = cur.g1;
-  if (NW > 1) lds_barrier();   // (a wave's own LDS accesses execute in order)
-  const int x = x0 + lane, y = y0 + w;
-  const float wx = (float)x + cur.u1;
-  const float wy = (float)y + cur.u2;
-  const int fx = tap_floor(wx);
-  const int fy = tap_floor(wy);
-  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
-  const bool inwin = fx - 1 >= x0 - M && fx + 2 < x0 + 64 + M && fy - 1 >= y - M && fy + 2 <= y + M;
-  if (inwin)
-    warp_gather_taps([&](int cy) { return reinterpret_cast<const float4 *>(ring + (cy & (R - 1)) * WW); },
-                     [&](int cx) { return cx - (x0 - M); }, wx, wy, fx, fy, sum, sumx, sumy, wsum);
-  else
-    warp_gather<false>(a.G, a.P, 0, 0, a.W, a.H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
-  const float coeff = recip_rn(wsum);
-  const float I1wv = sum * coeff;
-  const float I1wxv = sumx * coeff;
-  const float I1wyv = sumy * coeff;
-  if (x < a.W && y < ye) {
-    const size_t o = (size_t)y * a.P + x;
-    a.I1wx[o] = I1wxv;
-    a.I1wy[o] = I1wyv;
-    a.rho[o] = I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0;
-  }
-}
-
-template <int M, int NW>
-__global__ __launch_bounds__(64 * NW) void k_warp_roll(WarpRollArgs a) {
-  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>();
-  static_assert(2 * NW + 2 * M <= R, "ring too small for the margin");
-  static_assert(2 * M <= 64, "second window slot per lane");
-  __shared__ vf4 ring[R * WW];
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
-  if (wid >= a.waves) return;   // whole blocks
-  const int band = wid % a.bands, seg = wid / a.bands;
-  const int x0 = band * 64;
-  const int xg0 = imin(imax(x0 - M + lane, 0), a.W - 1);        // window slot lane
-  const int xg1 = imin(imax(x0 - M + 64 + lane, 0), a.W - 1);   // window slot 64 + lane
-  const int xc = imin(x0 + lane, a.W - 1);
-  const int ys = seg * a.seg_rows, ye = imin(ys + a.seg_rows, a.H);
-  // ring prologue: window rows ys - M .. ys + M - 1, wave w taking rows w, w + NW, ...;
-  // all loads are issued before the first write
-  {
-    constexpr int PR = (2 * M + NW - 1) / NW;
-    vf4 t0[PR], t1[PR];
-#pragma unroll
-    for (int i = 0; i < PR; ++i) {
-      const vf4 *Gr = reinterpret_cast<const vf4 *>(a.G) +
-                      (size_t)imin(imax(ys - M + w + NW * i, 0), a.H - 1) * a.P;
-      t0[i] = Gr[xg0];
-      t1[i] = Gr[xg1];
-    }
-#pragma unroll
-    for (int i = 0; i < PR; ++i) {
-      const int r = ys - M + w + NW * i;
-      if (r < ys + M) {
-        vf4 *dst = ring + (r & (R - 1)) * WW;
-        dst[lane] = t0[i];
-        if (lane < 2 * M) dst[64 + lane] = t1[i];
-      }
-    }
-  }
-  static_assert(kWarpAhead == 2, "the step loop below is unrolled for a 3-row ring");
-  WarpRow A, B, C;
-  warp_row_load<M>(A, a, ys + M + w, ys + w, xg0, xg1, xc);
-  warp_row_load<M>(B, a, ys + NW + M + w, ys + NW + w, xg0, xg1, xc);
-  for (int y0 = ys; y0 < ye; y0 += 3 * NW) {
-    warp_roll_step<M, NW>(ring, A, C, a, y0, ye, w, lane, x0, xg0, xg1, xc);
-    warp_roll_step<M, NW>(ring, B, A, a, y0 + NW, ye, w, lane, x0, xg0, xg1, xc);
-    warp_roll_step<M, NW>(ring, C, B, a, y0 + 2 * NW, ye, w, lane, x0, xg0, xg1, xc);
-  }
-}
-
-// warpBackward, streaming from the level image: k_warp_roll's schedule, but the window
-// ring is filled from I1 and holds three float planes (I1, I1x, I1y) -- each window slot's
+// The window ring is filled from I1 and holds three float planes (I1, I1x, I1y) -- each window slot's
 // centred gradient is computed when its row enters the ring with centeredGradient's
 // exact formula at the clamped slot coordinate (the texture-clamp value of the gradient
 // image), so there is no G plane: HBM per px and warp is I1 (4 B x 1 + 2M/64) + u1, u2,
@@ -761,7 +557,7 @@ __device__ __forceinline__ void warp_ring_put(float *__restrict__ ring, const Wa
   }
 }
 
-template <int M, int NW>
+template <int M, int NW, int FM>
 __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const WarpRowI &cur,
                                                WarpRowI &ahead, const WarpRingArgs &a, int y0,
                                                int ye, int w, int lane, int x0,
@@ -783,14 +579,14 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
   float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
   const bool inwin = fx - 1 >= x0 - M && fx + 2 < x0 + 64 + M && fy - 1 >= y - M && fy + 2 <= y + M;
   if (inwin) {
-    warp_gather_fn(
+    warp_gather_fn<FM>(
         [&](int cy, int cx) {
           const float *p = ring + (cy & (R - 1)) * (3 * WW) + (cx - (x0 - M));
           return Tap3{p[0], p[WW], p[2 * WW]};
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
   } else {
-    warp_gather_fn(
+    warp_gather_fn<FM>(
         [&](int cy, int cx) {
           const int rx = imin(imax(cx, 0), a.W - 1), ry = imin(imax(cy, 0), a.H - 1);
           const float *row = a.I1 + (size_t)ry * a.P;
@@ -801,17 +597,17 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
   }
-  const float coeff = recip_rn(wsum);
+  const float coeff = approx(FM) ? __builtin_amdgcn_rcpf(wsum) : recip_rn(wsum);
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
   const unsigned vo = x < a.W && y < ye ? (unsigned)y * rowb + 4u * (unsigned)x : kOOB;
   bstore<kWarpStoreAux>(a.I1wx, nb, vo, 0, I1wxv);
   bstore<kWarpStoreAux>(a.I1wy, nb, vo, 0, I1wyv);
-  bstore<kWarpStoreAux>(a.rho, nb, vo, 0, I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0);
+  bstore<kWarpStoreAux>(a.rho, nb, vo, 0, rho_c<FM>(I1wv, I1wxv, I1wyv, cur.u1, cur.u2, cur.i0));
 }
 
-template <int M, int NW>
+template <int M, int NW, int FM>
 __device__ __forceinline__ void warp_ring_body(const WarpRingArgs &a, int wid, float *__restrict__ ring) {
   constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>(), PL = R * WW;
   static_assert(3 * WW < 256, "one tap row within ds_read2_b32 offsets");
@@ -858,18 +654,18 @@ __device__ __forceinline__ void warp_ring_body(const WarpRingArgs &a, int wid, f
   first(A, 0);
   first(B, 1);
   for (int y0 = ys; y0 < ye; y0 += 3 * NW) {
-    warp_ring_step<M, NW>(ring, A, C, a, y0, ye, w, lane, x0, xs, xcb, nb, rowb);
-    warp_ring_step<M, NW>(ring, B, A, a, y0 + NW, ye, w, lane, x0, xs, xcb, nb, rowb);
-    warp_ring_step<M, NW>(ring, C, B, a, y0 + 2 * NW, ye, w, lane, x0, xs, xcb, nb, rowb);
+    warp_ring_step<M, NW, FM>(ring, A, C, a, y0, ye, w, lane, x0, xs, xcb, nb, rowb);
+    warp_ring_step<M, NW, FM>(ring, B, A, a, y0 + NW, ye, w, lane, x0, xs, xcb, nb, rowb);
+    warp_ring_step<M, NW, FM>(ring, C, B, a, y0 + 2 * NW, ye, w, lane, x0, xs, xcb, nb, rowb);
   }
 }
 
-template <int M, int NW>
+template <int M, int NW, int FM = 0>
 __global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
   __shared__ float ring[3 * warp_ring_rows<M, NW>() * (64 + 2 * M)];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= a.waves) return;   // whole blocks
-  warp_ring_body<M, NW>(a, wid, ring);
+  warp_ring_body<M, NW, FM>(a, wid, ring);
 }
 
 // warpBackward straight from the level image (no precomputed gradient plane): the
@@ -877,7 +673,7 @@ __global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
 // (I1, I1x, I1y) window from it with centeredGradient's exact formula
 //   I1x = 0.5f * (I1[y][min(x+1,W-1)] - I1[y][max(x-1,0)])   (likewise I1y)
 // evaluated at the CLAMPED tap coordinate (texture clamp of the gradient images), and
-// gathers as k_warp_lds.  Every image coordinate that formula needs for a window cell
+// gathers every tap from LDS.  Every image coordinate that formula needs for a window cell
 // lies in [ox-1, ox+WW] x [oy-1, oy+WH], so the extended I1 window covers it.  HBM per
 // px: u1, u2, I0, I1 (16 B) + 12 B of outputs, instead of 16 B of gradient plane.
 constexpr int kWarpEW = kWarpWW + 2, kWarpEH = kWarpWH + 2;
@@ -894,38 +690,24 @@ __device__ __forceinline__ float4 grad_cell(const float *__restrict__ ext, int o
 
 // Global-memory gather for pixels whose taps leave the window: the same taps, with the
 // gradient of each (clamped) tap computed from I1 in global memory.
+template <int FM>
 __device__ __forceinline__ void warp_gather_img_global(const float *__restrict__ I1, int P, int W,
                                                        int H, float wx, float wy, int fx, int fy,
                                                        float &sum, float &sumx, float &sumy,
                                                        float &wsum) {
-  float kx[4], ky[4];
-  kx[0] = cubic_out(wx - (float)(fx - 1));
-  kx[1] = cubic_in(wx - (float)fx);
-  kx[2] = cubic_in(wx - (float)(fx + 1));
-  kx[3] = cubic_out(wx - (float)(fx + 2));
-  ky[0] = cubic_out(wy - (float)(fy - 1));
-  ky[1] = cubic_in(wy - (float)fy);
-  ky[2] = cubic_in(wy - (float)(fy + 1));
-  ky[3] = cubic_out(wy - (float)(fy + 2));
-  for (int j = 0; j < 4; ++j) {
-    const int ry = imin(imax(fy - 1 + j, 0), H - 1);
-    const float *row = I1 + (size_t)ry * P;
-    const float *up = I1 + (size_t)imax(ry - 1, 0) * P;
-    const float *dn = I1 + (size_t)imin(ry + 1, H - 1) * P;
-    for (int i = 0; i < 4; ++i) {
-      const int rx = imin(imax(fx - 1 + i, 0), W - 1);
-      const float w = kx[i] * ky[j];
-      const float c = row[rx];
-      const float gx = 0.5f * (row[imin(rx + 1, W - 1)] - row[imax(rx - 1, 0)]);
-      const float gy = 0.5f * (dn[rx] - up[rx]);
-      sum = sum + w * c;
-      sumx = sumx + w * gx;
-      sumy = sumy + w * gy;
-      wsum = wsum + w;
-    }
-  }
+  warp_gather_fn<FM>(
+      [&](int cy, int cx) {
+        const int rx = imin(imax(cx, 0), W - 1), ry = imin(imax(cy, 0), H - 1);
+        const float *row = I1 + (size_t)ry * P;
+        const float gx = 0.5f * (row[imin(rx + 1, W - 1)] - row[imax(rx - 1, 0)]);
+        const float gy = 0.5f * (I1[(size_t)imin(ry + 1, H - 1) * P + rx] -
+                                 I1[(size_t)imax(ry - 1, 0) * P + rx]);
+        return Tap3{row[rx], gx, gy};
+      },
+      wx, wy, fx, fy, sum, sumx, sumy, wsum);
 }
 
+template <int FM>
 __global__ __launch_bounds__(256) void k_warp_img(const float *__restrict__ I0,
                                                   const float *__restrict__ I1,
                                                   const float *__restrict__ u1,
@@ -976,16 +758,21 @@ __global__ __launch_bounds__(256) void k_warp_img(const float *__restrict__ I0,
     float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
     const bool inwin = fx - 1 >= ox && fx + 2 < ox + kWarpWW && fy - 1 >= oy && fy + 2 < oy + kWarpWH;
     if (inwin)
-      warp_gather<true>(win, kWarpWW, ox, oy, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+      warp_gather_fn<FM>(
+          [&](int cy, int cx) {
+            const float4 g = win[(cy - oy) * kWarpWW + (cx - ox)];
+            return Tap3{g.x, g.y, g.z};
+          },
+          wx, wy, fx, fy, sum, sumx, sumy, wsum);
     else
-      warp_gather_img_global(I1, P, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
-    const float coeff = recip_rn(wsum);
+      warp_gather_img_global<FM>(I1, P, W, H, wx, wy, fx, fy, sum, sumx, sumy, wsum);
+    const float coeff = approx(FM) ? __builtin_amdgcn_rcpf(wsum) : recip_rn(wsum);
     const float I1wv = sum * coeff;
     const float I1wxv = sumx * coeff;
     const float I1wyv = sumy * coeff;
     I1wx[i] = I1wxv;
     I1wy[i] = I1wyv;
-    rho[i] = I1wv - I1wxv * u1v[j] - I1wyv * u2v[j] - i0v[j];
+    rho[i] = rho_c<FM>(I1wv, I1wxv, I1wyv, u1v[j], u2v[j], i0v[j]);
   }
 }
 
@@ -1074,33 +861,29 @@ __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float
   return x > 0 ? rest : col0;
 }
 
-// Fast-math mode (tvl1_params.fast_math; FM template argument): the reference's own
-// OpenCV build flags (CUDA_FAST_MATH: nvcc -use_fast_math = approximate division and
-// sqrt, a*b + c contracted to fma; singularity/optflow.def:33-34) restated for CDNA4:
-// a / b -> a * v_rcp_f32(b), sqrt -> v_sqrt_f32 (both 1 ulp), and the products feeding a
-// sum are fused as nvcc would contract them.  Not bit-identical to oracle/: it is held to
-// the north-star tolerance (mean EPE <= 1e-3 px, same per-warp iteration counts) in
-// tests/test_gpu_parity.py.
+// Contracting modes (FM != kIEEE, see kIEEE / kFast / kFma): fm_fma marks the fused sites.
 __device__ __forceinline__ float fm_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
 __device__ __forceinline__ float th_quot(float rho, float gradv, bool mid);
 
 // estimateU's TH step at one px: v = u^{n-1} + d from the warp constants (pointwise).
 // CPUP: profile 1 (OpenCV's CPU estimateV): rho = rho_c + (I1wx*u1 + I1wy*u2) [+ gamma*u3]
-template <bool G, bool FM = false, bool CPUP = false>
+template <bool G, int FM = 0, bool CPUP = false>
 __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, float u1o, float u2o,
                                       float u3o, const IterArgs &a, float &v1, float &v2,
                                       float &v3) {
   const float Ix2 = I1wxv * I1wxv;
   const float Iy2 = I1wyv * I1wyv;
-  const float gradv = FM ? fm_fma(I1wyv, I1wyv, Ix2) : Ix2 + Iy2;
+  // warpBackward's grad = Ix2 + Iy2 (contracted: fma(I1wx, I1wx, Iy2))
+  const float gradv = contracts(FM) ? fm_fma(I1wxv, I1wxv, Iy2) : Ix2 + Iy2;
   // gamma*u3 inside the parentheses (with gamma = 0 either association gives
-  // the same bits, signed zeros included)
+  // the same bits, signed zeros included).  Contracted: rho_c + fma(gamma, u3, fma(I1wx,
+  // u1, I1wy*u2)), with u3 = 0 (gamma ? u3 : 0) when gamma = 0 -- the fma still turns a
+  // -0 sum into +0, as the reference's expression does.
   const float rho =
       CPUP ? (G ? rhoc + (I1wxv * u1o + I1wyv * u2o) + a.gamma * u3o
                 : rhoc + (I1wxv * u1o + I1wyv * u2o))
-      : FM ? rhoc + (G ? fm_fma(a.gamma, u3o, fm_fma(I1wyv, u2o, I1wxv * u1o))
-                       : fm_fma(I1wyv, u2o, I1wxv * u1o))
+      : contracts(FM) ? rhoc + fm_fma(a.gamma, G ? u3o : 0.0f, fm_fma(I1wxv, u1o, I1wyv * u2o))
            : rhoc + (I1wxv * u1o + I1wyv * u2o + a.gamma * (G ? u3o : 0.0f));
   // TH operator, branch-free: the three candidate steps are computed with the
   // reference's exact expressions and the applicable one selected.
@@ -1108,7 +891,7 @@ __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, floa
   const bool hi = rho > a.l_t * gradv;
   const bool mid = gradv > kFltEps;
   // only selected when gradv > FLT_EPSILON
-  const float fi = FM ? -rho * __builtin_amdgcn_rcpf(gradv) : th_quot(rho, gradv, mid);
+  const float fi = approx(FM) ? -rho * __builtin_amdgcn_rcpf(gradv) : th_quot(rho, gradv, mid);
   float d1 = mid ? fi * I1wxv : 0.0f;
   float d2 = mid ? fi * I1wyv : 0.0f;
   float d3 = mid ? fi * a.gamma : 0.0f;
@@ -1125,7 +908,7 @@ __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, floa
 
 // estimateU's second half at one px: u^n = v + theta * div(p^{n-1}).  pl = p*1 at x-1,
 // pu = p*2 at y-1.
-template <bool G, bool FM = false>
+template <bool G, int FM = 0>
 __device__ __forceinline__ void u_from_v(float v1, float v2, float v3, float p11, float p11l,
                                          float p12, float p12u, float p21, float p21l,
                                          float p22, float p22u, float p31, float p31l,
@@ -1133,18 +916,25 @@ __device__ __forceinline__ void u_from_v(float v1, float v2, float v3, float p11
                                          const IterArgs &a, float &n1, float &n2, float &n3) {
   const float div1 = divergence(p11, p11l, p12, p12u, x, y);
   const float div2 = divergence(p21, p21l, p22, p22u, x, y);
-  n1 = FM ? fm_fma(a.theta, div1, v1) : v1 + a.theta * div1;
-  n2 = FM ? fm_fma(a.theta, div2, v2) : v2 + a.theta * div2;
+  n1 = contracts(FM) ? fm_fma(a.theta, div1, v1) : v1 + a.theta * div1;
+  n2 = contracts(FM) ? fm_fma(a.theta, div2, v2) : v2 + a.theta * div2;
   if (G) {
     const float div3 = divergence(p31, p31l, p32, p32u, x, y);
-    n3 = FM ? fm_fma(a.theta, div3, v3) : v3 + a.theta * div3;
+    n3 = contracts(FM) ? fm_fma(a.theta, div3, v3) : v3 + a.theta * div3;
   }
+}
+
+// estimateU's error term (u1Old - u1New)^2 + (u2Old - u2New)^2 (contracted: fma(d1, d1,
+// d2*d2)); cuda::sum accumulates it in double.
+template <int FM>
+__device__ __forceinline__ float residual_px(float d1, float d2) {
+  return contracts(FM) ? fm_fma(d1, d1, d2 * d2) : d1 * d1 + d2 * d2;
 }
 
 // estimateU at one px (x, y): the TH step from the warp constants and u^{n-1}, then
 // u^n = v + theta * div(p^{n-1}).  Shared by every iteration kernel, so they all run
 // exactly this sequence of IEEE float operations.
-template <bool G, bool FM = false, bool CPUP = false>
+template <bool G, int FM = 0, bool CPUP = false>
 __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rhoc, float u1o,
                                               float u2o, float u3o, float p11, float p11l,
                                               float p12, float p12u, float p21, float p21l,
@@ -1159,7 +949,7 @@ __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rh
 }
 
 // estimateU for the PX px of this lane on row y.  up* = p12/p22/p32 of row y-1.
-template <bool G, int PX = 4, bool FM = false, bool CPUP = false>
+template <bool G, int PX = 4, int FM = 0, bool CPUP = false>
 __device__ __forceinline__ void estimate_u(const Row<G, PX> &r, const float (&up12)[PX],
                                            const float (&up22)[PX], const float (&up32)[PX],
                                            int X0, int y, const IterArgs &a, float (&n1)[PX],
@@ -1259,7 +1049,11 @@ __device__ __forceinline__ float div_short(float a, const Recip &R) {
 __device__ __forceinline__ float th_quot(float rho, float gradv, bool mid) {
   float fi = div_short(-rho, recip_of(gradv));
   const bool bad = mid && __builtin_fabsf(rho) < 0x1p-100f;
+#ifndef TVL1_EXP_NOBRANCH
   if (__ballot(bad)) fi = bad ? -rho / gradv : fi;
+#else
+  (void)bad;
+#endif
   return fi;
 }
 
@@ -1268,7 +1062,7 @@ __device__ __forceinline__ float th_quot(float rho, float gradv, bool mid) {
 // EXACT: plain IEEE divisions, for taut < 0 or non-finite (k_iterate<G, true>; the host
 // routes such parameters there), where ng >= 1 does not hold.
 // CPUP: profile 1, |grad u| as glibc hypotf: (float) sqrt((double) a*a + (double) b*b)
-template <bool EXACT = false, bool BR = false, bool FM = false, bool CPUP = false>
+template <bool EXACT = false, bool BR = false, int FM = 0, bool CPUP = false>
 __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_right,
                                         bool has_down, float taut, float pa, float pb, float &oa,
                                         float &ob) {
@@ -1276,16 +1070,19 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
   const float down = has_down ? ud : uc;
   const float ux = right - uc;
   const float uy = down - uc;
-  if (FM && !EXACT) {
-    const float g = __builtin_amdgcn_sqrtf(fm_fma(uy, uy, ux * ux));
+  // contracted (the reference's hypotf restated as sqrt(ux*ux + uy*uy)): ux*ux + uy*uy ->
+  // fma(ux, ux, uy*uy); 1 + taut*g -> fma(taut, g, 1); p + taut*ux -> fma(taut, ux, p)
+  if (approx(FM) && !EXACT) {
+    const float g = __builtin_amdgcn_sqrtf(fm_fma(ux, ux, uy * uy));
     const float r = __builtin_amdgcn_rcpf(fm_fma(taut, g, 1.0f));
     oa = fm_fma(taut, ux, pa) * r;
     ob = fm_fma(taut, uy, pb) * r;
     return;
   }
   const float g = CPUP ? (float)__builtin_sqrt((double)ux * ux + (double)uy * uy)
-                       : hypot_f<BR>(ux, uy);
-  const float ng = 1.0f + taut * g;
+                  : contracts(FM) ? sqrt_nn<BR>(fm_fma(ux, ux, uy * uy))
+                                  : hypot_f<BR>(ux, uy);
+  const float ng = contracts(FM) ? fm_fma(taut, g, 1.0f) : 1.0f + taut * g;
   if (EXACT) {
     oa = (pa + taut * ux) / ng;
     ob = (pb + taut * uy) / ng;
@@ -1294,11 +1091,17 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
     // or zero numerator, in a branch the wavefront skips when it has none (in the unrolled
     // pipelines too: +2.7 % there, where the sqrt's scaling branch was slower than a select)
     const Recip R = recip_of(ng);
-    const float na = pa + taut * ux, nb = pb + taut * uy;
+    const float na = contracts(FM) ? fm_fma(taut, ux, pa) : pa + taut * ux;
+    const float nb = contracts(FM) ? fm_fma(taut, uy, pb) : pb + taut * uy;
     oa = div_short(na, R);
     ob = div_short(nb, R);
     const bool tiny = __builtin_fabsf(na) < 0x1p-100f || __builtin_fabsf(nb) < 0x1p-100f;
-    if (__ballot(tiny)) {
+#ifdef TVL1_EXP_NOBRANCH
+    if (0)
+#else
+    if (__ballot(tiny))
+#endif
+    {
       oa = tiny ? div_by(na, R) : oa;
       ob = tiny ? div_by(nb, R) : ob;
     }
@@ -1306,7 +1109,7 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
 }
 
 // One projection component for the PX px of this lane.
-template <int PX, bool EXACT = false, bool FM = false, bool CPUP = false>
+template <int PX, bool EXACT = false, int FM = 0, bool CPUP = false>
 __device__ __forceinline__ void dual_component(const float (&uc)[PX], const float (&un)[PX],
                                                bool has_down, int X0, int W, float taut,
                                                const float (&pa)[PX], const float (&pb)[PX],
@@ -1435,7 +1238,7 @@ struct TBArgs {
 // Pass body of the blocked kernel: stage the vertically read planes, run the pass's
 // iterations on register-resident state, store the exact interior and the residual
 // partial of the last iteration.  lds = NPL planes of RH x LPR vectors of PX floats.
-template <bool G, int RH, int NG, int PX, bool FM>
+template <bool G, int RH, int NG, int PX, int FM>
 __device__ __forceinline__ void tb_iterate_store(const TBArgs &t,
                                                  typename VecT<PX>::type *__restrict__ lds,
                                                  Row<G, PX> (&r)[NG], const int (&Y)[NG], int X,
@@ -1485,9 +1288,7 @@ __device__ __forceinline__ void tb_iterate_store(const TBArgs &t,
 #pragma unroll
         for (int k = 0; k < PX; ++k) {
           if (X + k < a.W) {
-            const float f1 = (r[g].u1[k] - n1[k]) * (r[g].u1[k] - n1[k]);
-            const float f2 = (r[g].u2[k] - n2[k]) * (r[g].u2[k] - n2[k]);
-            acc += (double)(f1 + f2);
+            acc += (double)residual_px<FM>(r[g].u1[k] - n1[k], r[g].u2[k] - n2[k]);
           }
         }
       }
@@ -1572,7 +1373,7 @@ __device__ __forceinline__ void tb_iterate_store(const TBArgs &t,
   }
 }
 
-template <bool G, int RH, int NG, int PX = 4, bool FM = false>
+template <bool G, int RH, int NG, int PX = 4, int FM = 0>
 __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterate_tb(TBArgs t) {
   constexpr int LPR = 64 / PX;
   constexpr int HALF = RH / NG;
@@ -1714,12 +1515,12 @@ __device__ __forceinline__ float right_of(const float (&v)[PX], int j) {
 // the dependency list above; the border forms select, never combine).
 // VIN: in.u1 / u2 / u3 hold stage 1's v = u^0 + TH step (th_px, computed by the caller)
 // instead of u^0
-template <bool G, int K, int PX, bool VIN = false, bool FM = false>
+template <bool G, int K, int PX, bool VIN = false, int FM = 0>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                              const IterArgs &a, int r, const RollLane &L,
                                              unsigned nb, unsigned rowb, double &acc);
 
-template <bool G, int K, int PX, bool FM>
+template <bool G, int K, int PX, int FM>
 __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                           RollIn<G, PX> &ahead, const IterArgs &a, int r,
                                           const RollLane &L, unsigned nb, unsigned rowb,
@@ -1734,7 +1535,7 @@ __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G,
 
 // The compute and stores of one step: input row r (in `in`) enters stage 0 and every
 // stage advances one row.
-template <bool G, int K, int PX, bool VIN, bool FM>
+template <bool G, int K, int PX, bool VIN, int FM>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                              const IterArgs &a, int r, const RollLane &L,
                                              unsigned nb, unsigned rowb, double &acc) {
@@ -1786,9 +1587,8 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
                          G ? left_of<PX>(S.P31c[n - 1], j) : 0.0f, S.P32c[n - 1][j],
                          S.P32p[n - 1][j], L.X + j, yU, a, n1, n2, n3);
       if (n == K && a.calc_err) {
-        const float f1 = (S.U1p[n - 1][j] - n1) * (S.U1p[n - 1][j] - n1);
-        const float f2 = (S.U2p[n - 1][j] - n2) * (S.U2p[n - 1][j] - n2);
-        acc += stU && L.X + j < a.W ? (double)(f1 + f2) : 0.0;
+        const float e = residual_px<FM>(S.U1p[n - 1][j] - n1, S.U2p[n - 1][j] - n2);
+        acc += stU && L.X + j < a.W ? (double)e : 0.0;
       }
       S.U1c[n][j] = n1; S.U2c[n][j] = n2; if (G) S.U3c[n][j] = n3;
     }
@@ -1834,7 +1634,7 @@ constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
 
 // The pass of one wavefront (band / segment wid < ra.waves); k_iterate_roll and the
 // batched kb_iterate_roll differ only in how they find their planes and wid.
-template <bool G, int K, int PX, bool FM>
+template <bool G, int K, int PX, int FM>
 __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   constexpr int HALO = roll_halo<K, PX>();
   constexpr int BW = 64 * PX;            // band width (px)
@@ -1920,211 +1720,13 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   }
 }
 
-template <bool G, int K, int PX, bool FM = false>
+template <bool G, int K, int PX, int FM = 0>
 __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
   // wave-uniform (scalar) band / segment
   const int wid =
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
   if (wid >= ra.waves) return;                       // whole wavefronts only
   roll_body<G, K, PX, FM>(ra, wid);
-}
-
-// ---------------------------------------------------------------- K5 + first K6/K8 pass
-// k_warp_pass<M>: warpBackward of a warp fused into that warp's first iteration pass,
-// which always runs 2 iterations (procOneScale's first check is at n = 1).  One
-// wavefront = one k_iterate_roll<false, 2, 1> band (64 lanes, 2-px halo, 60 output px) of
-// a row segment.  Before input row r enters the pipeline, its warp constants are gathered
-// from an LDS ring of the (I1, I1x, I1y) window rows r-M .. r+M that the same wavefront
-// streams (k_warp_ring's per-slot centeredGradient, same taps and order), so the
-// constants reach their first use without a round trip through HBM.  They are still
-// stored (output columns / rows) for the warp's later passes.  HBM per px: I1 + I0 + u +
-// p in, u + p + constants out (~71 B) instead of ~92 B for k_warp_ring + the first pass.
-struct WarpPassArgs {
-  RollArgs ra;              // pass geometry and planes; ra.it.I1wx / I1wy / rho are written
-  const float *I0, *I1;     // level images
-};
-
-struct WinRow {   // this lane's 2 window slots of one I1 row: centre, x-1, x+1, y-1, y+1
-  float c0, l0, r0, n0, s0, c1, l1, r1, n1, s1;
-};
-
-struct PassIn {   // one pipeline input row at this lane (constants are computed) + window row
-  float u1, u2, p11, p12, p21, p22, i0;
-  WinRow g;
-};
-
-__device__ __forceinline__ void win_load(WinRow &v, const float *__restrict__ I1, int P, int H,
-                                         int gy, const int (&xs)[2][3]) {
-  const int r = imin(imax(gy, 0), H - 1);
-  const float *row = I1 + (size_t)r * P;
-  const float *up = I1 + (size_t)imax(r - 1, 0) * P;
-  const float *dn = I1 + (size_t)imin(r + 1, H - 1) * P;
-  v.c0 = row[xs[0][0]]; v.l0 = row[xs[0][1]]; v.r0 = row[xs[0][2]];
-  v.n0 = up[xs[0][0]]; v.s0 = dn[xs[0][0]];
-  v.c1 = row[xs[1][0]]; v.l1 = row[xs[1][1]]; v.r1 = row[xs[1][2]];
-  v.n1 = up[xs[1][0]]; v.s1 = dn[xs[1][0]];
-}
-
-template <int M>
-__device__ __forceinline__ void win_store(float *__restrict__ ring, const WinRow &v, int r, int lane) {
-  constexpr int WW = 64 + 2 * M, PL = kWarpRing16 * WW;
-  float *dst = ring + (r & (kWarpRing16 - 1)) * WW;
-  dst[lane] = v.c0;
-  dst[PL + lane] = 0.5f * (v.r0 - v.l0);
-  dst[2 * PL + lane] = 0.5f * (v.s0 - v.n0);
-  if (lane < 2 * M) {
-    dst[64 + lane] = v.c1;
-    dst[PL + 64 + lane] = 0.5f * (v.r1 - v.l1);
-    dst[2 * PL + 64 + lane] = 0.5f * (v.s1 - v.n1);
-  }
-}
-
-template <int M>
-__device__ __forceinline__ void pass_load(PassIn &v, const WarpPassArgs &w, unsigned nb,
-                                          unsigned rowb, int r, const RollLane &L,
-                                          const int (&xs)[2][3]) {
-  const IterArgs &a = w.ra.it;
-  const unsigned so = (unsigned)imin(r, a.H - 1) * rowb;
-  float t[1];
-  bload<1>(t, a.u1s, nb, L.vload, so); v.u1 = t[0];
-  bload<1>(t, a.u2s, nb, L.vload, so); v.u2 = t[0];
-  bload<1>(t, a.p11s, nb, L.vload, so); v.p11 = t[0];
-  bload<1>(t, a.p12s, nb, L.vload, so); v.p12 = t[0];
-  bload<1>(t, a.p21s, nb, L.vload, so); v.p21 = t[0];
-  bload<1>(t, a.p22s, nb, L.vload, so); v.p22 = t[0];
-  bload<1>(t, w.I0, nb, L.vload, so); v.i0 = t[0];
-  win_load(v.g, w.I1, a.P, a.H, r + M, xs);
-}
-
-template <int M>
-__device__ __forceinline__ void pass_step(RollPipe<false, 2, 1> &S, float *__restrict__ ring,
-                                          const PassIn &cur, PassIn &ahead,
-                                          const WarpPassArgs &w, int r, const RollLane &L,
-                                          int lane, int x0w, unsigned nb, unsigned rowb,
-                                          const int (&xs)[2][3], double &acc) {
-  constexpr int WW = 64 + 2 * M, PL = kWarpRing16 * WW;
-  const IterArgs &a = w.ra.it;
-  pass_load<M>(ahead, w, nb, rowb, r + kRollAhead, L, xs);
-  __builtin_amdgcn_sched_barrier(0);
-  // window row r + M enters the ring (it replaces row r + M - 16 < r - M)
-  win_store<M>(ring, cur.g, r + M, lane);
-  // warpBackward of input row r at this lane's column
-  const int x = L.X;
-  const float wx = (float)x + cur.u1;
-  const float wy = (float)r + cur.u2;
-  const int fx = tap_floor(wx);
-  const int fy = tap_floor(wy);
-  float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
-  const bool inwin = fx - 1 >= x0w && fx + 2 < x0w + WW && fy - 1 >= r - M && fy + 2 <= r + M;
-  if (inwin) {
-    warp_gather_fn(
-        [&](int cy, int cx) {
-          const float *q = ring + (cy & (kWarpRing16 - 1)) * WW + (cx - x0w);
-          return Tap3{q[0], q[PL], q[2 * PL]};
-        },
-        wx, wy, fx, fy, sum, sumx, sumy, wsum);
-  } else {
-    warp_gather_fn(
-        [&](int cy, int cx) {
-          const int rx = imin(imax(cx, 0), a.W - 1), ry = imin(imax(cy, 0), a.H - 1);
-          const float *row = w.I1 + (size_t)ry * a.P;
-          const float gx = 0.5f * (row[imin(rx + 1, a.W - 1)] - row[imax(rx - 1, 0)]);
-          const float gy = 0.5f * (w.I1[(size_t)imin(ry + 1, a.H - 1) * a.P + rx] -
-                                   w.I1[(size_t)imax(ry - 1, 0) * a.P + rx]);
-          return Tap3{row[rx], gx, gy};
-        },
-        wx, wy, fx, fy, sum, sumx, sumy, wsum);
-  }
-  const float coeff = recip_rn(wsum);
-  const float I1wv = sum * coeff;
-  RollIn<false, 1> in;
-  in.wx[0] = sumx * coeff;
-  in.wy[0] = sumy * coeff;
-  in.rh[0] = I1wv - in.wx[0] * cur.u1 - in.wy[0] * cur.u2 - cur.i0;
-  in.u1[0] = cur.u1; in.u2[0] = cur.u2; in.u3[0] = 0.0f;
-  in.p11[0] = cur.p11; in.p12[0] = cur.p12; in.p21[0] = cur.p21; in.p22[0] = cur.p22;
-  in.p31[0] = in.p32[0] = 0.0f;
-  // the constants of output cells, for the warp's later passes
-  const unsigned vo = L.out && r >= L.ys && r < L.ye ? (unsigned)r * rowb + L.vst : kOOB;
-  bstore((float *)a.I1wx, nb, vo, 0, in.wx[0]);
-  bstore((float *)a.I1wy, nb, vo, 0, in.wy[0]);
-  bstore((float *)a.rho, nb, vo, 0, in.rh[0]);
-  roll_advance<false, 2, 1>(S, in, a, r, L, nb, rowb, acc);
-}
-
-template <int M>
-__global__ __launch_bounds__(64) void k_warp_pass(WarpPassArgs w) {
-  constexpr int K = 2, HALO = 2, WW = 64 + 2 * M, PL = kWarpRing16 * WW;
-  static_assert(2 * M + 1 + kRollAhead <= kWarpRing16, "ring too small for the margin");
-  __shared__ float ring[3 * PL];
-  const RollArgs &ra = w.ra;
-  const IterArgs &a = ra.it;
-  const int lane = threadIdx.x;
-  const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
-  if (wid >= ra.waves) return;
-  const int band = wid % ra.bands, seg = wid / ra.bands;
-  RollLane L;
-  L.X = band * (64 - 2 * HALO) - HALO + lane;
-  L.vload = 4u * imin(imax(L.X, 0), a.P - 1);
-  L.out = lane >= HALO && lane < 64 - HALO && L.X < a.W;
-  L.vst = 4u * (unsigned)imax(L.X, 0);
-  const unsigned nb = 4u * (unsigned)a.P * (unsigned)a.H;
-  const unsigned rowb = 4u * (unsigned)a.P;
-  L.ys = seg * ra.seg_rows;
-  L.ye = imin(L.ys + ra.seg_rows, a.H);
-  const int r0 = imax(L.ys - K, 0);
-  const int thirds = (L.ye + K - r0 + 2) / 3;
-  const int x0w = L.X - lane - M;                   // window column of slot 0
-  int xs[2][3];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int slot = k == 0 || lane < 2 * M ? lane + 64 * k : lane;
-    const int cc = imin(imax(x0w + slot, 0), a.W - 1);
-    xs[k][0] = cc;
-    xs[k][1] = imax(cc - 1, 0);
-    xs[k][2] = imin(cc + 1, a.W - 1);
-  }
-  // ring prologue: window rows r0 - M .. r0 + M - 1, loads issued in two batches
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    WinRow t[M];
-#pragma unroll
-    for (int i = 0; i < M; ++i) win_load(t[i], w.I1, a.P, a.H, r0 - M + b * M + i, xs);
-#pragma unroll
-    for (int i = 0; i < M; ++i) win_store<M>(ring, t[i], r0 - M + b * M + i, lane);
-  }
-  RollPipe<false, K, 1> S;
-#pragma unroll
-  for (int n = 0; n <= K; ++n) {
-    S.U1c[n][0] = S.U2c[n][0] = S.U3c[n][0] = S.U1p[n][0] = S.U2p[n][0] = S.U3p[n][0] = 0.0f;
-    S.P11c[n][0] = S.P12c[n][0] = S.P21c[n][0] = S.P22c[n][0] = S.P31c[n][0] = S.P32c[n][0] = 0.0f;
-    S.P11p[n][0] = S.P12p[n][0] = S.P21p[n][0] = S.P22p[n][0] = S.P31p[n][0] = S.P32p[n][0] = 0.0f;
-  }
-#pragma unroll
-  for (int n = 0; n < K; ++n) S.CX[n][0] = S.CY[n][0] = S.CR[n][0] = 0.0f;
-  // as many dropped stores after each prologue load as a step issues (see k_iterate_roll)
-  auto dummy_stores = [&]() {
-    float *outs[9] = {(float *)a.I1wx, (float *)a.I1wy, (float *)a.rho, a.u1d, a.u2d,
-                      a.p11d, a.p12d, a.p21d, a.p22d};
-#pragma unroll
-    for (int k = 0; k < 9; ++k) bstore(outs[k], nb, kOOB, 0, 0.0f);
-  };
-  PassIn A, B, C;
-  pass_load<M>(A, w, nb, rowb, r0, L, xs);
-  dummy_stores();
-  pass_load<M>(B, w, nb, rowb, r0 + 1, L, xs);
-  dummy_stores();
-  double acc = 0.0;
-  for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
-    pass_step<M>(S, ring, A, C, w, r, L, lane, x0w, nb, rowb, xs, acc);
-    pass_step<M>(S, ring, B, A, w, r + 1, L, lane, x0w, nb, rowb, xs, acc);
-    pass_step<M>(S, ring, C, B, w, r + 2, L, lane, x0w, nb, rowb, xs, acc);
-  }
-  if (a.calc_err) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-    if (lane == 0) a.partials[wid] = acc;
-  }
 }
 
 // ---------------------------------------------------------------- K5 + first pass, two roles
@@ -2185,7 +1787,7 @@ struct WiLane {
   bool outc;
 };
 
-template <int M, bool FM, int BW>
+template <int M, int FM, int BW>
 __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__restrict__ cring,
                                              const WarpRowI &cur, WarpRowI &ahead,
                                              const WarpRingArgs &wa, const WarpIterArgs &w,
@@ -2226,12 +1828,11 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
   }
-  const float coeff = FM ? __builtin_amdgcn_rcpf(wsum) : recip_rn(wsum);
+  const float coeff = approx(FM) ? __builtin_amdgcn_rcpf(wsum) : recip_rn(wsum);
   const float I1wv = sum * coeff;
   const float I1wxv = sumx * coeff;
   const float I1wyv = sumy * coeff;
-  const float rh = FM ? __builtin_fmaf(-I1wyv, cur.u2, __builtin_fmaf(-I1wxv, cur.u1, I1wv)) - cur.i0
-                      : I1wv - I1wxv * cur.u1 - I1wyv * cur.u2 - cur.i0;
+  const float rh = rho_c<FM>(I1wv, I1wxv, I1wyv, cur.u1, cur.u2, cur.i0);
   // the first iteration's TH step is pointwise: the producer does it (the consumer sets
   // the block's pace), and the C ring carries v = u^0 + d instead of u^0
   float v1, v2, v3;
@@ -2264,7 +1865,7 @@ __device__ __forceinline__ void wi_p_load(WiP<PX> &v, const IterArgs &a, unsigne
   bload<PX>(v.p22, a.p22s, nb, voff, soff);
 }
 
-template <bool FM, int PX>
+template <int FM, int PX>
 __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
                                              const float *__restrict__ cring, const WiP<PX> &cur,
                                              WiP<PX> &ahead, const IterArgs &a, int r,
@@ -2291,7 +1892,7 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
   roll_advance<false, 2, PX, true, FM>(S, in, a, r, L, nb, rowb, acc);
 }
 
-template <int M, bool FM, int BW>
+template <int M, int FM, int BW>
 __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, float *__restrict__ ring,
                                                float *__restrict__ cring) {
   constexpr int K = 2, PX = BW / 64, HALO = roll_halo<2, PX>(), WW = wi_ww<M, BW>();
@@ -2420,7 +2021,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
   }
 }
 
-template <int M, bool FM = false, int BW = 128>
+template <int M, int FM = 0, int BW = 128>
 __global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
   __shared__ float ring[kWiRows * 3 * wi_ww<M, BW>()];
   __shared__ float cring[2 * 5 * BW];

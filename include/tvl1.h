@@ -73,11 +73,14 @@ typedef struct tvl1_params {
   double gamma;        /* 0.0   optflow.cpp:511 */
   int32_t use_initial_flow; /* read at optflow.cpp:512 but NOT passed to create() (:518): ignored, as in the reference */
   int32_t median_filtering; /* build-only: 1 = off (reference behaviour); 3 or 5 = median of u,v before each warp */
-  int32_t fast_math;   /* build-only: 0 = IEEE float32, bit-identical to oracle/ (default);
+  int32_t fast_math;   /* build-only arithmetic mode:
+                          0 = IEEE float32, no contraction: bit-identical to oracle/ (default);
                           1 = the reference build's CUDA_FAST_MATH semantics (singularity/optflow.def:33-34):
-                          approximate division and sqrt, fused multiply-add.  Held to the north-star
-                          tolerance (mean EPE <= 1e-3 px vs oracle/), not to bit identity.  gamma != 0
-                          solves stay IEEE. */
+                              a*b + c contracted as nvcc does, approximate division and sqrt.  Held to
+                              the tolerance of DESIGN.md 2 against oracle/, not to bit identity;
+                          2 = nvcc's default -fmad=true contraction alone, IEEE division and sqrt:
+                              bit-identical to oracle/'s fma mode.
+                          gamma != 0 and tau/theta < 0 solves stay IEEE. */
   int32_t profile;     /* build-only: 0 = cv::cuda::OpticalFlowDual_TVL1,
                           the reference's path (default); 1 = the schedule of OpenCV's CPU
                           cv::DualTVL1OpticalFlow: half-pixel pyramid/upsample, remap INTER_CUBIC

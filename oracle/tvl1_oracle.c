@@ -21,6 +21,15 @@
  * expression order as in the upstream kernels, residual sums in double.  The
  * reference build used fast math (approximate division/hypot, FMA): its own
  * outputs differ from any IEEE restatement at the ulp level (A.7).
+ *
+ * fma mode (tvl1_params.fast_math = 2): the same algorithm with every a*b + c that nvcc's
+ * default -fmad=true contracts written as one fmaf (IEEE division and sqrt kept), so the
+ * distance between the two arithmetics -- and the tolerance parity must hold to -- can be
+ * measured.  The rule, NVPTX's DAG combine with aggressive FMA fusion: an
+ * add or subtract with a multiply operand becomes one fma, the LEFT operand's product when
+ * both are products (a*b + c*d -> fma(a, b, c*d)); a - b*c -> fma(-b, c, a).  Each site is
+ * marked FMA below.  fast_math = 1 (approximate division / sqrt) has no exact C form: the
+ * oracle solves it in IEEE and the engine is held to the tolerance bar.
  */
 #include "tvl1_oracle.h"
 
@@ -64,31 +73,51 @@ void orc_convert_u8(const uint8_t *src, size_t pitch, int w, int h, float *dst) 
 /* [A.2] cuda::resize INTER_LINEAR (resize.cu resize_linear / LinearFilter):
  * corner-aligned source coordinate src = dst * f, taps floor/+1, the +1 tap
  * clamped to the last column/row (BrdReplicate / texture clamp). */
-void orc_resize_linear(const float *src, int sw, int sh, float *dst, int dw, int dh,
-                       float fx, float fy) {
+static void resize_linear(const float *src, int sw, int sh, float *dst, int dw, int dh,
+                          float fx, float fy, int fma_mode) {
   if (sw == dw && sh == dh) { /* resize.cpp: dsize == src.size() -> copyTo */
     memcpy(dst, src, sizeof(float) * (size_t)sw * sh);
     return;
   }
 #pragma omp parallel for schedule(static)
   for (int dy = 0; dy < dh; ++dy) {
-    const float src_y = (float)dy * fy;
+    const float dyf = (float)dy;
+    const float src_y = dyf * fy;
     const int y1 = (int)floorf(src_y);
     const int y2 = y1 + 1;
     const int y2r = imin(y2, sh - 1);
     for (int dx = 0; dx < dw; ++dx) {
-      const float src_x = (float)dx * fx;
+      const float dxf = (float)dx;
+      const float src_x = dxf * fx;
       const int x1 = (int)floorf(src_x);
       const int x2 = x1 + 1;
       const int x2r = imin(x2, sw - 1);
+      const float t00 = src[IDX(x1, y1, sw)], t01 = src[IDX(x2r, y1, sw)];
+      const float t10 = src[IDX(x1, y2r, sw)], t11 = src[IDX(x2r, y2r, sw)];
       float out = 0.0f;
-      out = out + src[IDX(x1, y1, sw)] * (((float)x2 - src_x) * ((float)y2 - src_y));
-      out = out + src[IDX(x2r, y1, sw)] * ((src_x - (float)x1) * ((float)y2 - src_y));
-      out = out + src[IDX(x1, y2r, sw)] * (((float)x2 - src_x) * (src_y - (float)y1));
-      out = out + src[IDX(x2r, y2r, sw)] * ((src_x - (float)x1) * (src_y - (float)y1));
+      if (fma_mode) {
+        /* FMA: x2 - dst_x*fx -> fma(-dst_x, fx, x2), dst_x*fx - x1 -> fma(dst_x, fx, -x1)
+         * (the floor takes the rounded product); out + src*w -> fma(src, w, out) */
+        const float ax = fmaf(-dxf, fx, (float)x2), bx = fmaf(dxf, fx, -(float)x1);
+        const float ay = fmaf(-dyf, fy, (float)y2), by = fmaf(dyf, fy, -(float)y1);
+        out = fmaf(t00, ax * ay, out);
+        out = fmaf(t01, bx * ay, out);
+        out = fmaf(t10, ax * by, out);
+        out = fmaf(t11, bx * by, out);
+      } else {
+        out = out + t00 * (((float)x2 - src_x) * ((float)y2 - src_y));
+        out = out + t01 * ((src_x - (float)x1) * ((float)y2 - src_y));
+        out = out + t10 * (((float)x2 - src_x) * (src_y - (float)y1));
+        out = out + t11 * ((src_x - (float)x1) * (src_y - (float)y1));
+      }
       dst[IDX(dx, dy, dw)] = out;
     }
   }
+}
+
+void orc_resize_linear(const float *src, int sw, int sh, float *dst, int dw, int dh,
+                       float fx, float fy) {
+  resize_linear(src, sw, sh, dst, dw, dh, fx, fy, 0);
 }
 
 /* [A.2] dst size = saturate_cast<int>(cols * scaleStep) (cvRound, half-to-even);
@@ -121,8 +150,13 @@ void orc_centered_gradient(const float *I, int w, int h, float *Ix, float *Iy) {
 }
 
 /* [A.3] Keys cubic kernel, a = -0.5 (tvl1flow.cu `cubic`). */
-static inline float cubic(float x) {
+static inline float cubic(float x, int fma_mode) {
   x = fabsf(x);
+  if (fma_mode) { /* FMA: x*x*t + 1 -> fma(x*x, t, 1), t = 1.5x - 2.5 -> fma(1.5, x, -2.5) */
+    if (x <= 1.0f) return fmaf(x * x, fmaf(1.5f, x, -2.5f), 1.0f);
+    if (x < 2.0f) return fmaf(x, fmaf(x, fmaf(-0.5f, x, 2.5f), -4.0f), 2.0f);
+    return 0.0f;
+  }
   if (x <= 1.0f) return x * x * (1.5f * x - 2.5f) + 1.0f;
   if (x < 2.0f) return x * (x * (-0.5f * x + 2.5f) - 4.0f) + 2.0f;
   return 0.0f;
@@ -131,9 +165,9 @@ static inline float cubic(float x) {
 /* [A.3] warpBackward: 4x4(5x5) cubic gather of I1, I1x, I1y at (x+u1, y+u2) with
  * texture clamp, weight-normalised; grad = I1wx^2 + I1wy^2;
  * rho_c = I1w - I1wx*u1 - I1wy*u2 - I0. */
-void orc_warp_backward(const float *I0, const float *I1, const float *I1x, const float *I1y,
-                       const float *u1, const float *u2, int w, int h, float *I1wx,
-                       float *I1wy, float *grad, float *rho_c) {
+static void warp_backward(const float *I0, const float *I1, const float *I1x, const float *I1y,
+                          const float *u1, const float *u2, int w, int h, float *I1wx,
+                          float *I1wy, float *grad, float *rho_c, int fma_mode) {
 #pragma omp parallel for schedule(static)
   for (int y = 0; y < h; ++y)
     for (int x = 0; x < w; ++x) {
@@ -151,11 +185,17 @@ void orc_warp_backward(const float *I0, const float *I1, const float *I1x, const
         const int ry = imin(imax(cy, 0), h - 1);
         for (int cx = xmin; cx <= xmax; ++cx) {
           const int rx = imin(imax(cx, 0), w - 1);
-          const float wgt = cubic(wx - (float)cx) * cubic(wy - (float)cy);
+          const float wgt = cubic(wx - (float)cx, fma_mode) * cubic(wy - (float)cy, fma_mode);
           const size_t j = IDX(rx, ry, w);
-          sum = sum + wgt * I1[j];
-          sumx = sumx + wgt * I1x[j];
-          sumy = sumy + wgt * I1y[j];
+          if (fma_mode) { /* FMA: sum + w*I -> fma(w, I, sum) */
+            sum = fmaf(wgt, I1[j], sum);
+            sumx = fmaf(wgt, I1x[j], sumx);
+            sumy = fmaf(wgt, I1y[j], sumy);
+          } else {
+            sum = sum + wgt * I1[j];
+            sumx = sumx + wgt * I1x[j];
+            sumy = sumy + wgt * I1y[j];
+          }
           wsum = wsum + wgt;
         }
       }
@@ -167,9 +207,21 @@ void orc_warp_backward(const float *I0, const float *I1, const float *I1x, const
       I1wy[i] = I1wyv;
       const float Ix2 = I1wxv * I1wxv;
       const float Iy2 = I1wyv * I1wyv;
-      grad[i] = Ix2 + Iy2;
-      rho_c[i] = I1wv - I1wxv * u1v - I1wyv * u2v - I0[i];
+      if (fma_mode) { /* FMA: Ix2 + Iy2 -> fma(I1wx, I1wx, Iy2); the two products of rho_c
+                       * fused into the running difference */
+        grad[i] = fmaf(I1wxv, I1wxv, Iy2);
+        rho_c[i] = fmaf(-I1wyv, u2v, fmaf(-I1wxv, u1v, I1wv)) - I0[i];
+      } else {
+        grad[i] = Ix2 + Iy2;
+        rho_c[i] = I1wv - I1wxv * u1v - I1wyv * u2v - I0[i];
+      }
     }
+}
+
+void orc_warp_backward(const float *I0, const float *I1, const float *I1x, const float *I1y,
+                       const float *u1, const float *u2, int w, int h, float *I1wx,
+                       float *I1wy, float *grad, float *rho_c) {
+  warp_backward(I0, I1, I1x, I1y, u1, u2, w, h, I1wx, I1wy, grad, rho_c, 0);
 }
 
 /* [A.3] backward-difference divergence with OpenCV's special row/column 0 forms
@@ -186,11 +238,11 @@ static inline float divergence(const float *v1, const float *v2, int y, int x, i
 }
 
 /* [A.3] estimateU: TH thresholding + u = v + theta * div(p). */
-double orc_estimate_u(const float *I1wx, const float *I1wy, const float *grad,
-                      const float *rho_c, const float *p11, const float *p12,
-                      const float *p21, const float *p22, const float *p31,
-                      const float *p32, float *u1, float *u2, float *u3, int w, int h,
-                      float l_t, float theta, float gamma, int calc_error) {
+static double estimate_u(const float *I1wx, const float *I1wy, const float *grad,
+                         const float *rho_c, const float *p11, const float *p12,
+                         const float *p21, const float *p22, const float *p31,
+                         const float *p32, float *u1, float *u2, float *u3, int w, int h,
+                         float l_t, float theta, float gamma, int calc_error, int fma_mode) {
   double *rows = calc_error ? (double *)calloc((size_t)h, sizeof(double)) : NULL;
 #pragma omp parallel for schedule(static)
   for (int y = 0; y < h; ++y) {
@@ -205,7 +257,10 @@ double orc_estimate_u(const float *I1wx, const float *I1wy, const float *grad,
       const float u3o = gamma != 0.0f ? u3[i] : 0.0f;
       /* rho = rho_c + (I1wx*u1 + I1wy*u2 + gamma*u3) -- gamma*u3 inside the
        * parentheses (with gamma = 0 either association gives the same bits) */
-      const float rho = rho_c[i] + (I1wxv * u1o + I1wyv * u2o + gamma * u3o);
+      /* FMA: rho_c + fma(gamma, u3, fma(I1wx, u1, I1wy*u2)) (u3 = 0 when gamma = 0: the fma
+       * still turns a -0 sum into +0) */
+      const float rho = fma_mode ? rho_c[i] + fmaf(gamma, u3o, fmaf(I1wxv, u1o, I1wyv * u2o))
+                                 : rho_c[i] + (I1wxv * u1o + I1wyv * u2o + gamma * u3o);
       float d1 = 0.0f, d2 = 0.0f, d3 = 0.0f;
       if (rho < -l_t * gradv) {
         d1 = l_t * I1wxv;
@@ -227,15 +282,16 @@ double orc_estimate_u(const float *I1wx, const float *I1wy, const float *grad,
       const float div1 = divergence(p11, p12, y, x, w);
       const float div2 = divergence(p21, p22, y, x, w);
       const float div3 = gamma != 0.0f ? divergence(p31, p32, y, x, w) : 0.0f;
-      const float u1n = v1 + theta * div1;
-      const float u2n = v2 + theta * div2;
+      /* FMA: v + theta*div -> fma(theta, div, v) */
+      const float u1n = fma_mode ? fmaf(theta, div1, v1) : v1 + theta * div1;
+      const float u2n = fma_mode ? fmaf(theta, div2, v2) : v2 + theta * div2;
       u1[i] = u1n;
       u2[i] = u2n;
-      if (gamma != 0.0f) u3[i] = v3 + theta * div3;
+      if (gamma != 0.0f) u3[i] = fma_mode ? fmaf(theta, div3, v3) : v3 + theta * div3;
       if (calc_error) {
-        const float n1 = (u1o - u1n) * (u1o - u1n);
-        const float n2 = (u2o - u2n) * (u2o - u2n);
-        rsum += (double)(n1 + n2);
+        const float e1 = u1o - u1n, e2 = u2o - u2n;
+        /* FMA: n1 + n2 -> fma(e1, e1, e2*e2) */
+        rsum += (double)(fma_mode ? fmaf(e1, e1, e2 * e2) : e1 * e1 + e2 * e2);
       }
     }
     if (rows) rows[y] = rsum;
@@ -248,13 +304,31 @@ double orc_estimate_u(const float *I1wx, const float *I1wy, const float *grad,
   return total;
 }
 
-static inline float hypot_f(float a, float b) { return sqrtf(a * a + b * b); }
+double orc_estimate_u(const float *I1wx, const float *I1wy, const float *grad,
+                      const float *rho_c, const float *p11, const float *p12,
+                      const float *p21, const float *p22, const float *p31,
+                      const float *p32, float *u1, float *u2, float *u3, int w, int h,
+                      float l_t, float theta, float gamma, int calc_error) {
+  return estimate_u(I1wx, I1wy, grad, rho_c, p11, p12, p21, p22, p31, p32, u1, u2, u3, w, h,
+                    l_t, theta, gamma, calc_error, 0);
+}
+
+/* hypotf restated as sqrt(a*a + b*b) (FMA: fma(a, a, b*b)); CUDA's library hypotf is not
+ * available here */
+static inline float hypot_f(float a, float b, int fma_mode) {
+  return fma_mode ? sqrtf(fmaf(a, a, b * b)) : sqrtf(a * a + b * b);
+}
+
+/* one projection component: p' = (p + taut*du) / ng (FMA: fma(taut, du, p)) */
+static inline float proj(float p, float du, float taut, float ng, int fma_mode) {
+  return (fma_mode ? fmaf(taut, du, p) : p + taut * du) / ng;
+}
 
 /* [A.3] estimateDualVariables: forward differences (0 at last col/row),
- * ng = 1 + taut*|grad u|, p = (p + taut*grad u) / ng. */
-void orc_estimate_dual(const float *u1, const float *u2, const float *u3, float *p11,
-                       float *p12, float *p21, float *p22, float *p31, float *p32, int w,
-                       int h, float taut, float gamma) {
+ * ng = 1 + taut*|grad u| (FMA: fma(taut, g, 1)), p = (p + taut*grad u) / ng. */
+static void estimate_dual(const float *u1, const float *u2, const float *u3, float *p11,
+                          float *p12, float *p21, float *p22, float *p31, float *p32, int w,
+                          int h, float taut, float gamma, int fma_mode) {
 #pragma omp parallel for schedule(static)
   for (int y = 0; y < h; ++y) {
     const int yn = imin(y + 1, h - 1);
@@ -265,24 +339,30 @@ void orc_estimate_dual(const float *u1, const float *u2, const float *u3, float 
       const float u1y = u1[IDX(x, yn, w)] - u1[i];
       const float u2x = u2[IDX(xn, y, w)] - u2[i];
       const float u2y = u2[IDX(x, yn, w)] - u2[i];
-      const float g1 = hypot_f(u1x, u1y);
-      const float g2 = hypot_f(u2x, u2y);
-      const float ng1 = 1.0f + taut * g1;
-      const float ng2 = 1.0f + taut * g2;
-      p11[i] = (p11[i] + taut * u1x) / ng1;
-      p12[i] = (p12[i] + taut * u1y) / ng1;
-      p21[i] = (p21[i] + taut * u2x) / ng2;
-      p22[i] = (p22[i] + taut * u2y) / ng2;
+      const float g1 = hypot_f(u1x, u1y, fma_mode);
+      const float g2 = hypot_f(u2x, u2y, fma_mode);
+      const float ng1 = fma_mode ? fmaf(taut, g1, 1.0f) : 1.0f + taut * g1;
+      const float ng2 = fma_mode ? fmaf(taut, g2, 1.0f) : 1.0f + taut * g2;
+      p11[i] = proj(p11[i], u1x, taut, ng1, fma_mode);
+      p12[i] = proj(p12[i], u1y, taut, ng1, fma_mode);
+      p21[i] = proj(p21[i], u2x, taut, ng2, fma_mode);
+      p22[i] = proj(p22[i], u2y, taut, ng2, fma_mode);
       if (gamma != 0.0f) {
         const float u3x = u3[IDX(xn, y, w)] - u3[i];
         const float u3y = u3[IDX(x, yn, w)] - u3[i];
-        const float g3 = hypot_f(u3x, u3y);
-        const float ng3 = 1.0f + taut * g3;
-        p31[i] = (p31[i] + taut * u3x) / ng3;
-        p32[i] = (p32[i] + taut * u3y) / ng3;
+        const float g3 = hypot_f(u3x, u3y, fma_mode);
+        const float ng3 = fma_mode ? fmaf(taut, g3, 1.0f) : 1.0f + taut * g3;
+        p31[i] = proj(p31[i], u3x, taut, ng3, fma_mode);
+        p32[i] = proj(p32[i], u3y, taut, ng3, fma_mode);
       }
     }
   }
+}
+
+void orc_estimate_dual(const float *u1, const float *u2, const float *u3, float *p11,
+                       float *p12, float *p21, float *p22, float *p31, float *p32, int w,
+                       int h, float taut, float gamma) {
+  estimate_dual(u1, u2, u3, p11, p12, p21, p22, p31, p32, w, h, taut, gamma, 0);
 }
 
 /* Build-only median filter: cv::medianBlur on CV_32F
@@ -373,6 +453,10 @@ int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
   int ws[TVL1_MAX_LEVELS], hs[TVL1_MAX_LEVELS];
   const int L = orc_pyramid_sizes(w, h, nsc, prm->scale_step, ws, hs);
   const int use_gamma = prm->gamma != 0.0;
+  /* fma mode for the gamma = 0 path with 0 <= tau/theta < inf (the engine's streaming
+   * kernels; other parameter sets run IEEE there too) */
+  const float taut_f = (float)(prm->tau / prm->theta);
+  const int fma_mode = prm->fast_math == 2 && !use_gamma && taut_f >= 0.0f && taut_f <= FLT_MAX;
 
   level_bufs lv[TVL1_MAX_LEVELS];
   memset(lv, 0, sizeof(lv));
@@ -408,8 +492,8 @@ int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
   orc_convert_u8(I1, pitch1, w, h, lv[0].I1);
   const float fdown = (float)(1.0 / prm->scale_step);
   for (int s = 1; s < L; ++s) {
-    orc_resize_linear(lv[s - 1].I0, ws[s - 1], hs[s - 1], lv[s].I0, ws[s], hs[s], fdown, fdown);
-    orc_resize_linear(lv[s - 1].I1, ws[s - 1], hs[s - 1], lv[s].I1, ws[s], hs[s], fdown, fdown);
+    resize_linear(lv[s - 1].I0, ws[s - 1], hs[s - 1], lv[s].I0, ws[s], hs[s], fdown, fdown, fma_mode);
+    resize_linear(lv[s - 1].I1, ws[s - 1], hs[s - 1], lv[s].I1, ws[s], hs[s], fdown, fdown, fma_mode);
   }
 
   const float l_t = (float)(prm->lambda * prm->theta);
@@ -438,16 +522,16 @@ int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
         orc_median(lv[s].u2, lw, lh, prm->median_filtering, tmp);
         memcpy(lv[s].u2, tmp, N * sizeof(float));
       }
-      orc_warp_backward(lv[s].I0, lv[s].I1, I1x, I1y, lv[s].u1, lv[s].u2, lw, lh, I1wx, I1wy,
-                        grad, rho_c);
+      warp_backward(lv[s].I0, lv[s].I1, I1x, I1y, lv[s].u1, lv[s].u2, lw, lh, I1wx, I1wy, grad,
+                    rho_c, fma_mode);
       double error = DBL_MAX;
       double prevError = 0.0;
       int n;
       for (n = 0; error > scaledEps && n < prm->iterations; ++n) {
         const int calcError = (prm->epsilon > 0) && (n & 1) && (prevError < scaledEps);
-        const double e = orc_estimate_u(I1wx, I1wy, grad, rho_c, p11, p12, p21, p22, p31, p32,
-                                        lv[s].u1, lv[s].u2, lv[s].u3, lw, lh, l_t, theta_f,
-                                        gamma_f, calcError);
+        const double e = estimate_u(I1wx, I1wy, grad, rho_c, p11, p12, p21, p22, p31, p32,
+                                    lv[s].u1, lv[s].u2, lv[s].u3, lw, lh, l_t, theta_f, gamma_f,
+                                    calcError, fma_mode);
         if (calcError) {
           error = e;
           prevError = error;
@@ -456,8 +540,8 @@ int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
           error = DBL_MAX;
           prevError -= scaledEps;
         }
-        orc_estimate_dual(lv[s].u1, lv[s].u2, lv[s].u3, p11, p12, p21, p22, p31, p32, lw, lh,
-                          taut, gamma_f);
+        estimate_dual(lv[s].u1, lv[s].u2, lv[s].u3, p11, p12, p21, p22, p31, p32, lw, lh, taut,
+                      gamma_f, fma_mode);
       }
       level_iters[s] += n;
       if (stats && stats->warp_iterations &&
@@ -470,9 +554,9 @@ int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
     const int dw = ws[s - 1], dh = hs[s - 1];
     const float fxu = (float)(1.0 / ((double)dw / lw));
     const float fyu = (float)(1.0 / ((double)dh / lh));
-    orc_resize_linear(lv[s].u1, lw, lh, lv[s - 1].u1, dw, dh, fxu, fyu);
-    orc_resize_linear(lv[s].u2, lw, lh, lv[s - 1].u2, dw, dh, fxu, fyu);
-    if (use_gamma) orc_resize_linear(lv[s].u3, lw, lh, lv[s - 1].u3, dw, dh, fxu, fyu);
+    resize_linear(lv[s].u1, lw, lh, lv[s - 1].u1, dw, dh, fxu, fyu, fma_mode);
+    resize_linear(lv[s].u2, lw, lh, lv[s - 1].u2, dw, dh, fxu, fyu, fma_mode);
+    if (use_gamma) resize_linear(lv[s].u3, lw, lh, lv[s - 1].u3, dw, dh, fxu, fyu, fma_mode);
     const size_t Nd = (size_t)dw * dh;
     for (size_t i = 0; i < Nd; ++i) {
       lv[s - 1].u1[i] = lv[s - 1].u1[i] * upmul;

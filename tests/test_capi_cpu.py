@@ -69,7 +69,7 @@ def test_create_rejects_bad_params_and_missing_gpu(built):
     bad = capi.make_params(nscales=0)
     assert lib.tvl1_create(C.byref(ctx), 0, C.byref(bad)) == 1        # TVL1_EINVAL
     assert b"nscales" in lib.tvl1_last_error(None)
-    bad = capi.make_params(fast_math=2)
+    bad = capi.make_params(fast_math=3)   # 0 IEEE, 1 fast, 2 fma
     assert lib.tvl1_create(C.byref(ctx), 0, C.byref(bad)) == 1        # TVL1_EINVAL
     assert b"fastMath" in lib.tvl1_last_error(None)
     bad = capi.make_params(profile=2)

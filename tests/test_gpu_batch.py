@@ -54,14 +54,15 @@ def pairs(n, w, h, seed):
     (1, 97, 40, dict(nscales=3, warps=3)),
     (5, 200, 60, dict(nscales=4, warps=3, epsilon=0.0, iterations=7)),   # fixed work
 ])
-@pytest.mark.parametrize("env", ["", "TVL1_BATCH_TB=1", "TVL1_BATCH_WARP=1,TVL1_BATCH_FUSE=0",
-                                 "TVL1_BATCH_FUSE=0"])
-def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw):
-    for k in ("TVL1_BATCH_TB", "TVL1_BATCH_WARP", "TVL1_BATCH_FUSE"):
-        monkeypatch.delenv(k, raising=False)
+@pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0"])
+@pytest.mark.parametrize("math", [0, 2])
+def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw, math):
+    """kb_warp_iter (fused warp + first pass), kb_warp_ring, kb_iterate_roll<K, 2>: IEEE and
+    fma mode, each bit-identical to the oracle in that mode."""
+    monkeypatch.delenv("TVL1_BATCH_FUSE", raising=False)
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
-    p = capi.make_params(**kw)
+    p = capi.make_params(fast_math=math, **kw)
     eng = capi.Engine(p)
     I0s, I1s = pairs(n, w, h, seed=100 + n)
     u, v, st = run_batch(eng, I0s, I1s)
@@ -112,9 +113,13 @@ def test_batch_median(built, kw):
     check_against_oracle(p, I0s, I1s, u, v, st)
 
 
-def test_batch_fast_math_within_tolerance(built):
-    """fast_math = 1 batches (the FM kernels): the oracle's iteration schedule, mean EPE
-    <= 1e-3 px (tests/test_gpu_fastmath.py's bar)."""
+@pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0"])
+def test_batch_fast_math_within_tolerance(built, monkeypatch, env):
+    """fast_math = 1 batches: the oracle's iteration schedule, mean EPE <= 1e-3 px
+    (tests/test_gpu_fastmath.py's bar)."""
+    monkeypatch.delenv("TVL1_BATCH_FUSE", raising=False)
+    for kv in filter(None, env.split(",")):
+        monkeypatch.setenv(*kv.split("="))
     kw = dict(nscales=10, warps=5)
     eng = capi.Engine(capi.make_params(fast_math=1, **kw))
     I0s, I1s = pairs(4, 300, 100, seed=71)

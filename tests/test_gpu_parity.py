@@ -89,51 +89,42 @@ def test_constant_images_give_zero_flow(engine):
     assert np.all(u == 0) and np.all(v == 0)
 
 
-# Every kernel / schedule configuration must give the same bits (selected by env at
-# tvl1_create): TVL1_ITER_MODE=1 -> one iteration per launch (rolling-strip kernel),
-# TVL1_ITER_MODE=2 -> wavefront-pipelined passes (TVL1_ROLL_SEG rows per segment,
-# TVL1_ROLL_PX px per lane), TVL1_ITER_MODE=3 -> hybrid (the default),
-# TVL1_TB_CFG = 0/1/2/3 -> temporally blocked regions 64x32/512thr, 64x32/256thr,
-# 64x64/1024thr, 2 px per lane; TVL1_WARP_MODE=1/0 -> global-memory gather / gradient
-# from I1 in LDS; TVL1_WARP_TH -> warp tile height; TVL1_SPECULATE=1 -> speculative
-# enqueueing at check iterations.
-MODES = ["TVL1_ITER_MODE=0", "TVL1_ITER_MODE=1", "TVL1_ITER_MODE=2", "TVL1_ITER_MODE=3",
-         "TVL1_ITER_MODE=2,TVL1_ROLL_SEG=8", "TVL1_ITER_MODE=2,TVL1_ROLL_SEG=64",
-         "TVL1_ITER_MODE=2,TVL1_ROLL_PX=1", "TVL1_ITER_MODE=2,TVL1_ROLL_PX=1,TVL1_ROLL_SEG=8",
-         "TVL1_ITER_MODE=0,TVL1_TB_CFG_LONG=0", "TVL1_TB_CFG=0", "TVL1_TB_CFG=1",
-         "TVL1_TB_CFG=2", "TVL1_TB_CFG=3", "TVL1_WARP_TH=8", "TVL1_WARP_TH=32",
-         "TVL1_WARP_MODE=1", "TVL1_WARP_MODE=0", "TVL1_WARP_MODE=3",
-         "TVL1_WARP_MODE=3,TVL1_WARP_MARGIN=4", "TVL1_WARP_MODE=3,TVL1_ROLL_SEG=8",
-         "TVL1_WARP_NW=1", "TVL1_WARP_NW=4", "TVL1_WARP_NW=4,TVL1_ROLL_SEG=8",
-         "TVL1_WARP_MODE=4", "TVL1_WARP_MODE=4,TVL1_WARP_NW=1", "TVL1_WARP_MODE=4,TVL1_WARP_NW=4",
-         "TVL1_WARP_MODE=4,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8", "TVL1_FUSE=1",
-         "TVL1_FUSE=1,TVL1_ITER_MODE=2", "TVL1_FUSE=1,TVL1_ROLL_SEG=8,TVL1_WARP_MARGIN=4",
-         "TVL1_BUF_LIMIT=100000", "TVL1_BUF_LIMIT=0",
-         "TVL1_WARP_MARGIN=4", "TVL1_SPECULATE=1",
-         "TVL1_ROLL_PX4_MIN=0", "TVL1_ROLL_PX4_MIN=0,TVL1_ROLL_SEG=8",
-         "TVL1_ROLL_PX4_MIN=0,TVL1_ITER_MODE=2", "TVL1_ROLL_PX_SHORT=2",
-         "TVL1_FUSE_MIN=0", "TVL1_FUSE_MIN=0,TVL1_FUSE_STORE=1", "TVL1_FUSE_MIN=0,TVL1_ROLL_SEG=8",
-         "TVL1_FUSE_MIN=0,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8", "TVL1_FUSE=0",
-         "TVL1_FUSE_MIN=0,TVL1_ROLL_PX4_MIN=0", "TVL1_FUSE_MIN=0,TVL1_WITER_BW=64",
-         "TVL1_FUSE_MIN=0,TVL1_WITER_BW=64,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8"]
-KNOBS = ("TVL1_ITER_MODE", "TVL1_ROLL_SEG", "TVL1_ROLL_PX", "TVL1_ROLL_PX_SHORT", "TVL1_ROLL_PX4_MIN", "TVL1_ROLL_LDS", "TVL1_TB_CFG",
-         "TVL1_TB_CFG_LONG", "TVL1_WARP_MODE",
-         "TVL1_SPECULATE", "TVL1_WARP_TH", "TVL1_WARP_MARGIN", "TVL1_WARP_LDS", "TVL1_WARP_NW", "TVL1_FUSE", "TVL1_FUSE_STORE", "TVL1_FUSE_MIN", "TVL1_WITER_BW",
-         "TVL1_ROLL_FILL", "TVL1_WARP_FILL", "TVL1_BUF_LIMIT")
-
-
-@pytest.mark.parametrize("env", MODES)
-@pytest.mark.parametrize("W,H,seed,kw", [
+# Every shipped kernel instantiation must give the same bits.  The default dispatch
+#  on these small levels reaches k_warp_ring<6,2>, k_iterate_roll<G,1|2,2> and
+# k_iterate_tb<G,32,1,2>; the knobs (read at tvl1_create) reach the rest:
+#   TVL1_ROLL_LONG_MIN=0  >= 3-iteration passes stream too: k_iterate_roll<G,3|4,2>
+#   TVL1_ROLL_PX4_MIN=0   2-iteration passes at 4 px per lane: k_iterate_roll<G,1|2,4>
+#   TVL1_FUSE_MIN=0       warpBackward fused with each warp's first pass: k_warp_iter<6,-,128>
+#   TVL1_FUSE=0           never fused (k_warp_ring + the pass, on every level)
+#   TVL1_ROLL_SEG=8|64    streaming kernels' segment boundaries (8 = many short segments)
+#   TVL1_BUF_LIMIT=N      planes >= N bytes take the 64-bit-addressed kernels: k_warp_img and
+#                         k_iterate_tb for every pass (N = 0: every level)
+# k_iterate<G, true> (tau/theta < 0) and the profile-1 kernels have their own tests below.
+MODES = ["", "TVL1_ROLL_LONG_MIN=0", "TVL1_ROLL_LONG_MIN=0,TVL1_ROLL_SEG=8", "TVL1_ROLL_SEG=8",
+         "TVL1_ROLL_SEG=64", "TVL1_ROLL_PX4_MIN=0", "TVL1_ROLL_PX4_MIN=0,TVL1_ROLL_SEG=8",
+         "TVL1_FUSE_MIN=0", "TVL1_FUSE_MIN=0,TVL1_ROLL_SEG=8", "TVL1_FUSE_MIN=0,TVL1_ROLL_PX4_MIN=0",
+         "TVL1_FUSE=0,TVL1_ROLL_LONG_MIN=0", "TVL1_BUF_LIMIT=100000", "TVL1_BUF_LIMIT=0"]
+KNOBS = ("TVL1_ROLL_SEG", "TVL1_ROLL_PX4_MIN", "TVL1_ROLL_LONG_MIN", "TVL1_FUSE", "TVL1_FUSE_MIN",
+         "TVL1_BUF_LIMIT", "TVL1_BATCH_FUSE")
+CONFIG_CASES = [
     (250, 131, 21, dict(nscales=5, warps=5)),
     (97, 201, 22, dict(nscales=4, warps=3, gamma=0.1)),
     (400, 300, 23, dict(nscales=3, warps=4, epsilon=0.0, iterations=9)),
     (300, 200, 24, dict(nscales=1, warps=2)),
-])
-def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
+]
+
+
+def set_knobs(monkeypatch, env):
     for k in KNOBS:
         monkeypatch.delenv(k, raising=False)
-    for kv in env.split(","):
+    for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
+
+
+@pytest.mark.parametrize("env", MODES)
+@pytest.mark.parametrize("W,H,seed,kw", CONFIG_CASES)
+def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
+    set_knobs(monkeypatch, env)
     p = capi.make_params(**kw)
     eng = capi.Engine(p)
     I0, I1 = synth.gen_pair(W, H, seed=seed)
@@ -142,6 +133,25 @@ def test_kernel_configs_bit_identical(built, monkeypatch, env, W, H, seed, kw):
     ur, vr, sr, wr = checker.oracle_calc(I0, I1, p)
     np.testing.assert_array_equal(wi, wr)
     assert bits_equal(u, ur) and bits_equal(v, vr)
+
+
+# fma mode (tvl1_params.fast_math = 2): nvcc's -fmad=true contraction restated in both the
+# engine and the oracle -- bit-identical too, on every shipped kernel instantiation
+@pytest.mark.parametrize("env", MODES)
+@pytest.mark.parametrize("W,H,seed,kw", [CONFIG_CASES[0], CONFIG_CASES[2],
+                                         (128, 96, 25, dict(median_filtering=5, nscales=4))])
+def test_fma_mode_bit_identical(built, monkeypatch, env, W, H, seed, kw):
+    set_knobs(monkeypatch, env)
+    p = capi.make_params(fast_math=2, **kw)
+    eng = capi.Engine(p)
+    I0, I1 = synth.gen_pair(W, H, seed=seed)
+    u, v, st, wi = eng.calc_host(I0, I1)
+    eng.close()
+    ur, vr, sr, wr = checker.oracle_calc(I0, I1, p)
+    np.testing.assert_array_equal(wi, wr)
+    assert bits_equal(u, ur) and bits_equal(v, vr)
+    ui, vi, _, _ = checker.oracle_calc(I0, I1, capi.make_params(**kw))
+    assert not (bits_equal(u, ui) and bits_equal(v, vi)), "fma mode computed the IEEE result"
 
 
 GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
@@ -159,19 +169,13 @@ def test_engine_reproduces_golden(engine, path):
     assert bits_equal(u, g["u"]) and bits_equal(v, g["v"])
 
 
-@pytest.mark.parametrize("env", ["TVL1_WARP_MODE=2", "TVL1_WARP_MODE=3", "TVL1_WARP_NW=1", "TVL1_WARP_NW=4",
-                                 "TVL1_WARP_MODE=4", "TVL1_WARP_MODE=4,TVL1_WARP_MARGIN=4",
-                                 "TVL1_FUSE=1", "TVL1_FUSE=1,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8",
-                                 "TVL1_WARP_MODE=3,TVL1_WARP_MARGIN=4", "TVL1_FUSE_MIN=0",
-                                 "TVL1_FUSE_MIN=0,TVL1_WARP_MARGIN=4,TVL1_ROLL_SEG=8",
-                                 "TVL1_FUSE_MIN=0,TVL1_WITER_BW=64"])
-def test_large_flow_uses_global_gather_fallback(built, monkeypatch, env):
-    """A ~7 px shift puts taps outside the warp kernels' LDS windows (margin 4-6 px):
-    the global-memory fallback must give the same bits."""
-    for k in KNOBS:
-        monkeypatch.delenv(k, raising=False)
-    for kv in env.split(","):
-        monkeypatch.setenv(*kv.split("="))
+@pytest.mark.parametrize("env", ["", "TVL1_FUSE_MIN=0", "TVL1_FUSE_MIN=0,TVL1_ROLL_SEG=8",
+                                 "TVL1_BUF_LIMIT=0"])
+@pytest.mark.parametrize("math", [0, 2])
+def test_large_flow_uses_global_gather_fallback(built, monkeypatch, env, math):
+    """A ~7 px shift puts taps outside the warp kernels' LDS windows (margin 6 px): the
+    global-memory fallback must give the same bits (IEEE and fma mode)."""
+    set_knobs(monkeypatch, env)
     engine = capi.Engine(capi.make_params())
     from scipy import ndimage
     base = synth.base_texture(192, 160, seed=31)
@@ -179,7 +183,7 @@ def test_large_flow_uses_global_gather_fallback(built, monkeypatch, env):
     I0 = np.clip(np.rint(base), 0, 255).astype(np.uint8)
     I1 = np.clip(np.rint(ndimage.map_coordinates(base, [ys + 6.75, xs - 7.5], order=3,
                                                  mode="nearest")), 0, 255).astype(np.uint8)
-    p = capi.make_params(nscales=4, warps=6)
+    p = capi.make_params(nscales=4, warps=6, fast_math=math)
     engine.set_params(p)
     u, v, st, wi = engine.calc_host(I0, I1)
     engine.close()
