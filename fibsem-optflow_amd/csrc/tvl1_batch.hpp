@@ -139,6 +139,12 @@ __global__ __launch_bounds__(192) void kb_warp_iter(BatchWI bw) {
     w.I0 = bw.I0 + b * bw.ips;
     w.I1 = bw.I1 + b * bw.ips;
     w.store_c = 1;
+    RollBufs &B = w.ra.b;   // group geometry set by the host
+    B.c = a.I1wx;
+    B.us = a.u1s;
+    B.ud = a.u1d;
+    B.ps = a.p11s;
+    B.pd = a.p11d;
   }
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves) return;
@@ -185,6 +191,12 @@ __global__ __launch_bounds__(256) void kb_iterate_roll(BatchRoll br) {
     a.calc_err = bsel_bit(br.sel.cerr, b);
     a.p_zero = bsel_bit(br.sel.pzero, b);
     a.partials = br.partials + (size_t)b * br.nblk;
+    RollBufs &B = ra.b;   // group geometry set by the host
+    B.c = a.I1wx;
+    B.us = a.u1s;
+    B.ud = a.u1d;
+    B.ps = a.p11s;
+    B.pd = a.p11d;
   }
   const int wid =
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));

@@ -616,10 +616,27 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
 
   // ---- launch helpers
   // The streaming kernels (k_iterate_roll, k_warp_ring, k_warp_iter) take 32-bit buffer
-  // byte offsets: a level whose planes reach c->buf_limit bytes uses the 64-bit-addressed
-  // ones (k_warp_img, k_iterate_tb).
-  auto buffer_ok = [&](int s) {
-    return (size_t)g.ps[s] * g.hs[s] * sizeof(float) < c->buf_limit;
+  // byte offsets, and the iteration passes address a whole plane group (RollBufs: up to 6
+  // planes at the level-0 plane stride) through one descriptor: a level whose largest group
+  // reaches c->buf_limit bytes uses the 64-bit-addressed kernels (k_warp_img, k_iterate_tb).
+  const size_t pstride = (size_t)g.ps[0] * g.H * sizeof(float);   // arena plane stride
+  auto group_bytes = [&](int s, int planes) {
+    return (size_t)(planes - 1) * pstride + (size_t)g.ps[s] * g.hs[s] * sizeof(float);
+  };
+  auto buffer_ok = [&](int s) { return group_bytes(s, gam ? 6 : 4) < c->buf_limit; };
+  // the planes of a pass as RollBufs groups (the arena keeps each set's planes contiguous)
+  auto roll_bufs = [&](int s, int uset, int pset, int cbuf) {
+    RollBufs b;
+    b.c = c->C[cbuf][0];
+    b.us = c->U[uset][0];
+    b.ud = c->U[uset ^ 1][0];
+    b.ps = c->Pd[pset][0];
+    b.pd = c->Pd[pset ^ 1][0];
+    b.pstride = (unsigned)pstride;
+    b.cb = (unsigned)group_bytes(s, 3);
+    b.ub = (unsigned)group_bytes(s, gam ? 3 : 2);
+    b.pb = (unsigned)group_bytes(s, gam ? 6 : 4);
+    return b;
   };
   auto gather = [&](int s, int uset, int cbuf, int wp) -> tvl1_status {  // K5 warpBackward
     const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
@@ -761,6 +778,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
         double alg_extra = 0.0;   // the fused warpBackward's algorithmic bytes
         if (fuse && n == 0 && k == 2 && calc_end) {
           WarpIterArgs w;
+          w.ra.b = roll_bufs(s, ui, pi, cb);
           w.ra.it = a;
           w.ra.it.I1wx = c->C[cb][0];
           w.ra.it.I1wy = c->C[cb][1];
@@ -805,6 +823,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           hbm = Nl * 4.0 * (ld_planes + st_planes) * k;
         } else if (roll_ok && (k <= 2 || roll_long)) {
           RollArgs ra;
+          ra.b = roll_bufs(s, ui, pi, cb);
           ra.it = a;
           const int px = k <= 2 && (long)lw * lh >= c->roll_px4_min ? 4 : 2;
           const int halo = (k + px - 1) / px * px;   // roll_halo<K, PX>
@@ -1082,6 +1101,16 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
     const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
     BatchMask pzero{};   // p = 0 at every level start
     for (int b = 0; b < n; ++b) pzero.set(b);
+    // RollBufs geometry of the batch arena (the kernels point it at each pair's planes)
+    RollBufs batch_bufs{};
+    {
+      const size_t bstride = (size_t)(c->bC[1] - c->bC[0]) * sizeof(float);
+      const size_t lvl = (size_t)P * lh * sizeof(float);
+      batch_bufs.pstride = (unsigned)bstride;
+      batch_bufs.cb = (unsigned)(2 * bstride + lvl);
+      batch_bufs.ub = (unsigned)(bstride + lvl);
+      batch_bufs.pb = (unsigned)(3 * bstride + lvl);
+    }
     IterArgs it{};   // pass geometry and scalars (plane pointers are set per pair)
     it.W = lw;
     it.H = lh;
@@ -1110,6 +1139,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
       const bool fuse = c->batch_fuse && prm.epsilon > 0 && prm.iterations >= 2;
       if (fuse) {
         BatchWI wi{};
+        wi.w.ra.b = batch_bufs;
         wi.w.ra.it = it;
         wi.w.ra.bands = (lw + 123) / 124;
         wi.w.ra.seg_rows = roll_segment(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots);
@@ -1220,6 +1250,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         int blocks;   // residual partials per pair
         {   // wavefront pipelines: 128-px bands down the whole level, one per wave
           BatchRoll br{};
+          br.ra.b = batch_bufs;
           br.ra.it = it;
           const int halo = (K + 1) / 2 * 2;   // roll_halo<K, 2>
           br.ra.bands = (lw + 128 - 2 * halo - 1) / (128 - 2 * halo);
@@ -1700,19 +1731,29 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pi
   const float taut = (float)(prm.tau / prm.theta);
   // the batched kernels cover the reference's path with gamma = 0 (every production
   // config); other parameter sets solve the pairs one by one, same results
-  const bool batched = prm.profile == 0 && prm.gamma == 0.0 && taut >= 0.0f && taut <= FLT_MAX;
+  bool batched = prm.profile == 0 && prm.gamma == 0.0 && taut >= 0.0f && taut <= FLT_MAX;
   // chunk size: kBatchMax pairs, fewer when their batch arena would not fit in half of
   // the device memory free now (large frames: one chunk of 256 6144x4096 pairs is 0.7 TB)
   int chunk = kBatchMax;
   if (batched) {
+    // the batched passes address the 4 p planes of every pair of a chunk through one buffer
+    // descriptor (RollBufs): that group must stay below 2 GiB
+    const double pplane = (double)align_up((size_t)c->geo.ps[0] * H, 64) * sizeof(float);
+    const int nmax = (int)((double)(((size_t)1 << 31) - 8192) / (4.0 * pplane));
+    if (nmax < 1)
+      batched = false;   // frames this large solve one by one (tvl1_calc's fallbacks)
+    else
+      chunk = std::min(chunk, nmax);
+  }
+  if (batched) {
     const Geometry &g = c->geo;
-    double per_pair = 19.0 * align_up((size_t)g.ps[0] * H, 64) * sizeof(float);
+    double per_pair = 15.0 * align_up((size_t)g.ps[0] * H, 64) * sizeof(float);
     for (int l = 0; l < g.L; ++l) per_pair += 2.0 * (double)g.ps[l] * g.hs[l] * sizeof(float);
     per_pair += (((W + 55) / 56) * ((H + 23) / 24) + 64) * sizeof(double);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
       const double avail = 0.5 * (double)free_b + (double)c->barena_bytes;
-      chunk = (int)std::max(1.0, std::min((double)kBatchMax, avail / per_pair));
+      chunk = (int)std::max(1.0, std::min((double)chunk, avail / per_pair));
     }
   }
   // other contexts on the device may take memory between hipMemGetInfo and the arena's

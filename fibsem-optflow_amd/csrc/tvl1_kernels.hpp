@@ -106,19 +106,20 @@ __device__ __forceinline__ void bstore(float *p, unsigned bytes, unsigned voff, 
 }
 // PX consecutive floats of a plane (4-, 8- or 16-byte store)
 template <int PX>
-__device__ __forceinline__ void bstorev(float *p, unsigned bytes, unsigned voff, const float (&v)[PX]) {
+__device__ __forceinline__ void bstorev(float *p, unsigned bytes, unsigned voff, const float (&v)[PX],
+                                        unsigned soff = 0) {
   if constexpr (PX == 1) {
-    bstore(p, bytes, voff, 0, v[0]);
+    bstore(p, bytes, voff, soff, v[0]);
   } else if constexpr (PX == 4) {
     using T = decltype(__builtin_amdgcn_raw_buffer_load_b128(plane_rsrc(p, bytes), 0, 0, 0));
     T t;
     __builtin_memcpy(&t, v, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(t, plane_rsrc(p, bytes), (int)voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(t, plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
   } else {
     using T = decltype(__builtin_amdgcn_raw_buffer_load_b64(plane_rsrc(p, bytes), 0, 0, 0));
     T t;
     __builtin_memcpy(&t, v, 8);
-    __builtin_amdgcn_raw_buffer_store_b64(t, plane_rsrc(p, bytes), (int)voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(t, plane_rsrc(p, bytes), (int)voff, (int)soff, 0);
   }
 }
 // PX consecutive floats of a plane (4-, 8- or 16-byte load)
@@ -1428,7 +1429,23 @@ constexpr int kRollAhead = 2;   // input rows loaded ahead of the row entering t
 template <int PX>
 constexpr int roll_ahead() { return PX == 4 ? 1 : kRollAhead; }
 
+// The planes of a streaming pass as five buffer groups, one 4-SGPR descriptor each: the
+// warp constants (I1wx, I1wy, rho), the u set read and the u set written (u1, u2, u3), the
+// p set read and the p set written (p11, p12, p21, p22, p31, p32).  Plane k of a group sits
+// at byte offset k * pstride from its base (the arena lays a set's planes out contiguously)
+// and is addressed through the scalar offset.  One descriptor per plane (16) spilled SGPRs
+// into VGPR lanes in the unrolled pipelines.  A group spans < 2 GiB (the host checks), so a
+// masked store's offset kOOB lands past its records whatever the scalar offset.
+struct RollBufs {
+  const float *c;          // I1wx | I1wy | rho
+  const float *us, *ps;    // u, p read
+  float *ud, *pd;          // u, p written
+  unsigned cb, ub, pb;     // group bytes (descriptor records) of c, u, p
+  unsigned pstride;        // bytes between the planes of a group
+};
+
 struct RollArgs {
+  RollBufs b;
   IterArgs it;
   int bands;      // column bands per row: ceil(W / (64 PX - 2 halo))
   int seg_rows;   // output rows per segment
@@ -1453,21 +1470,22 @@ struct RollIn {   // one input row at this lane's PX px
 // p is loaded unconditionally and zeroed by a select when p == 0 (first pass of a level):
 // a branch here would make the compiler's wait counts conservative for every row.
 template <bool G, int PX>
-__device__ __forceinline__ void roll_load(RollIn<G, PX> &v, const IterArgs &a, unsigned nb,
-                                          unsigned soff, unsigned voff) {
-  bload<PX>(v.wx, a.I1wx, nb, voff, soff);
-  bload<PX>(v.wy, a.I1wy, nb, voff, soff);
-  bload<PX>(v.rh, a.rho, nb, voff, soff);
-  bload<PX>(v.u1, a.u1s, nb, voff, soff);
-  bload<PX>(v.u2, a.u2s, nb, voff, soff);
-  if (G) bload<PX>(v.u3, a.u3s, nb, voff, soff);
-  bload<PX>(v.p11, a.p11s, nb, voff, soff);
-  bload<PX>(v.p12, a.p12s, nb, voff, soff);
-  bload<PX>(v.p21, a.p21s, nb, voff, soff);
-  bload<PX>(v.p22, a.p22s, nb, voff, soff);
+__device__ __forceinline__ void roll_load(RollIn<G, PX> &v, const RollBufs &B, unsigned soff,
+                                          unsigned voff) {
+  const unsigned ps = B.pstride;
+  bload<PX>(v.wx, B.c, B.cb, voff, soff);
+  bload<PX>(v.wy, B.c, B.cb, voff, soff + ps);
+  bload<PX>(v.rh, B.c, B.cb, voff, soff + 2 * ps);
+  bload<PX>(v.u1, B.us, B.ub, voff, soff);
+  bload<PX>(v.u2, B.us, B.ub, voff, soff + ps);
+  if (G) bload<PX>(v.u3, B.us, B.ub, voff, soff + 2 * ps);
+  bload<PX>(v.p11, B.ps, B.pb, voff, soff);
+  bload<PX>(v.p12, B.ps, B.pb, voff, soff + ps);
+  bload<PX>(v.p21, B.ps, B.pb, voff, soff + 2 * ps);
+  bload<PX>(v.p22, B.ps, B.pb, voff, soff + 3 * ps);
   if (G) {
-    bload<PX>(v.p31, a.p31s, nb, voff, soff);
-    bload<PX>(v.p32, a.p32s, nb, voff, soff);
+    bload<PX>(v.p31, B.ps, B.pb, voff, soff + 4 * ps);
+    bload<PX>(v.p32, B.ps, B.pb, voff, soff + 5 * ps);
   }
 }
 
@@ -1517,28 +1535,29 @@ __device__ __forceinline__ float right_of(const float (&v)[PX], int j) {
 // instead of u^0
 template <bool G, int K, int PX, bool VIN = false, int FM = 0>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
-                                             const IterArgs &a, int r, const RollLane &L,
-                                             unsigned nb, unsigned rowb, double &acc);
+                                             const IterArgs &a, const RollBufs &B, int r,
+                                             const RollLane &L, unsigned rowb, double &acc);
 
 template <bool G, int K, int PX, int FM>
 __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
-                                          RollIn<G, PX> &ahead, const IterArgs &a, int r,
-                                          const RollLane &L, unsigned nb, unsigned rowb,
-                                          double &acc) {
-  roll_load<G, PX>(ahead, a, nb, (unsigned)imin(r + roll_ahead<PX>(), a.H - 1) * rowb, L.vload);
+                                          RollIn<G, PX> &ahead, const IterArgs &a,
+                                          const RollBufs &B, int r, const RollLane &L,
+                                          unsigned rowb, double &acc) {
+  roll_load<G, PX>(ahead, B, (unsigned)imin(r + roll_ahead<PX>(), a.H - 1) * rowb, L.vload);
   // keep the loads of row r + roll_ahead ahead of this step's stores: waiting for them
   // roll_ahead steps later then leaves the younger stores and loads in flight (vmcnt
   // counts in issue order)
   __builtin_amdgcn_sched_barrier(0);
-  roll_advance<G, K, PX, false, FM>(S, in, a, r, L, nb, rowb, acc);
+  roll_advance<G, K, PX, false, FM>(S, in, a, B, r, L, rowb, acc);
 }
 
 // The compute and stores of one step: input row r (in `in`) enters stage 0 and every
 // stage advances one row.
 template <bool G, int K, int PX, bool VIN, int FM>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
-                                             const IterArgs &a, int r, const RollLane &L,
-                                             unsigned nb, unsigned rowb, double &acc) {
+                                             const IterArgs &a, const RollBufs &B, int r,
+                                             const RollLane &L, unsigned rowb, double &acc) {
+  const unsigned ps = B.pstride;
   static_assert(!VIN || K >= 2, "stage 1's u^0 (replaced by v) is the K = 1 residual's input");
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
@@ -1594,9 +1613,9 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
     }
     if (n == K) {
       const unsigned vo = stU ? (unsigned)yU * rowb + L.vst : kOOB;
-      bstorev<PX>(a.u1d, nb, vo, S.U1c[n]);
-      bstorev<PX>(a.u2d, nb, vo, S.U2c[n]);
-      if (G) bstorev<PX>(a.u3d, nb, vo, S.U3c[n]);
+      bstorev<PX>(B.ud, B.ub, vo, S.U1c[n]);
+      bstorev<PX>(B.ud, B.ub, vo, S.U2c[n], ps);
+      if (G) bstorev<PX>(B.ud, B.ub, vo, S.U3c[n], 2 * ps);
     }
 
     const int yD = r - n;        // estimateDualVariables row of stage n
@@ -1616,13 +1635,13 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
     }
     if (n == K) {
       const unsigned vo = L.out && yD >= L.ys && yD < L.ye ? (unsigned)yD * rowb + L.vst : kOOB;
-      bstorev<PX>(a.p11d, nb, vo, S.P11c[n]);
-      bstorev<PX>(a.p12d, nb, vo, S.P12c[n]);
-      bstorev<PX>(a.p21d, nb, vo, S.P21c[n]);
-      bstorev<PX>(a.p22d, nb, vo, S.P22c[n]);
+      bstorev<PX>(B.pd, B.pb, vo, S.P11c[n]);
+      bstorev<PX>(B.pd, B.pb, vo, S.P12c[n], ps);
+      bstorev<PX>(B.pd, B.pb, vo, S.P21c[n], 2 * ps);
+      bstorev<PX>(B.pd, B.pb, vo, S.P22c[n], 3 * ps);
       if (G) {
-        bstorev<PX>(a.p31d, nb, vo, S.P31c[n]);
-        bstorev<PX>(a.p32d, nb, vo, S.P32c[n]);
+        bstorev<PX>(B.pd, B.pb, vo, S.P31c[n], 4 * ps);
+        bstorev<PX>(B.pd, B.pb, vo, S.P32c[n], 5 * ps);
       }
     }
   }
@@ -1639,6 +1658,7 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   constexpr int HALO = roll_halo<K, PX>();
   constexpr int BW = 64 * PX;            // band width (px)
   const IterArgs &a = ra.it;
+  const RollBufs &B = ra.b;
   const int lane = threadIdx.x & 63;
   const int band = wid % ra.bands, seg = wid / ra.bands;
   RollLane L;
@@ -1648,7 +1668,6 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   L.vload = 4u * imin(imax(L.X, 0), a.P - PX);
   L.out = PX * lane >= HALO && PX * lane < BW - HALO && L.X < a.W;
   L.vst = 4u * (unsigned)imax(L.X, 0);
-  const unsigned nb = 4u * (unsigned)a.P * (unsigned)a.H;   // plane bytes
   const unsigned rowb = 4u * (unsigned)a.P;                 // row pitch in bytes
   L.ys = seg * ra.seg_rows;
   L.ye = imin(L.ys + ra.seg_rows, a.H);
@@ -1676,41 +1695,42 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
     float z[PX];
 #pragma unroll
     for (int j = 0; j < PX; ++j) z[j] = 0.0f;
-    bstorev<PX>(a.u1d, nb, kOOB, z);
-    bstorev<PX>(a.u2d, nb, kOOB, z);
-    if (G) bstorev<PX>(a.u3d, nb, kOOB, z);
-    bstorev<PX>(a.p11d, nb, kOOB, z);
-    bstorev<PX>(a.p12d, nb, kOOB, z);
-    bstorev<PX>(a.p21d, nb, kOOB, z);
-    bstorev<PX>(a.p22d, nb, kOOB, z);
+    const unsigned ps = B.pstride;
+    bstorev<PX>(B.ud, B.ub, kOOB, z);
+    bstorev<PX>(B.ud, B.ub, kOOB, z, ps);
+    if (G) bstorev<PX>(B.ud, B.ub, kOOB, z, 2 * ps);
+    bstorev<PX>(B.pd, B.pb, kOOB, z);
+    bstorev<PX>(B.pd, B.pb, kOOB, z, ps);
+    bstorev<PX>(B.pd, B.pb, kOOB, z, 2 * ps);
+    bstorev<PX>(B.pd, B.pb, kOOB, z, 3 * ps);
     if (G) {
-      bstorev<PX>(a.p31d, nb, kOOB, z);
-      bstorev<PX>(a.p32d, nb, kOOB, z);
+      bstorev<PX>(B.pd, B.pb, kOOB, z, 4 * ps);
+      bstorev<PX>(B.pd, B.pb, kOOB, z, 5 * ps);
     }
   };
   double acc = 0.0;
   if constexpr (roll_ahead<PX>() == 1) {   // 2-row ring, steps unrolled by 2
-    RollIn<G, PX> A, B;
-    roll_load<G, PX>(A, a, nb, (unsigned)r0 * rowb, L.vload);
+    RollIn<G, PX> A, Bx;
+    roll_load<G, PX>(A, B, (unsigned)r0 * rowb, L.vload);
     dummy_stores();
     const int halves = (L.ye + K - r0 + 1) / 2;
     for (int h = 0, r = r0; h < halves; ++h, r += 2) {
-      roll_step<G, K, PX, FM>(S, A, B, a, r, L, nb, rowb, acc);
-      roll_step<G, K, PX, FM>(S, B, A, a, r + 1, L, nb, rowb, acc);
+      roll_step<G, K, PX, FM>(S, A, Bx, a, B, r, L, rowb, acc);
+      roll_step<G, K, PX, FM>(S, Bx, A, a, B, r + 1, L, rowb, acc);
     }
   } else {   // 3-row ring, steps unrolled by 3
     static_assert(roll_ahead<PX>() == 2, "the step loop below is unrolled for a 3-row ring");
-    RollIn<G, PX> A, B, C;
-    roll_load<G, PX>(A, a, nb, (unsigned)r0 * rowb, L.vload);
+    RollIn<G, PX> A, Bx, C;
+    roll_load<G, PX>(A, B, (unsigned)r0 * rowb, L.vload);
     dummy_stores();
-    roll_load<G, PX>(B, a, nb, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
+    roll_load<G, PX>(Bx, B, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
     dummy_stores();
     // steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K (rows >= H drain the pipeline)
     const int thirds = (L.ye + K - r0 + 2) / 3;
     for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
-      roll_step<G, K, PX, FM>(S, A, C, a, r, L, nb, rowb, acc);
-      roll_step<G, K, PX, FM>(S, B, A, a, r + 1, L, nb, rowb, acc);
-      roll_step<G, K, PX, FM>(S, C, B, a, r + 2, L, nb, rowb, acc);
+      roll_step<G, K, PX, FM>(S, A, C, a, B, r, L, rowb, acc);
+      roll_step<G, K, PX, FM>(S, Bx, A, a, B, r + 1, L, rowb, acc);
+      roll_step<G, K, PX, FM>(S, C, Bx, a, B, r + 2, L, rowb, acc);
     }
   }
   if (a.calc_err) {
@@ -1857,21 +1877,22 @@ struct WiP {   // the consumer's HBM input of one row: p at its PX px
 };
 
 template <int PX>
-__device__ __forceinline__ void wi_p_load(WiP<PX> &v, const IterArgs &a, unsigned nb, unsigned soff,
+__device__ __forceinline__ void wi_p_load(WiP<PX> &v, const RollBufs &B, unsigned soff,
                                           unsigned voff) {
-  bload<PX>(v.p11, a.p11s, nb, voff, soff);
-  bload<PX>(v.p12, a.p12s, nb, voff, soff);
-  bload<PX>(v.p21, a.p21s, nb, voff, soff);
-  bload<PX>(v.p22, a.p22s, nb, voff, soff);
+  const unsigned ps = B.pstride;
+  bload<PX>(v.p11, B.ps, B.pb, voff, soff);
+  bload<PX>(v.p12, B.ps, B.pb, voff, soff + ps);
+  bload<PX>(v.p21, B.ps, B.pb, voff, soff + 2 * ps);
+  bload<PX>(v.p22, B.ps, B.pb, voff, soff + 3 * ps);
 }
 
 template <int FM, int PX>
 __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
                                              const float *__restrict__ cring, const WiP<PX> &cur,
-                                             WiP<PX> &ahead, const IterArgs &a, int r,
-                                             const RollLane &L, int lane, unsigned nb,
-                                             unsigned rowb, double &acc) {
-  wi_p_load(ahead, a, nb, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vload);
+                                             WiP<PX> &ahead, const IterArgs &a,
+                                             const RollBufs &B, int r, const RollLane &L,
+                                             int lane, unsigned rowb, double &acc) {
+  wi_p_load(ahead, B, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vload);
   __builtin_amdgcn_sched_barrier(0);
   lds_barrier();   // C ring row r was written at the previous step
   constexpr int BW = 64 * PX;
@@ -1889,7 +1910,7 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
     in.p21[j] = cur.p21[j]; in.p22[j] = cur.p22[j];
     in.p31[j] = in.p32[j] = 0.0f;
   }
-  roll_advance<false, 2, PX, true, FM>(S, in, a, r, L, nb, rowb, acc);
+  roll_advance<false, 2, PX, true, FM>(S, in, a, B, r, L, rowb, acc);
 }
 
 template <int M, int FM, int BW>
@@ -1938,28 +1959,30 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
 #pragma unroll
       for (int j = 0; j < PX; ++j) S.CX[n][j] = S.CY[n][j] = S.CR[n][j] = 0.0f;
     // as many dropped stores after each prologue load as a step issues (k_iterate_roll)
+    const RollBufs &Bf = ra.b;
     auto dummy_stores = [&]() {
       float z[PX];
 #pragma unroll
       for (int j = 0; j < PX; ++j) z[j] = 0.0f;
-      bstorev<PX>(a.u1d, nb, kOOB, z);
-      bstorev<PX>(a.u2d, nb, kOOB, z);
-      bstorev<PX>(a.p11d, nb, kOOB, z);
-      bstorev<PX>(a.p12d, nb, kOOB, z);
-      bstorev<PX>(a.p21d, nb, kOOB, z);
-      bstorev<PX>(a.p22d, nb, kOOB, z);
+      const unsigned ps = Bf.pstride;
+      bstorev<PX>(Bf.ud, Bf.ub, kOOB, z);
+      bstorev<PX>(Bf.ud, Bf.ub, kOOB, z, ps);
+      bstorev<PX>(Bf.pd, Bf.pb, kOOB, z);
+      bstorev<PX>(Bf.pd, Bf.pb, kOOB, z, ps);
+      bstorev<PX>(Bf.pd, Bf.pb, kOOB, z, 2 * ps);
+      bstorev<PX>(Bf.pd, Bf.pb, kOOB, z, 3 * ps);
     };
     WiP<PX> A, B, C;
-    wi_p_load(A, a, nb, (unsigned)r0 * rowb, L.vload);
+    wi_p_load(A, Bf, (unsigned)r0 * rowb, L.vload);
     dummy_stores();
-    wi_p_load(B, a, nb, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
+    wi_p_load(B, Bf, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
     dummy_stores();
     lds_barrier();   // the producers' first step (row r0)
     double acc = 0.0;
     for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
-      wi_cons_step<FM, PX>(S, cring, A, C, a, r, L, lane, nb, rowb, acc);
-      wi_cons_step<FM, PX>(S, cring, B, A, a, r + 1, L, lane, nb, rowb, acc);
-      wi_cons_step<FM, PX>(S, cring, C, B, a, r + 2, L, lane, nb, rowb, acc);
+      wi_cons_step<FM, PX>(S, cring, A, C, a, Bf, r, L, lane, rowb, acc);
+      wi_cons_step<FM, PX>(S, cring, B, A, a, Bf, r + 1, L, lane, rowb, acc);
+      wi_cons_step<FM, PX>(S, cring, C, B, a, Bf, r + 2, L, lane, rowb, acc);
     }
     lds_barrier();   // the producers' last two steps
     lds_barrier();
