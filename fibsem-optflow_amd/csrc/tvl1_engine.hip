@@ -76,6 +76,8 @@ struct tvl1_ctx {
   long roll_px4_min = 5000000;   // TVL1_ROLL_PX4_MIN: 2-iteration passes take 4 px per lane on
                                  // levels of at least this many px (2 px below: more waves)
   int roll_slots[kRollMax + 1][2][5] = {};   // resident k_iterate_roll<G, K, PX> wavefronts
+  int fill = 100;            // TVL1_FILL: % of the resident slots a single-pair streaming launch
+                             // is sized for (segment rows)
   long roll_long_min = 0;    // >= 3-iteration passes stream (k_iterate_roll) on levels of at
                              // least this many 56 x 32 tiles, else k_iterate_tb
   int warp_ring_slots = 0;   // resident k_warp_ring<6, 2> blocks per device
@@ -663,7 +665,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
       wa.P = P;
       wa.bands = (lw + 63) / 64;
       wa.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                    : roll_segment(wa.bands, lh, 6, c->warp_ring_slots);
+                                    : roll_segment(wa.bands, lh, 6, c->warp_ring_slots * c->fill / 100);
       wa.waves = wa.bands * ((lh + wa.seg_rows - 1) / wa.seg_rows);
 #define WARP_RING(FM) \
   hipLaunchKernelGGL((k_warp_ring<6, 2, FM>), dim3(wa.waves), dim3(128), 0, st, wa);
@@ -793,7 +795,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           constexpr int M = 6, BW = 128;
           w.ra.bands = (lw + BW - 5) / (BW - 4);
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                          : roll_segment(w.ra.bands, lh, 2 + M, c->witer_slots);
+                                          : roll_segment(w.ra.bands, lh, 2 + M, c->witer_slots * c->fill / 100);
           w.ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           w.ra.waves = w.ra.bands * segs;
@@ -830,7 +832,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
           const int out_w = 64 * px - 2 * halo;
           ra.bands = (lw + out_w - 1) / out_w;
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px]);
+                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px] * c->fill / 100);
           ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           ra.waves = ra.bands * segs;
@@ -1642,6 +1644,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
+  if (const char *m = getenv("TVL1_FILL")) c->fill = std::max(10, atoi(m));
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void **)&c->pinned, sizeof(double) * (8 + kBatchMax),

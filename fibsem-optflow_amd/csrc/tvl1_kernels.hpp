@@ -884,8 +884,10 @@ __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, floa
   const float rho =
       CPUP ? (G ? rhoc + (I1wxv * u1o + I1wyv * u2o) + a.gamma * u3o
                 : rhoc + (I1wxv * u1o + I1wyv * u2o))
-      : contracts(FM) ? rhoc + fm_fma(a.gamma, G ? u3o : 0.0f, fm_fma(I1wxv, u1o, I1wyv * u2o))
-           : rhoc + (I1wxv * u1o + I1wyv * u2o + a.gamma * (G ? u3o : 0.0f));
+      // (gamma = 0 in the G = false kernels: gamma*u3 is +0, added as the literal)
+      : contracts(FM) ? rhoc + (G ? fm_fma(a.gamma, u3o, fm_fma(I1wxv, u1o, I1wyv * u2o))
+                                  : fm_fma(I1wxv, u1o, I1wyv * u2o) + 0.0f)
+           : rhoc + (I1wxv * u1o + I1wyv * u2o + (G ? a.gamma * u3o : 0.0f));
   // TH operator, branch-free: the three candidate steps are computed with the
   // reference's exact expressions and the applicable one selected.
   const bool lo = rho < -a.l_t * gradv;
@@ -1050,11 +1052,7 @@ __device__ __forceinline__ float div_short(float a, const Recip &R) {
 __device__ __forceinline__ float th_quot(float rho, float gradv, bool mid) {
   float fi = div_short(-rho, recip_of(gradv));
   const bool bad = mid && __builtin_fabsf(rho) < 0x1p-100f;
-#ifndef TVL1_EXP_NOBRANCH
   if (__ballot(bad)) fi = bad ? -rho / gradv : fi;
-#else
-  (void)bad;
-#endif
   return fi;
 }
 
@@ -1097,12 +1095,7 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
     oa = div_short(na, R);
     ob = div_short(nb, R);
     const bool tiny = __builtin_fabsf(na) < 0x1p-100f || __builtin_fabsf(nb) < 0x1p-100f;
-#ifdef TVL1_EXP_NOBRANCH
-    if (0)
-#else
-    if (__ballot(tiny))
-#endif
-    {
+    if (__ballot(tiny)) {
       oa = tiny ? div_by(na, R) : oa;
       ob = tiny ? div_by(nb, R) : ob;
     }
