@@ -646,7 +646,6 @@ def main():
             "step": f"one batch of {F} pair(s) solved concurrently per GPU (one ctx + stream each)",
             "iterations_per_pair": iters[0],
             "checks_per_pair": stats[0]["checks_total"],
-            "speculation_misses": stats[0]["speculation_misses"],
             "pair_algorithmic_GB": round(pair_bytes / 1e9, 2),
             # SURVEY 8(d) whole-pair byte model / step time, per GPU
             "pair_roofline_frac": round(pair_bytes * args.steps * F / elapsed / 1e9 / HBM_PEAK_GBS, 4),
