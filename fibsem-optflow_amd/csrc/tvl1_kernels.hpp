@@ -484,12 +484,41 @@ __device__ __forceinline__ float rho_c(float I1w, float I1wx, float I1wy, float 
                        : I1w - I1wx * u1 - I1wy * u2 - i0;
 }
 
+// Issue priority falling with a block's progress through its segment (step trip h of n):
+// at equal priority a SIMD's arbiter prefers its oldest wave, so in a one-round launch the
+// blocks dispatched last to a CU finish last and leave the CU part idle meanwhile.  Measured
+// on k_warp_iter at C2 level 0 (tools/wi_probe.hip, per-wave s_memrealtime): block lives of
+// 266 / 296 / 333 / 332 / 414 us by dispatch order on the CU, launch 424 us; with this
+// 327 / 329 / 350 / 356 / 386 us, launch 388 us.  (Progress against the XCD's other
+// blocks, from a per-XCD atomic counter, was slower: 616 us.)
+template <int PRIO>
+__device__ __forceinline__ void progress_prio(int h, int n) {
+  if (!PRIO) return;
+  if (h == 0) __builtin_amdgcn_s_setprio(3);
+  else if (h == n / 4) __builtin_amdgcn_s_setprio(2);
+  else if (h == n / 2) __builtin_amdgcn_s_setprio(1);
+  else if (h == 3 * n / 4) __builtin_amdgcn_s_setprio(0);
+}
+
 // LDS-only workgroup barrier: waits for this wave's LDS writes, not for its global loads
 // in flight (a plain __syncthreads() would drain the prefetch).
+#ifdef TVL1_BARRIER_PROBE
+// tools/wi_probe.hip: shader cycles each wave spends in lds_barrier (one slot per wave)
+__device__ unsigned long long *tvl1_probe_bar;
+#endif
 __device__ __forceinline__ void lds_barrier() {
+#ifdef TVL1_BARRIER_PROBE
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#ifdef TVL1_BARRIER_PROBE
+  const unsigned long long dt = __builtin_amdgcn_s_memtime() - t0;
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_add(tvl1_probe_bar + 3 * blockIdx.x + (threadIdx.x >> 6), dt,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 
 // The window ring is filled from I1 and holds three float planes (I1, I1x, I1y) -- each window slot's
@@ -1906,7 +1935,7 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
   roll_advance<false, 2, PX, true, FM>(S, in, a, B, r, L, rowb, acc);
 }
 
-template <int M, int FM, int BW>
+template <int M, int FM, int BW, int PRIO = 0>
 __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, float *__restrict__ ring,
                                                float *__restrict__ cring) {
   constexpr int K = 2, PX = BW / 64, HALO = roll_halo<2, PX>(), WW = wi_ww<M, BW>();
@@ -1973,6 +2002,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     lds_barrier();   // the producers' first step (row r0)
     double acc = 0.0;
     for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
+      progress_prio<PRIO>(h, thirds);
       wi_cons_step<FM, PX>(S, cring, A, C, a, Bf, r, L, lane, rowb, acc);
       wi_cons_step<FM, PX>(S, cring, B, A, a, Bf, r + 1, L, lane, rowb, acc);
       wi_cons_step<FM, PX>(S, cring, C, B, a, Bf, r + 2, L, lane, rowb, acc);
@@ -2030,6 +2060,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     warp_ring_load(B, wa, nb, rowb, r0 + 1 + M, xs);
     warp_flow_load(B, wa, nb, rowb, r0 + 1, P.xcb);
     for (int h = 0, g = r0; h <= thirds; ++h, g += 3) {
+      progress_prio<PRIO>(h, thirds);
       wi_prod_step<M, FM, BW>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
       wi_prod_step<M, FM, BW>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
       wi_prod_step<M, FM, BW>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
@@ -2037,13 +2068,13 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
   }
 }
 
-template <int M, int FM = 0, int BW = 128>
+template <int M, int FM = 0, int BW = 128, int PRIO = 1>
 __global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
   __shared__ float ring[kWiRows * 3 * wi_ww<M, BW>()];
   __shared__ float cring[2 * 5 * BW];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves) return;   // whole blocks
-  warp_iter_body<M, FM, BW>(w, wid, ring, cring);
+  warp_iter_body<M, FM, BW, PRIO>(w, wid, ring, cring);
 }
 
 // K7: fixed-order sum of the per-block partials (one block).
