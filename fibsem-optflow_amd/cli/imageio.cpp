@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -125,13 +126,83 @@ bool inflate_all(const std::vector<uint8_t> &in, std::vector<uint8_t> &out) {
 }
 }  // namespace
 
+// One Paeth-filtered byte (bpp 1): a = left, b = up, c = up-left (PNG specification 9.4).
+static inline uint8_t paeth_byte(uint8_t in, int a, int b, int c) {
+  const int pa = abs(b - c), pb = abs(a - c), pc = abs(a + b - 2 * c);
+  const int bc = pb <= pc ? b : c;
+  return (uint8_t)(in + ((pa <= pb) & (pa <= pc) ? a : bc));
+}
+
+// Unfilter 4 consecutive Paeth rows of an 8-bit gray image: raw = the first row's filter
+// byte (rows of n + 1 bytes), prev = the row above (zeros for the first), out = 4 rows of
+// n bytes.  Row k runs one column behind row k-1, so at each step the 4 chains are
+// independent; every byte gets the same operations as the one-row loop.
+static void paeth4(const uint8_t *raw, size_t n, const uint8_t *prev, uint8_t *out) {
+  const uint8_t *in[4];
+  const uint8_t *up[4];
+  uint8_t *o[4];
+  for (int k = 0; k < 4; ++k) {
+    in[k] = raw + k * (n + 1) + 1;
+    o[k] = out + k * n;
+    up[k] = k == 0 ? prev : out + (k - 1) * n;
+  }
+  // x = 0: Paeth(0, b, 0) = b; row k's column 0 needs row k-1's column 0 only
+  int a[4];
+  auto step = [&](int k, size_t x) {
+    a[k] = paeth_byte(in[k][x], a[k], up[k][x], up[k][x - 1]);
+    o[k][x] = (uint8_t)a[k];
+  };
+  // prologue: steps t = 0..2 (row k at x = t - k)
+  for (int t = 0; t < 3; ++t)
+    for (int k = 0; k <= t; ++k) {
+      const size_t x = (size_t)(t - k);
+      if (x == 0) {
+        a[k] = (uint8_t)(in[k][0] + up[k][0]);
+        o[k][0] = (uint8_t)a[k];
+      } else {
+        step(k, x);
+      }
+    }
+  for (size_t t = 3; t < n; ++t) {   // all 4 rows active, row 3 at x = t - 3 >= 0... >= 1 here
+    if (t == 3) {
+      step(0, 3);
+      step(1, 2);
+      step(2, 1);
+      a[3] = (uint8_t)(in[3][0] + up[3][0]);
+      o[3][0] = (uint8_t)a[3];
+      continue;
+    }
+    step(0, t);
+    step(1, t - 1);
+    step(2, t - 2);
+    step(3, t - 3);
+  }
+  // epilogue: rows 1..3 finish their last columns
+  for (size_t t = n; t < n + 3; ++t)
+    for (int k = (int)(t - n) + 1; k < 4; ++k) step(k, t - k);
+}
+
+#ifdef OFIO_TIMING
+double ofio_t_inflate = 0, ofio_t_unfilter = 0, ofio_t_chunks = 0;
+#define OFIO_NOW() std::chrono::steady_clock::now()
+#define OFIO_ADD(v, a, b) v += std::chrono::duration<double>((b) - (a)).count()
+#else
+#define OFIO_NOW() 0
+#define OFIO_ADD(v, a, b) (void)0
+#endif
+
 static bool decode_png(const std::string &buf, Image8 &img, std::string &err) {
+  [[maybe_unused]] auto tc0 = OFIO_NOW();
   const uint8_t *p = (const uint8_t *)buf.data();
   const size_t n = buf.size();
   size_t off = 8;
   uint32_t W = 0, H = 0;
   int depth = 0, ctype = -1, interlace = 0;
-  std::vector<uint8_t> idat, plte;
+  // the concatenated IDAT stream and the inflated rows live in per-thread buffers reused
+  // from slice to slice (a fresh 25 MB vector per slice costs its page faults + zero fill)
+  thread_local std::vector<uint8_t> idat;
+  idat.clear();
+  std::vector<uint8_t> plte;
   while (off + 12 <= n) {
     const uint32_t len = be32(p + off);
     const char *type = (const char *)p + off + 4;
@@ -182,11 +253,17 @@ static bool decode_png(const std::string &buf, Image8 &img, std::string &err) {
   }
   const size_t rowbytes = ((size_t)W * ch * depth + 7) / 8;
   const size_t bpp = std::max<size_t>(1, (size_t)ch * depth / 8);
-  std::vector<uint8_t> raw((rowbytes + 1) * H);
+  thread_local std::vector<uint8_t> raw;
+  raw.resize((rowbytes + 1) * H);
+  [[maybe_unused]] auto tc1 = OFIO_NOW();
+  OFIO_ADD(ofio_t_chunks, tc0, tc1);
   if (!inflate_all(idat, raw)) {
     err = "PNG: corrupt image data";
     return false;
   }
+  [[maybe_unused]] auto tc2 = OFIO_NOW();
+  OFIO_ADD(ofio_t_inflate, tc1, tc2);
+  (void)tc2;
   // unfilter (each row: 1 filter byte + rowbytes), one tight loop per filter type; 8-bit
   // gray rows unfilter straight into the image
   const bool gray8 = ctype == 0 && depth == 8;
@@ -197,7 +274,19 @@ static bool decode_png(const std::string &buf, Image8 &img, std::string &err) {
     img.data.resize((size_t)W * H);
   }
   std::vector<uint8_t> zero(rowbytes, 0);
-  for (uint32_t y = 0; y < H; ++y) {
+  for (uint32_t y = 0; y < H;) {
+    // 8-bit gray, 4 consecutive Paeth rows (the usual encoder choice for these slices): the
+    // per-byte chain through the left neighbour is serial within a row, so the 4 rows are
+    // unfiltered together, row k one column behind row k-1 (it needs row k-1's bytes at x
+    // and x-1): 4 independent chains per step instead of one.
+    if (gray8 && bpp == 1 && rowbytes >= 8 && y + 4 <= H && raw[y * (rowbytes + 1)] == 4 &&
+        raw[(y + 1) * (rowbytes + 1)] == 4 && raw[(y + 2) * (rowbytes + 1)] == 4 &&
+        raw[(y + 3) * (rowbytes + 1)] == 4) {
+      paeth4(raw.data() + (size_t)y * (rowbytes + 1), rowbytes,
+             y == 0 ? zero.data() : img.row((int)y - 1), img.row((int)y));
+      y += 4;
+      continue;
+    }
     const uint8_t f = raw[y * (rowbytes + 1)];
     const uint8_t *in = raw.data() + y * (rowbytes + 1) + 1;
     uint8_t *out = gray8 ? img.row((int)y) : px.data() + (size_t)y * rowbytes;
@@ -243,7 +332,9 @@ static bool decode_png(const std::string &buf, Image8 &img, std::string &err) {
         err = "PNG: bad filter type";
         return false;
     }
+    ++y;
   }
+  OFIO_ADD(ofio_t_unfilter, tc2, OFIO_NOW());
   if (gray8) return true;
   img.width = (int)W;
   img.height = (int)H;

@@ -255,6 +255,22 @@ def test_png_every_filter_type(tmp_path, built, kind, inflate, monkeypatch):
     assert np.array_equal(np.array(Image.open(out)), want)
 
 
+@pytest.mark.parametrize("W,H,filters", [(41, 23, [4]), (8, 9, [4]), (7, 13, [4]), (200, 37, [4, 4, 4, 4, 4, 2, 4, 4, 4, 4, 1, 4, 4, 4]),
+                                         (64, 4, [4]), (9, 6, [4, 4, 4, 0])])
+def test_png_paeth_runs(tmp_path, built, W, H, filters):
+    """8-bit gray Paeth rows, which the decoder unfilters 4 rows at a time (imageio.cpp
+    paeth4): runs of Paeth rows broken by other filters, heights not a multiple of 4,
+    widths at and below the interleaved path's minimum."""
+    rng = np.random.default_rng(W * 1000 + H)
+    a = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    a[: H // 2] = (np.add.outer(np.arange(H // 2), np.arange(W)) * 7 % 256).astype(np.uint8)
+    src = tmp_path / "in.png"
+    src.write_bytes(_png_bytes(a, W, H, 0, 8, filters))
+    out = tmp_path / "out.tif"
+    run("--decode", src, out)
+    assert np.array_equal(np.array(Image.open(out)), a)
+
+
 @pytest.mark.parametrize("threads", [1, 3])
 def test_decode_ahead_over_many_chunks(tmp_path, built, threads):
     """The decode-ahead pool (build-only "decode_threads") across several chunks of pairs:

@@ -40,15 +40,28 @@ def make_stack(d: Path, Z: int, W: int, H: int):
     return paths
 
 
-def run(cfg, d: Path, name: str):
+def run(cfg, d: Path, name: str, skip: int = 4):
+    """Wall time of the whole CLI process, and the steady rate: the CLI prints "p q" as it
+    starts each pair, so pairs after the first `skip` starts over the time from that start to
+    the process end leave out process start, device init and the first decodes."""
     p = d / f"{name}.json"
     p.write_text(json.dumps(cfg))
     t0 = time.perf_counter()
-    r = subprocess.run([str(OPTFLOW), str(p)], capture_output=True, text=True, timeout=900)
-    dt = time.perf_counter() - t0
-    if r.returncode != 0:
-        raise RuntimeError(r.stderr[-2000:])
-    return dt
+    proc = subprocess.Popen([str(OPTFLOW), str(p)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                            text=True)
+    starts = []
+    for line in proc.stdout:
+        if line.strip() and not line.startswith("{"):
+            starts.append(time.perf_counter())
+    err = proc.stderr.read()
+    rc = proc.wait(timeout=900)
+    t1 = time.perf_counter()
+    if rc != 0:
+        raise RuntimeError(err[-2000:])
+    steady = None
+    if len(starts) > skip + 1:
+        steady = (len(starts) - skip) / (t1 - starts[skip])
+    return t1 - t0, steady
 
 
 def main():
@@ -81,11 +94,12 @@ def main():
             if threads:
                 cfg["decode_threads"] = threads
             (d / name).mkdir(exist_ok=True)
-            dt = run(cfg, d, f"{name}_{threads or 'pool'}")
+            dt, steady = run(cfg, d, f"{name}_{threads or 'pool'}")
             n = len(pairs)
             print(json.dumps({"job": name, "decode_threads": threads or "default (pool)",
                               "pairs": n, "wall_s": round(dt, 3),
-                              "pairs_per_s": round(n / dt, 2)}), flush=True)
+                              "pairs_per_s": round(n / dt, 2),
+                              "steady_pairs_per_s": steady and round(steady, 2)}), flush=True)
 
 
 if __name__ == "__main__":
