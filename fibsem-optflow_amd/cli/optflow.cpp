@@ -29,6 +29,7 @@
 //     "matches_file", "stats_json", "skip_existing".
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -153,6 +154,7 @@ struct DeviceCtx {
   // frame reuse: the (name, scale) currently resident in d0 / d1
   std::string key0, key1;
   ofio::Image8 h0, h1;
+  bool faulted = false;   // a HIP / engine call failed: the context is reset before reuse
 };
 
 std::mutex g_io_mutex;
@@ -163,13 +165,15 @@ bool ensure(DeviceCtx &dc, size_t img_bytes, size_t flow_bytes, bool &realloc, s
     (void)hipStreamSynchronize(dc.stream);  // buffers may still be in use by queued work
   if (img_bytes > dc.cap_img) {
     realloc = true;
-    if (dc.d0) (void)hipFree(dc.d0);
-    if (dc.d1) (void)hipFree(dc.d1);
-    if (dc.dw) (void)hipFree(dc.dw);
+    for (uint8_t **b : {&dc.d0, &dc.d1, &dc.dw}) {
+      if (*b) (void)hipFree(*b);
+      *b = nullptr;
+    }
+    dc.cap_img = 0;
     if (hipMalloc((void **)&dc.d0, img_bytes) != hipSuccess ||
         hipMalloc((void **)&dc.d1, img_bytes) != hipSuccess ||
         hipMalloc((void **)&dc.dw, img_bytes) != hipSuccess) {
-      err = "hipMalloc failed for frames";
+      err = "hipMalloc failed for frames", dc.faulted = true;
       return false;
     }
     dc.cap_img = img_bytes;
@@ -177,11 +181,14 @@ bool ensure(DeviceCtx &dc, size_t img_bytes, size_t flow_bytes, bool &realloc, s
     dc.key1.clear();
   }
   if (flow_bytes > dc.cap_flow) {
-    if (dc.du) (void)hipFree(dc.du);
-    if (dc.dv) (void)hipFree(dc.dv);
+    for (float **b : {&dc.du, &dc.dv}) {
+      if (*b) (void)hipFree(*b);
+      *b = nullptr;
+    }
+    dc.cap_flow = 0;
     if (hipMalloc((void **)&dc.du, flow_bytes) != hipSuccess ||
         hipMalloc((void **)&dc.dv, flow_bytes) != hipSuccess) {
-      err = "hipMalloc failed for flow";
+      err = "hipMalloc failed for flow", dc.faulted = true;
       return false;
     }
     dc.cap_flow = flow_bytes;
@@ -322,12 +329,12 @@ bool random_points_sampled(DeviceCtx &dc, size_t fp, int W, int H, const ofio::I
     const size_t off = (size_t)pts[i].second * fp + (size_t)pts[i].first * 4;
     if (hipMemcpyAsync(&vx[i], (const char *)dc.du + off, 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
         hipMemcpyAsync(&vy[i], (const char *)dc.dv + off, 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess) {
-      err = "flow read-back failed";
+      err = "flow read-back failed", dc.faulted = true;
       return false;
     }
   }
   if (hipStreamSynchronize(dc.stream) != hipSuccess) {
-    err = "flow read-back failed";
+    err = "flow read-back failed", dc.faulted = true;
     return false;
   }
   emit_points(pts, vx, vy, total > 0, im, r0, r1, inv_scale, features);
@@ -361,7 +368,7 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
   const int W = r0.width, H = r0.height;
   tvl1_params prm = generate_TV_args(im, args);
   if (tvl1_set_params(dc.ctx, &prm) != TVL1_OK) {
-    err = tvl1_last_error(dc.ctx);
+    err = tvl1_last_error(dc.ctx), dc.faulted = true;
     return false;
   }
   const size_t pitch = (size_t)f0.width;  // device frames are packed, pitch = width
@@ -374,7 +381,7 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
   const auto t0 = std::chrono::steady_clock::now();
   tvl1_status s = tvl1_calc(dc.ctx, a, pitch, b, pitch1, W, H, dc.du, dc.dv, fp, &st, dc.stream);
   if (s != TVL1_OK) {
-    err = tvl1_last_error(dc.ctx);
+    err = tvl1_last_error(dc.ctx), dc.faulted = true;
     return false;
   }
   const std::string otype = output_type_of(im, args);
@@ -388,13 +395,13 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
   else
     s = tvl1_postprocess(dc.ctx, dc.du, dc.dv, fp, b, pitch1, W, H, mode, dc.stream);
   if (s != TVL1_OK) {
-    err = tvl1_last_error(dc.ctx);
+    err = tvl1_last_error(dc.ctx), dc.faulted = true;
     return false;
   }
   const bool sampled = otype == "random_points" && !args.get("debug", false).asBool();
   if (sampled) {
     if (hipStreamSynchronize(dc.stream) != hipSuccess) {
-      err = "solve failed";
+      err = "solve failed", dc.faulted = true;
       return false;
     }
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -414,7 +421,7 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
   if (hipMemcpyAsync(fx.data(), dc.du, fx.size() * 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
       hipMemcpyAsync(fy.data(), dc.dv, fy.size() * 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
       hipStreamSynchronize(dc.stream) != hipSuccess) {
-    err = "flow download failed";
+    err = "flow download failed", dc.faulted = true;
     return false;
   }
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -494,7 +501,7 @@ bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1,
                                       (size_t)f0.width, f0.width, f0.height, &p, affine, &n_good,
                                       &outcome, dc.stream);
   if (s != TVL1_OK) {
-    err = std::string("find_alignment: ") + tvl1_last_error(dc.ctx);
+    err = std::string("find_alignment: ") + tvl1_last_error(dc.ctx), dc.faulted = true;
     return false;
   }
   if (args.get("debug", Value(false)).asBool())
@@ -506,7 +513,7 @@ bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1,
   s = tvl1_warp_affine_u8(dc.ctx, dc.d1, (size_t)w1, w1, h1, dc.dw,
                           (size_t)f0.width, f0.width, f0.height, affine, dc.stream);
   if (s != TVL1_OK) {
-    err = std::string("warpAffine: ") + tvl1_last_error(dc.ctx);
+    err = std::string("warpAffine: ") + tvl1_last_error(dc.ctx), dc.faulted = true;
     return false;
   }
   aligned.width = f0.width;
@@ -515,12 +522,65 @@ bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1,
   if (hipMemcpyAsync(aligned.data.data(), dc.dw, aligned.data.size(), hipMemcpyDeviceToHost, dc.stream) !=
           hipSuccess ||
       hipStreamSynchronize(dc.stream) != hipSuccess) {
-    err = "download of the aligned frame failed";
+    err = "download of the aligned frame failed", dc.faulted = true;
     return false;
   }
   std::swap(dc.d1, dc.dw);
   dc.key1.clear();  // the device copy is the aligned frame, not the slice
   return true;
+}
+
+// Device context of one worker: engine ctx, stream and buffers.
+bool open_device(DeviceCtx &dc, int device, std::string &err) {
+  dc.device = device;
+  tvl1_params p;
+  tvl1_params_default(&p);
+  if (tvl1_create(&dc.ctx, device, &p) != TVL1_OK) {
+    err = tvl1_last_error(nullptr);
+    dc.ctx = nullptr;
+    return false;
+  }
+  (void)hipSetDevice(device);
+  if (hipStreamCreateWithFlags(&dc.stream, hipStreamNonBlocking) != hipSuccess) {
+    err = "hipStreamCreate failed";
+    dc.stream = nullptr;
+    return false;
+  }
+  dc.faulted = false;
+  return true;
+}
+
+void close_device(DeviceCtx &dc) {
+  if (dc.stream) (void)hipStreamSynchronize(dc.stream);
+  if (dc.ctx) tvl1_destroy(dc.ctx);
+  if (dc.stream) (void)hipStreamDestroy(dc.stream);
+  for (void *ptr : {(void *)dc.d0, (void *)dc.d1, (void *)dc.dw, (void *)dc.du, (void *)dc.dv})
+    if (ptr) (void)hipFree(ptr);
+  dc.ctx = nullptr;
+  dc.stream = nullptr;
+  dc.d0 = dc.d1 = dc.dw = nullptr;
+  dc.du = dc.dv = nullptr;
+  dc.cap_img = dc.cap_flow = 0;
+  dc.key0.clear();
+  dc.key1.clear();
+}
+
+// Test hook: OPTFLOW_INJECT_FAULT="i,j,..." makes the first attempt of those pairs fail as
+// a device error would (before any device work), to exercise the recovery below.
+bool inject_fault(size_t pair) {
+  static const std::vector<size_t> list = [] {
+    std::vector<size_t> v;
+    if (const char *e = getenv("OPTFLOW_INJECT_FAULT"))
+      for (const char *q = e; *q;) {
+        char *end;
+        const unsigned long x = strtoul(q, &end, 10);
+        if (end == q) break;
+        v.push_back(x);
+        q = *end ? end + 1 : end;
+      }
+    return v;
+  }();
+  return std::find(list.begin(), list.end(), pair) != list.end();
 }
 
 // solve_rois (optflow.cpp:312-392)
@@ -550,11 +610,11 @@ bool solve_rois(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1_in
   if (realloc) f0_resident = f1_resident = false;
   // GpuMat::upload (optflow.cpp:315-316), skipped when the slice is already resident
   if (!f0_resident && hipMemcpyAsync(dc.d0, f0.data.data(), f0.data.size(), hipMemcpyHostToDevice, dc.stream) != hipSuccess) {
-    err = "upload failed";
+    err = "upload failed", dc.faulted = true;
     return false;
   }
   if (!f1_resident && hipMemcpyAsync(dc.d1, f1p->data.data(), f1p->data.size(), hipMemcpyHostToDevice, dc.stream) != hipSuccess) {
-    err = "upload failed";
+    err = "upload failed", dc.faulted = true;
     return false;
   }
   bool ok = true;
@@ -693,16 +753,14 @@ static int from_file(Value &args, bool plan_only) {
     DeviceCtx dc;
     dc.device = device;
     if (!plan_only) {
-      tvl1_params p;
-      tvl1_params_default(&p);
-      if (tvl1_create(&dc.ctx, device, &p) != TVL1_OK) {
+      std::string err;
+      if (!open_device(dc, device, err)) {
         std::lock_guard<std::mutex> lk(g_io_mutex);
-        fprintf(stderr, "Error: cannot use GPU %d: %s\n", device, tvl1_last_error(nullptr));
+        fprintf(stderr, "Error: cannot use GPU %d: %s\n", device, err.c_str());
+        close_device(dc);
         hard_error = 1;
         return;
       }
-      (void)hipSetDevice(device);
-      (void)hipStreamCreateWithFlags(&dc.stream, hipStreamNonBlocking);
     }
     // this worker's chunks of pairs: the current one and the next, both queued for decode
     std::map<std::string, LoadFuture> pending;   // slice key -> its decode
@@ -867,10 +925,42 @@ static int from_file(Value &args, bool plan_only) {
             continue;
           }
         }
-        results[i].ok = solve_rois(dc, dc.h0, dc.h1, r0, r1, rois, im, args, results[i], err);
+        if (inject_fault(i)) {
+          results[i].ok = false;
+          dc.faulted = true;
+          err = "injected device fault";
+        } else {
+          results[i].ok = solve_rois(dc, dc.h0, dc.h1, r0, r1, rois, im, args, results[i], err);
+        }
         if (!results[i].ok) {  // device contents are unknown after a failure
           dc.key0.clear();
           dc.key1.clear();
+        }
+        // failure recovery: a pair that failed on a device error is solved once
+        // more on a fresh context (engine ctx, stream and buffers rebuilt); input errors
+        // (an ROI outside the image) are reported as the reference reports them
+        if (!results[i].ok && dc.faulted) {
+          {
+            std::lock_guard<std::mutex> lk(g_io_mutex);
+            fprintf(stderr, "Warning: pair %zu (%s %s): %s; retrying on a fresh device context\n",
+                    i, p.c_str(), q.c_str(), err.c_str());
+          }
+          close_device(dc);
+          results[i] = PairResult();
+          std::string e2;
+          if (!open_device(dc, device, e2)) {
+            err = "device context could not be rebuilt: " + e2;
+          } else {
+            err.clear();
+            results[i].ok = solve_rois(dc, dc.h0, dc.h1, false, false, rois, im, args, results[i], err);
+            if (!results[i].ok) {
+              dc.key0.clear();
+              dc.key1.clear();
+            } else {
+              dc.key0 = k0;
+              dc.key1 = k1;
+            }
+          }
         }
         results[i].done = true;
         if (!results[i].ok) {
@@ -879,10 +969,7 @@ static int from_file(Value &args, bool plan_only) {
         }
       }
     }
-    if (dc.ctx) tvl1_destroy(dc.ctx);
-    if (dc.stream) (void)hipStreamDestroy(dc.stream);
-    for (void *ptr : {(void *)dc.d0, (void *)dc.d1, (void *)dc.dw, (void *)dc.du, (void *)dc.dv})
-      if (ptr) (void)hipFree(ptr);
+    close_device(dc);
   };
 
   // build-only "inflight": pairs solved concurrently per GPU (one worker thread, ctx and

@@ -200,3 +200,39 @@ def test_dualtvl1_profile_via_json(tmp_path, pair):
     out = sorted(tmp_path.glob("pq*_x.tiff"))
     assert out, list(tmp_path.iterdir())
     assert np.array_equal(tif(out[0]).view(np.uint32), u.view(np.uint32))
+
+
+@pytest.mark.parametrize("rois", [{"top": 40, "bottom": 50}, None])
+def test_device_fault_recovery(tmp_path, built, rois):
+    """SURVEY 5 failure handling: a pair whose solve fails on a device error is solved again
+    on a rebuilt device context (engine ctx, stream, buffers), and its outputs equal a
+    fault-free run's.  OPTFLOW_INJECT_FAULT makes the first attempt of the listed pairs fail
+    before any device work; a strip job (ROIs top/bottom, 8 workers) and a full-frame job."""
+    import os
+    zs = [synth.gen_pair(150, 110, seed=50 + k)[0] for k in range(4)]
+    for k, z in enumerate(zs):
+        Image.fromarray(z).save(tmp_path / f"s{k}.png")
+    images = [{"p": str(tmp_path / f"s{k}.png"), "q": str(tmp_path / f"s{k + 1}.png"),
+               "output_name": f"z{k}"} for k in range(3)]
+    outs = {}
+    for tag, fault in (("clean", None), ("fault", "0,2")):
+        d = tmp_path / tag
+        d.mkdir()
+        cfg = {"output_dir": str(d), "scale": 1, "output_type": "flow", "nscales": 3,
+               "warps": 3, "images": images}
+        if rois:
+            cfg["rois"] = rois
+        p = tmp_path / f"{tag}.json"
+        p.write_text(json.dumps(cfg))
+        env = dict(os.environ)
+        if fault:
+            env["OPTFLOW_INJECT_FAULT"] = fault
+        r = subprocess.run([str(OPTFLOW), str(p)], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0, r.stderr
+        if fault:
+            assert r.stderr.count("retrying on a fresh device context") == 2, r.stderr
+        outs[tag] = {f.name: tif(f) for f in sorted(d.glob("*.tif*"))}
+    assert outs["clean"] and outs["clean"].keys() == outs["fault"].keys()
+    for name, a in outs["clean"].items():
+        assert np.array_equal(a.view(np.uint32), outs["fault"][name].view(np.uint32)), name
