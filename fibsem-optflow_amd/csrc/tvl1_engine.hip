@@ -400,15 +400,6 @@ static double survey_bytes(const Geometry &g, int warps, const int64_t *iters) {
 // so those iterations run as ONE temporally blocked pass (<= kTbMax iterations);
 // the residual of the check is then read exactly where OpenCV reads it.
 //
-// Speculation (default on, TVL1_SPECULATE=0 disables): right after a check pass,
-// before the host blocks on its residual, the work that follows if the warp has
-// converged is enqueued — the next warp's warpBackward (into the other constants
-// buffer), or at the end of a level the flow upsample + the next level's gradient
-// + its first warpBackward.  Converged (the common case): that work is simply used.
-// Not converged: it wrote only buffers the continuing warp does not read (the
-// spare constants buffer, the next ping-pong u set, the gradient of a level whose
-// gathers are done) and is redone at the next check.  Results are bit-identical
-// either way; the GPU just never idles while the host reads a residual.
 // resize(): an exact 2x downscale of INTER_LINEAR takes the INTER_AREA fast path
 static int area_fast_of(double sx, double sy) {
   const int ix = (int)std::lrint(sx), iy = (int)std::lrint(sy);
@@ -421,16 +412,34 @@ static int area_fast_of(double sx, double sy) {
 // medianFiltering, of up to innerIterations primal-dual iterations, every one of which
 // evaluates the residual (one k_iterate launch + k_reduce + one host read each).  This is
 // a compatibility mode, not the benchmark path: it keeps OpenCV's per-iteration check.
-static tvl1_status solve_dualtvl1(tvl1_ctx *c, const uint8_t *I0, size_t pitch0,
-                                  const uint8_t *I1, size_t pitch1, int W, int H, float *u,
+// The two input frames of a solve: u8 (tvl1_calc) or f32 (tvl1_calc_f32), device pointers,
+// row pitches in bytes.
+struct Frames {
+  const void *I0, *I1;
+  size_t pitch0, pitch1;
+  bool f32;
+};
+
+// [A.1] I0f = convertTo(CV_32F, u8 ? 1 : 255) into the level-0 planes
+static void convert_frames(tvl1_ctx *c, const Frames &in, int W, int H, hipStream_t st) {
+  if (in.f32)
+    hipLaunchKernelGGL(k_convert_f32, grid2(W, H, 2), kBlk2, 0, st, (const float *)in.I0,
+                       in.pitch0, (const float *)in.I1, in.pitch1, c->I0s[0], c->I1s[0], W, H,
+                       c->geo.ps[0]);
+  else
+    hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 2), kBlk2, 0, st, (const uint8_t *)in.I0,
+                       in.pitch0, (const uint8_t *)in.I1, in.pitch1, c->I0s[0], c->I1s[0], W, H,
+                       c->geo.ps[0]);
+}
+
+static tvl1_status solve_dualtvl1(tvl1_ctx *c, const Frames &in, int W, int H, float *u,
                                   float *v, size_t fpitch, tvl1_stats *stats, hipStream_t st) {
   const tvl1_params &prm = c->prm;
   const Geometry &g = c->geo;
   const int L = g.L;
   const bool gam = g.gamma;
   const bool median = prm.median_filtering > 1;
-  hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 2), kBlk2, 0, st, I0, pitch0, I1, pitch1,
-                     c->I0s[0], c->I1s[0], W, H, g.ps[0]);
+  convert_frames(c, in, W, H, st);
   const double dscale = 1. / prm.scale_step;
   const int afast = area_fast_of(dscale, dscale);
   for (int s = 1; s < L; ++s)
@@ -553,12 +562,10 @@ static tvl1_status solve_dualtvl1(tvl1_ctx *c, const uint8_t *I0, size_t pitch0,
   return TVL1_OK;
 }
 
-static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8_t *I1,
-                         size_t pitch1, int W, int H, float *u, float *v, size_t fpitch,
-                         tvl1_stats *stats, hipStream_t st) {
+static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, float *v,
+                         size_t fpitch, tvl1_stats *stats, hipStream_t st) {
   const tvl1_params &prm = c->prm;
-  if (prm.profile == 1)
-    return solve_dualtvl1(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch, stats, st);
+  if (prm.profile == 1) return solve_dualtvl1(c, in, W, H, u, v, fpitch, stats, st);
   const Geometry &g = c->geo;
   const int L = g.L;
   const bool gam = g.gamma;
@@ -570,8 +577,7 @@ static tvl1_status solve(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const ui
 
   // [A.1] convertTo + [A.2] pyramid, kernel step = float(1/scaleStep)
   size_t tk = prof_begin(c, st);
-  hipLaunchKernelGGL(k_convert_u8, grid2(W, H, 2), kBlk2, 0, st, I0, pitch0, I1, pitch1,
-                     c->I0s[0], c->I1s[0], W, H, g.ps[0]);
+  convert_frames(c, in, W, H, st);
   const float fdown = (float)(1.0 / prm.scale_step);
   const bool contract_pyr = contracts(math_of(prm));
   for (int s = 1; s < L; ++s) {
@@ -1710,7 +1716,23 @@ tvl1_status tvl1_calc(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8
   HIP_TRY(c, hipSetDevice(c->device));
   s = ensure_geometry(c, W, H, (hipStream_t)stream);
   if (s != TVL1_OK) return s;
-  return solve(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch, stats, (hipStream_t)stream);
+  return solve(c, Frames{I0, I1, pitch0, pitch1, false}, W, H, u, v, fpitch, stats,
+               (hipStream_t)stream);
+}
+
+tvl1_status tvl1_calc_f32(tvl1_ctx *c, const float *I0, size_t pitch0, const float *I1,
+                          size_t pitch1, int32_t W, int32_t H, float *u, float *v, size_t fpitch,
+                          tvl1_stats *stats, void *stream) {
+  tvl1_status s = check_call(c, I0, pitch0, I1, pitch1, W, H, u, v, fpitch);
+  if (s != TVL1_OK) return s;
+  if (pitch0 < sizeof(float) * (size_t)W || pitch1 < sizeof(float) * (size_t)W ||
+      pitch0 % sizeof(float) || pitch1 % sizeof(float))
+    return set_err(c, TVL1_EINVAL, "f32 input pitch must be >= 4*width and a multiple of 4");
+  HIP_TRY(c, hipSetDevice(c->device));
+  s = ensure_geometry(c, W, H, (hipStream_t)stream);
+  if (s != TVL1_OK) return s;
+  return solve(c, Frames{I0, I1, pitch0, pitch1, true}, W, H, u, v, fpitch, stats,
+               (hipStream_t)stream);
 }
 
 
@@ -1769,7 +1791,7 @@ tvl1_status tvl1_calc_batch(tvl1_ctx *c, int32_t n, const uint8_t *I0, size_t pi
     s = batched ? solve_batch_chunk(c, m, i0, pitch0, pair_stride0, i1, pitch1, pair_stride1, W,
                                     H, ub, vb, fpitch, flow_pair_stride, stats ? stats + b0 : nullptr,
                                     (hipStream_t)stream)
-                : solve(c, i0, pitch0, i1, pitch1, W, H, ub, vb, fpitch, stats ? stats + b0 : nullptr,
+                : solve(c, Frames{i0, i1, pitch0, pitch1, false}, W, H, ub, vb, fpitch, stats ? stats + b0 : nullptr,
                         (hipStream_t)stream);
     if (s == TVL1_ENOMEM && batched && m > 1) {
       chunk = m / 2;
@@ -1947,7 +1969,8 @@ tvl1_status tvl1_calc_host(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const 
   // GpuMat::upload (optflow.cpp:315-316)
   HIP_TRY(c, hipMemcpy2DAsync(c->in0, P0, I0, pitch0, W, H, hipMemcpyHostToDevice, st));
   HIP_TRY(c, hipMemcpy2DAsync(c->in1, P0, I1, pitch1, W, H, hipMemcpyHostToDevice, st));
-  s = solve(c, c->in0, P0, c->in1, P0, W, H, c->outu, c->outv, P0 * sizeof(float), stats, st);
+  s = solve(c, Frames{c->in0, c->in1, P0, P0, false}, W, H, c->outu, c->outv, P0 * sizeof(float),
+            stats, st);
   if (s != TVL1_OK) return s;
   // download (optflow.cpp:475-476)
   HIP_TRY(c, hipMemcpy2DAsync(u, fpitch, c->outu, P0 * sizeof(float), W * sizeof(float), H,

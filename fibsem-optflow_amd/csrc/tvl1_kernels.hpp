@@ -155,6 +155,20 @@ __global__ void k_convert_u8(const uint8_t *__restrict__ s0, size_t sp0,
     d1[(size_t)y * P + x] = (float)s1[(size_t)y * sp1 + x];
 }
 
+// [A.1] for CV_32FC1 inputs: convertTo(CV_32F, 255.0) = src * 255 + 0 (nvcc contracts it
+// to fma(255, src, 0): the same value, -0 becomes +0 either way).  Pitches in bytes.
+__global__ void k_convert_f32(const float *__restrict__ s0, size_t sp0,
+                              const float *__restrict__ s1, size_t sp1,
+                              float *__restrict__ d0, float *__restrict__ d1, int W, int H,
+                              int P) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const float *s = blockIdx.z == 0 ? (const float *)((const char *)s0 + (size_t)y * sp0)
+                                   : (const float *)((const char *)s1 + (size_t)y * sp1);
+  (blockIdx.z == 0 ? d0 : d1)[(size_t)y * P + x] = s[x] * 255.0f + 0.0f;
+}
+
 // ---------------------------------------------------------------- K2 / K9 resize
 // cuda::resize INTER_LINEAR: corner-aligned, src = dst * f, +1 taps clamped.
 // C (contracting modes): the tap weights' differences take the product src_x = dst_x * fx

@@ -18,7 +18,7 @@ REPO_ROOT = PKG_ROOT.parent
 ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
 
 TVL1_MAX_LEVELS = 32
-ABI_VERSION = 4          # TVL1_ABI_VERSION of include/tvl1.h
+ABI_VERSION = 5          # TVL1_ABI_VERSION of include/tvl1.h
 STATUS = {0: "TVL1_OK", 1: "TVL1_EINVAL", 2: "TVL1_ESIZE", 3: "TVL1_EHIP",
           4: "TVL1_ENOMEM", 5: "TVL1_ENODEV"}
 
@@ -163,6 +163,8 @@ def load_engine() -> C.CDLL:
                               C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_size_t,
                               C.POINTER(TVL1Stats), C.c_void_p]
     lib.tvl1_calc.restype = C.c_int
+    lib.tvl1_calc_f32.argtypes = lib.tvl1_calc.argtypes
+    lib.tvl1_calc_f32.restype = C.c_int
     lib.tvl1_calc_batch.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_size_t, C.c_size_t,
                                     C.c_void_p, C.c_size_t, C.c_size_t, C.c_int32, C.c_int32,
                                     C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
@@ -265,7 +267,9 @@ class Engine:
 
     def calc_device(self, dI0: int, pitch0: int, dI1: int, pitch1: int, w: int, h: int,
                     du: int, dv: int, flow_pitch: int, stream: int = 0, stats: bool = True,
-                    warp_iters: bool = False):
+                    warp_iters: bool = False, f32: bool = False):
+        """tvl1_calc on device buffers (u8 frames, pitches in bytes), or tvl1_calc_f32 with
+        f32=True (float frames in [0, 1], pitches in bytes)."""
         st = TVL1Stats() if stats or warp_iters else None
         wi = None
         if warp_iters:
@@ -273,11 +277,12 @@ class Engine:
             wi = np.full(cap, -1, np.int32)
             st.warp_iterations = wi.ctypes.data_as(C.POINTER(C.c_int32))
             st.warp_iterations_capacity = cap
-        rc = self.lib.tvl1_calc(self.ctx, C.c_void_p(dI0), pitch0, C.c_void_p(dI1), pitch1,
-                                w, h, C.c_void_p(du), C.c_void_p(dv), flow_pitch,
-                                C.byref(st) if st is not None else None,
-                                C.c_void_p(stream) if stream else None)
-        self._check(rc, "tvl1_calc")
+        fn = self.lib.tvl1_calc_f32 if f32 else self.lib.tvl1_calc
+        rc = fn(self.ctx, C.c_void_p(dI0), pitch0, C.c_void_p(dI1), pitch1,
+                w, h, C.c_void_p(du), C.c_void_p(dv), flow_pitch,
+                C.byref(st) if st is not None else None,
+                C.c_void_p(stream) if stream else None)
+        self._check(rc, "tvl1_calc_f32" if f32 else "tvl1_calc")
         if st is None:
             return None
         sd = stats_dict(st)

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TVL1_ABI_VERSION 4
+#define TVL1_ABI_VERSION 5
 #define TVL1_MAX_LEVELS 32
 
 typedef enum tvl1_status {
@@ -140,6 +140,13 @@ tvl1_status tvl1_calc(tvl1_ctx *ctx,
                       int32_t width, int32_t height,
                       float *u, float *v, size_t flow_pitch,
                       tvl1_stats *stats, void *stream);
+
+/* CV_32FC1 frames: calc converts f32 inputs with convertTo(CV_32F, 255), so
+ * pixel values are expected in [0, 1]; everything else as tvl1_calc.  Device pointers,
+ * pitches in bytes (>= 4 * width, multiples of 4). */
+tvl1_status tvl1_calc_f32(tvl1_ctx *ctx, const float *I0, size_t pitch0, const float *I1,
+                          size_t pitch1, int32_t width, int32_t height, float *u, float *v,
+                          size_t flow_pitch, tvl1_stats *stats, void *stream);
 
 /* Batched solve (build addition for the production workload, SURVEY 3.2: two 3072x100
  * ROI strips per slice pair, each a solve of ~400 tiny launches): n pairs of one size,

@@ -25,6 +25,11 @@ def load_oracle() -> C.CDLL:
                                   C.POINTER(C.c_uint8), C.c_size_t, C.c_int, C.c_int,
                                   C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_size_t,
                                   C.POINTER(TVL1Stats)]
+    lib.orc_tvl1_calc_f32.restype = C.c_int
+    lib.orc_tvl1_calc_f32.argtypes = [C.POINTER(TVL1Params), C.POINTER(C.c_float), C.c_size_t,
+                                      C.POINTER(C.c_float), C.c_size_t, C.c_int, C.c_int,
+                                      C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_size_t,
+                                      C.POINTER(TVL1Stats)]
     lib.orc_num_threads.restype = C.c_int
     lib.orc_set_num_threads.argtypes = [C.c_int]
     return lib
@@ -32,13 +37,16 @@ def load_oracle() -> C.CDLL:
 
 def oracle_calc(I0: np.ndarray, I1: np.ndarray, params: TVL1Params | None = None,
                 warp_iters: bool = True, threads: int | None = None):
-    """Run the CPU restatement on host u8 images; returns (u, v, stats, warp_iters)."""
+    """Run the CPU restatement on host u8 images (or float32 images: tvl1_calc_f32's
+    contract, values scaled by 255); returns (u, v, stats, warp_iters)."""
     lib = load_oracle()
     if threads:
         lib.orc_set_num_threads(int(threads))
     params = params or make_params()
-    I0 = np.ascontiguousarray(I0, dtype=np.uint8)
-    I1 = np.ascontiguousarray(I1, dtype=np.uint8)
+    f32 = np.asarray(I0).dtype == np.float32
+    dt = np.float32 if f32 else np.uint8
+    I0 = np.ascontiguousarray(I0, dtype=dt)
+    I1 = np.ascontiguousarray(I1, dtype=dt)
     h, w = I0.shape
     u = np.zeros((h, w), np.float32)
     v = np.zeros((h, w), np.float32)
@@ -49,8 +57,12 @@ def oracle_calc(I0: np.ndarray, I1: np.ndarray, params: TVL1Params | None = None
         wi = np.full(cap, -1, np.int32)
         st.warp_iterations = wi.ctypes.data_as(C.POINTER(C.c_int32))
         st.warp_iterations_capacity = cap
-    rc = lib.orc_tvl1_calc(C.byref(params), _u8_ptr(I0), w, _u8_ptr(I1), w, w, h,
-                           _f32_ptr(u), _f32_ptr(v), 4 * w, C.byref(st))
+    if f32:
+        rc = lib.orc_tvl1_calc_f32(C.byref(params), _f32_ptr(I0), 4 * w, _f32_ptr(I1), 4 * w, w,
+                                   h, _f32_ptr(u), _f32_ptr(v), 4 * w, C.byref(st))
+    else:
+        rc = lib.orc_tvl1_calc(C.byref(params), _u8_ptr(I0), w, _u8_ptr(I1), w, w, h,
+                               _f32_ptr(u), _f32_ptr(v), 4 * w, C.byref(st))
     if rc != 0:
         raise TVL1Error(f"oracle: {STATUS.get(rc, rc)}")
     sd = stats_dict(st)

@@ -70,6 +70,23 @@ void orc_convert_u8(const uint8_t *src, size_t pitch, int w, int h, float *dst) 
     for (int x = 0; x < w; ++x) dst[IDX(x, y, w)] = (float)src[(size_t)y * pitch + x];
 }
 
+/* [A.1] for CV_32FC1 inputs: convertTo(CV_32F, 255.0) = src * 255 + 0 (pitch in bytes). */
+void orc_convert_f32(const float *src, size_t pitch, int w, int h, float *dst) {
+#pragma omp parallel for schedule(static)
+  for (int y = 0; y < h; ++y) {
+    const float *row = (const float *)((const char *)src + (size_t)y * pitch);
+    for (int x = 0; x < w; ++x) dst[IDX(x, y, w)] = row[x] * 255.0f + 0.0f;
+  }
+}
+
+/* the level-0 frames of a solve from u8 (pitch in px) or f32 (pitch in bytes) inputs */
+void orc_convert_in(const void *src, size_t pitch, int f32, int w, int h, float *dst) {
+  if (f32)
+    orc_convert_f32((const float *)src, pitch, w, h, dst);
+  else
+    orc_convert_u8((const uint8_t *)src, pitch, w, h, dst);
+}
+
 /* [A.2] cuda::resize INTER_LINEAR (resize.cu resize_linear / LinearFilter):
  * corner-aligned source coordinate src = dst * f, taps floor/+1, the +1 tap
  * clamped to the last column/row (BrdReplicate / texture clamp). */
@@ -434,18 +451,20 @@ typedef struct {
   float *I0, *I1, *u1, *u2, *u3;
 } level_bufs;
 
-/* [A.1]-[A.4] calc / calcImpl / procOneScale. */
-int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
-                  const uint8_t *I1, size_t pitch1, int w, int h, float *u, float *v,
-                  size_t flow_pitch, tvl1_stats *stats) {
+/* [A.1]-[A.4] calc / calcImpl / procOneScale; u8 inputs (pitch in px) or f32 (bytes). */
+static int calc_in(const tvl1_params *prm, const void *I0, size_t pitch0, const void *I1,
+                   size_t pitch1, int f32, int w, int h, float *u, float *v,
+                   size_t flow_pitch, tvl1_stats *stats) {
   if (!prm || !I0 || !I1 || !u || !v) return TVL1_EINVAL;
+  if (w <= 0 || h <= 0) return TVL1_ESIZE;
+  const size_t in_bytes = f32 ? sizeof(float) * (size_t)w : (size_t)w;
+  if (pitch0 < in_bytes || pitch1 < in_bytes || flow_pitch < sizeof(float) * (size_t)w)
+    return TVL1_EINVAL;
   if (prm->profile == 1)
-    return orc_tvl1_calc_dualtvl1(prm, I0, pitch0, I1, pitch1, w, h, u, v, flow_pitch, stats);
+    return orc_tvl1_calc_dualtvl1_in(prm, I0, pitch0, I1, pitch1, f32, w, h, u, v, flow_pitch,
+                                     stats);
   if (prm->profile != 0) return TVL1_EINVAL;
   if (prm->nscales <= 0 || prm->warps < 0 || prm->iterations < 0) return TVL1_EINVAL;
-  if (w <= 0 || h <= 0) return TVL1_ESIZE;
-  if (pitch0 < (size_t)w || pitch1 < (size_t)w || flow_pitch < sizeof(float) * (size_t)w)
-    return TVL1_EINVAL;
   if (prm->median_filtering > 1 && prm->median_filtering != 3 && prm->median_filtering != 5)
     return TVL1_EINVAL;
 
@@ -488,8 +507,8 @@ int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
   int64_t checks = 0;
 
   /* [A.1] convertTo + [A.2] pyramid (fx passed to the kernel = float(1/scaleStep)) */
-  orc_convert_u8(I0, pitch0, w, h, lv[0].I0);
-  orc_convert_u8(I1, pitch1, w, h, lv[0].I1);
+  orc_convert_in(I0, pitch0, f32, w, h, lv[0].I0);
+  orc_convert_in(I1, pitch1, f32, w, h, lv[0].I1);
   const float fdown = (float)(1.0 / prm->scale_step);
   for (int s = 1; s < L; ++s) {
     resize_linear(lv[s - 1].I0, ws[s - 1], hs[s - 1], lv[s].I0, ws[s], hs[s], fdown, fdown, fma_mode);
@@ -594,4 +613,17 @@ int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
   free(I1x); free(I1y); free(I1wx); free(I1wy); free(grad); free(rho_c);
   free(p11); free(p12); free(p21); free(p22); free(p31); free(p32); free(tmp);
   return TVL1_OK;
+}
+
+int orc_tvl1_calc(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
+                  const uint8_t *I1, size_t pitch1, int w, int h, float *u, float *v,
+                  size_t flow_pitch, tvl1_stats *stats) {
+  return calc_in(prm, I0, pitch0, I1, pitch1, 0, w, h, u, v, flow_pitch, stats);
+}
+
+/* tvl1_calc_f32 on host buffers (pitches in bytes) */
+int orc_tvl1_calc_f32(const tvl1_params *prm, const float *I0, size_t pitch0, const float *I1,
+                      size_t pitch1, int w, int h, float *u, float *v, size_t flow_pitch,
+                      tvl1_stats *stats) {
+  return calc_in(prm, I0, pitch0, I1, pitch1, 1, w, h, u, v, flow_pitch, stats);
 }

@@ -75,11 +75,21 @@ void orc_remap_cubic(const float *I0, const float *I1, const float *I1x, const f
 int orc_tvl1_calc_dualtvl1(const tvl1_params *params, const uint8_t *I0, size_t pitch0,
                            const uint8_t *I1, size_t pitch1, int w, int h, float *u, float *v,
                            size_t flow_pitch, tvl1_stats *stats);
+/* the same on u8 (pitch in px, f32 = 0) or f32 inputs (pitch in bytes, f32 = 1) */
+int orc_tvl1_calc_dualtvl1_in(const tvl1_params *params, const void *I0, size_t pitch0,
+                              const void *I1, size_t pitch1, int f32, int w, int h, float *u,
+                              float *v, size_t flow_pitch, tvl1_stats *stats);
+/* [A.1] level-0 frames: float(u8), or f32 * 255 + 0 (convertTo(CV_32F, 255)) */
+void orc_convert_in(const void *src, size_t pitch, int f32, int w, int h, float *dst);
 
 /* ---- whole solve: same contract as tvl1_calc_host (include/tvl1.h) ---- */
 int orc_tvl1_calc(const tvl1_params *params, const uint8_t *I0, size_t pitch0,
                   const uint8_t *I1, size_t pitch1, int w, int h, float *u, float *v,
                   size_t flow_pitch, tvl1_stats *stats);
+/* ... and tvl1_calc_f32's contract (f32 frames, pitches in bytes) */
+int orc_tvl1_calc_f32(const tvl1_params *params, const float *I0, size_t pitch0,
+                      const float *I1, size_t pitch1, int w, int h, float *u, float *v,
+                      size_t flow_pitch, tvl1_stats *stats);
 
 /* solve_wrapper post-ops (optflow.cpp:445-473) on host buffers */
 void orc_postprocess(float *u, float *v, size_t flow_pitch, const uint8_t *I1, size_t pitch1,

@@ -258,6 +258,12 @@ static int area_fast_of(double scale_x, double scale_y) {
 int orc_tvl1_calc_dualtvl1(const tvl1_params *prm, const uint8_t *I0, size_t pitch0,
                            const uint8_t *I1, size_t pitch1, int w, int h, float *u, float *v,
                            size_t flow_pitch, tvl1_stats *stats) {
+  return orc_tvl1_calc_dualtvl1_in(prm, I0, pitch0, I1, pitch1, 0, w, h, u, v, flow_pitch, stats);
+}
+
+int orc_tvl1_calc_dualtvl1_in(const tvl1_params *prm, const void *I0, size_t pitch0,
+                              const void *I1, size_t pitch1, int f32, int w, int h, float *u,
+                              float *v, size_t flow_pitch, tvl1_stats *stats) {
   if (prm->nscales <= 0 || prm->warps < 0 || prm->inner_iterations < 0 ||
       prm->outer_iterations < 0)
     return TVL1_EINVAL;
@@ -294,8 +300,8 @@ int orc_tvl1_calc_dualtvl1(const tvl1_params *prm, const uint8_t *I0, size_t pit
   memset(level_iters, 0, sizeof(level_iters));
 
   /* calc(): convertTo(CV_32F), then resize(.., Size(), scaleStep, scaleStep) per level */
-  orc_convert_u8(I0, pitch0, w, h, I0s[0]);
-  orc_convert_u8(I1, pitch1, w, h, I1s[0]);
+  orc_convert_in(I0, pitch0, f32, w, h, I0s[0]);
+  orc_convert_in(I1, pitch1, f32, w, h, I1s[0]);
   const double dscale = 1. / prm->scale_step;
   const int afast = area_fast_of(dscale, dscale);
   for (int s = 1; s < L; ++s) {

@@ -10,6 +10,8 @@ import pytest
 from optflow_amd import capi, synth
 from oracle import checker
 
+torch = pytest.importorskip("torch")   # device buffers of the f32 test; imported before HIP init
+
 pytestmark = pytest.mark.gpu
 
 EPE_TOL = 1e-3  # px, BASELINE.json north_star
@@ -242,3 +244,39 @@ def test_dualtvl1_profile_identity(engine):
     u, v, st, wi = engine.calc_host(I0, I0)
     assert np.all(u == 0) and np.all(v == 0)
     assert np.all(wi == 1)
+
+
+@pytest.mark.parametrize("profile", [0, 1])
+def test_f32_inputs_match_oracle(built, profile):
+    """tvl1_calc_f32 (CV_32FC1 frames, scaled by 255 on entry) vs the oracle's f32 path,
+    bitwise, on off-grid float frames; and u8 frames given as k / 255 reproduce tvl1_calc."""
+    I0, I1 = synth.gen_pair(203, 131, seed=77)
+    kw = dict(nscales=4, warps=5) if profile == 0 else dict(profile=1, nscales=3, warps=2,
+                                                               inner_iterations=4,
+                                                               outer_iterations=2)
+    p = capi.make_params(**kw)
+    eng = capi.Engine(p)
+    rng = np.random.default_rng(5)
+    J0 = (I0 / 255.0 + rng.normal(0, 2e-3, I0.shape)).astype(np.float32)
+    J1 = (I1 / 255.0 + rng.normal(0, 2e-3, I1.shape)).astype(np.float32)
+    H, W = I0.shape
+    dev = torch.device("cuda", 0)
+    for F0, F1 in ((J0, J1), (I0.astype(np.float32) / np.float32(255),
+                               I1.astype(np.float32) / np.float32(255))):
+        d0 = torch.from_numpy(F0).to(dev)
+        d1 = torch.from_numpy(F1).to(dev)
+        du = torch.zeros((H, W), dtype=torch.float32, device=dev)
+        dv = torch.zeros_like(du)
+        st = eng.calc_device(d0.data_ptr(), 4 * W, d1.data_ptr(), 4 * W, W, H, du.data_ptr(),
+                             dv.data_ptr(), 4 * W, warp_iters=True, f32=True)
+        torch.cuda.synchronize()
+        u, v = du.cpu().numpy(), dv.cpu().numpy()
+        ur, vr, sr, wr = checker.oracle_calc(F0, F1, p)
+        assert np.array_equal(u.view(np.uint32), ur.view(np.uint32))
+        assert np.array_equal(v.view(np.uint32), vr.view(np.uint32))
+        np.testing.assert_array_equal(st["warp_iters"], wr)
+    # the k / 255 frames (last loop pass) against the u8 entry point
+    uu, vu, _, _ = eng.calc_host(I0, I1)
+    assert np.array_equal(u.view(np.uint32), uu.view(np.uint32))
+    assert np.array_equal(v.view(np.uint32), vu.view(np.uint32))
+    eng.close()

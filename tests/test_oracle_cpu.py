@@ -150,3 +150,26 @@ def test_oracle_under_asan_ubsan():
                        timeout=300)
     assert r.returncode == 0 and "0 failures" in r.stdout, r.stdout + r.stderr
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr
+
+
+@pytest.mark.parametrize("profile", [0, 1])
+def test_f32_inputs_scale_by_255(built, profile):
+    """tvl1_calc_f32's contract (convertTo(CV_32F, 255) for CV_32FC1 frames):
+    u8 frames given as k / 255 in float32 reproduce the u8 solve bit for bit (255 * (k / 255)
+    rounds back to k for every k), and off-grid float frames solve to finite flows."""
+    I0, I1 = synth.gen_pair(61, 47, seed=31)
+    kw = dict(nscales=3, warps=2) if profile == 0 else dict(profile=1, nscales=2, warps=2,
+                                                               inner_iterations=3,
+                                                               outer_iterations=2)
+    p = capi.make_params(**kw)
+    u8 = checker.oracle_calc(I0, I1, p)
+    f = checker.oracle_calc(I0.astype(np.float32) / np.float32(255),
+                            I1.astype(np.float32) / np.float32(255), p)
+    for a, b in zip(u8[:2], f[:2]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    np.testing.assert_array_equal(u8[3], f[3])
+    rng = np.random.default_rng(3)
+    J0 = (I0 / 255.0 + rng.normal(0, 1e-3, I0.shape)).astype(np.float32)
+    J1 = (I1 / 255.0 + rng.normal(0, 1e-3, I1.shape)).astype(np.float32)
+    u, v, _, _ = checker.oracle_calc(J0, J1, p)
+    assert np.isfinite(u).all() and np.isfinite(v).all()
