@@ -975,11 +975,12 @@ static int from_file(Value &args, bool plan_only) {
   // build-only "inflight": pairs solved concurrently per GPU (one worker thread, ctx and
   // stream each) so one pair's residual read-backs overlap another pair's kernels.  Strip
   // jobs (every ROI "top" / "bottom", the production shape: two 100-row strips per pair)
-  // are launch- and sync-bound per solve, so they default to 8 in flight.
+  // are launch- and sync-bound per solve, so they default to 8 in flight, full frames to 3
+  // (DESIGN.md 5.1, 9).
   bool strip_job = args.isMember("rois") && args["rois"].isObject() && args["rois"].size() > 0;
   if (strip_job)
     for (auto &k : args["rois"].memberNames()) strip_job = strip_job && (k == "top" || k == "bottom");
-  const int inflight = std::max(1, args.get("inflight", strip_job ? 8 : 2).asInt());
+  const int inflight = std::max(1, args.get("inflight", strip_job ? 8 : 3).asInt());
   if (plan_only || (devices.size() == 1 && inflight == 1)) {
     worker(devices[0]);
   } else {
