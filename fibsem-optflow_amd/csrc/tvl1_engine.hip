@@ -68,6 +68,9 @@ struct tvl1_ctx {
   double *pinned = nullptr;      // host-pinned residual landing slot (coherent, mapped)
   double *pinned_dev = nullptr;  // its device address: k_reduce stores the residual there
   hipEvent_t ev_check = nullptr;  // recorded after each residual copy
+  unsigned long long check_seq = 0;  // sequence number of the last residual check
+  int poll = 1;                      // TVL1_POLL: wait for a residual by polling its
+                                     // sequence number in host memory (0: event sync)
   hipEvent_t ev_order = nullptr;  // orders work on the caller's stream after a zero fill
   std::vector<char *> retired;    // arenas outgrown while possibly in use (arena_alloc)
   // dispatch: the defaults are the measured best; the environment knobs are
@@ -400,6 +403,37 @@ static double survey_bytes(const Geometry &g, int warps, const int64_t *iters) {
 // so those iterations run as ONE temporally blocked pass (<= kTbMax iterations);
 // the residual of the check is then read exactly where OpenCV reads it.
 //
+// One residual check: k_reduce sums the per-block partials in a fixed order into coherent
+// host memory, and the host reads it once the kernel is done -- by polling the check's
+// sequence number, which k_reduce stores after the residual (a few us sooner than an event
+// wait), or with c->poll = 0 by an event.  The poll gives up on a stream error.
+static tvl1_status read_residual(tvl1_ctx *c, hipStream_t st, int nparts, double *out) {
+  unsigned long long *seq_host = (unsigned long long *)(c->pinned + 1);
+  unsigned long long *seq_dev = (unsigned long long *)(c->pinned_dev + 1);
+  const unsigned long long seq = ++c->check_seq;
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, nparts, c->pinned_dev,
+                     c->poll ? seq_dev : nullptr, seq);
+  if (!c->poll) {
+    HIP_TRY(c, hipEventRecord(c->ev_check, st));
+    HIP_TRY(c, hipEventSynchronize(c->ev_check));
+  } else {
+    HIP_TRY(c, hipGetLastError());
+    for (unsigned spins = 1;; ++spins) {
+      if (__atomic_load_n(seq_host, __ATOMIC_ACQUIRE) == seq) break;
+      if ((spins & 4095) == 0) {   // now and then: has the stream failed or finished?
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipSuccess && e != hipErrorNotReady)
+          return set_err(c, TVL1_EHIP, "residual check: %s", hipGetErrorString(e));
+        if (e == hipSuccess && __atomic_load_n(seq_host, __ATOMIC_ACQUIRE) != seq)
+          return set_err(c, TVL1_EHIP, "residual check: stream idle without the residual");
+      }
+      __builtin_ia32_pause();
+    }
+  }
+  *out = *(volatile double *)c->pinned;
+  return TVL1_OK;
+}
+
 // resize(): an exact 2x downscale of INTER_LINEAR takes the INTER_AREA fast path
 static int area_fast_of(double sx, double sy) {
   const int ix = (int)std::lrint(sx), iy = (int)std::lrint(sy);
@@ -510,11 +544,12 @@ static tvl1_status solve_dualtvl1(tvl1_ctx *c, const Frames &in, int W, int H, f
             hipLaunchKernelGGL((k_iterate<true, false, true>), dim3(nblk), dim3(kBlock), 0, st, a);
           else
             hipLaunchKernelGGL((k_iterate<false, false, true>), dim3(nblk), dim3(kBlock), 0, st, a);
-          hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, nblk,
-                             c->pinned_dev);
-          HIP_TRY(c, hipEventRecord(c->ev_check, st));
-          HIP_TRY(c, hipEventSynchronize(c->ev_check));
-          error = (float)*c->pinned;
+          double e = 0.0;
+          {
+            const tvl1_status r = read_residual(c, st, nblk, &e);
+            if (r != TVL1_OK) return r;
+          }
+          error = (float)e;
           p_zero = false;
           ui ^= 1;
           pi ^= 1;
@@ -921,11 +956,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
         if (calc_end) {
           // the residual lands in coherent host memory (no copy launch); the event below
           // orders the host's read after the kernel
-          hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, blocks,
-                             c->pinned_dev);
-          HIP_TRY(c, hipEventRecord(c->ev_check, st));
-          HIP_TRY(c, hipEventSynchronize(c->ev_check));  // the cuda::sum -> host read
-          error = *c->pinned;
+          TRY(read_residual(c, st, blocks, &error));   // the cuda::sum -> host read
           prevError = error;
           ++checks;
           const bool ends = !(error > scaledEps && n < prm.iterations);
@@ -1645,6 +1676,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_ROLL_SEG")) c->roll_seg = atoi(m);
   if (const char *m = getenv("TVL1_ROLL_PX4_MIN")) c->roll_px4_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_POLL")) c->poll = atoi(m);
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
   if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels

@@ -2092,7 +2092,11 @@ __global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
 }
 
 // K7: fixed-order sum of the per-block partials (one block).
-__global__ void k_reduce(const double *__restrict__ partials, int n, double *__restrict__ out) {
+// The residual goes to coherent host memory; with seq_out set, the check's sequence number
+// follows it there (after a system-scope fence), so the host can poll for it instead of
+// waiting on an event.
+__global__ void k_reduce(const double *__restrict__ partials, int n, double *__restrict__ out,
+                         unsigned long long *seq_out, unsigned long long seq) {
   __shared__ double s[kBlock];
   double acc = 0.0;
   for (int i = threadIdx.x; i < n; i += kBlock) acc += partials[i];
@@ -2102,7 +2106,13 @@ __global__ void k_reduce(const double *__restrict__ partials, int n, double *__r
     if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = s[0];
+  if (threadIdx.x == 0) {
+    out[0] = s[0];
+    if (seq_out) {
+      __threadfence_system();
+      *(volatile unsigned long long *)seq_out = seq;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- misc

@@ -29,7 +29,10 @@ using namespace tvl1k;
     }                                                                            \
   } while (0)
 
-constexpr int M = 6, BW = 128;
+#ifndef WI_BW
+#define WI_BW 128
+#endif
+constexpr int M = 6, BW = WI_BW;
 
 template <int FM, int PRIO>
 __global__ __launch_bounds__(64 + BW) void k_probe(WarpIterArgs w, unsigned long long *ts) {
