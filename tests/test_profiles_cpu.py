@@ -1,0 +1,54 @@
+"""The committed measurement evidence agrees with itself: the bench line's
+roofline fraction, which the engine computes from its live per-launch byte accounting and
+HIP-event launch times, must match the fraction recomputed by hand from the rocprofv3 kernel
+stats and the PMC byte counts of the same tree within 5 %, and the accounted bytes must match
+the PMC bytes.  Reads only files under profiles/ (tools/roofline_check.py does the same)."""
+import csv
+import json
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+PROF = ROOT / "profiles"
+ITER = ("k_iterate", "k_warp_iter")
+
+
+def _bench(name):
+    return json.loads(Path(PROF / "r2" / name).read_text().splitlines()[-1])
+
+
+@pytest.mark.parametrize("stats,bench", [("kernel_stats_single_pair_prio.csv", "bench_c2_final.json")])
+def test_roofline_frac_matches_rocprof_and_pmc(stats, bench):
+    traffic = json.loads((PROF / "traffic.json").read_text())
+    calls = ns = 0.0
+    for r in csv.DictReader(open(PROF / "r2" / stats)):
+        name = r["Name"].split("(")[0].replace("void ", "").replace("tvl1k::", "")
+        if name.startswith(ITER):
+            calls += int(r["Calls"])
+            ns += float(r["TotalDurationNs"])
+    assert calls == traffic["dispatches"]
+    avg_us = ns / calls / 1e3
+    by_hand = traffic["iterate_hbm_bytes_per_launch"] / (avg_us * 1e-6) / 8e12
+    roof = _bench(bench)["roofline"]
+    assert roof["unit"] == "GB/s" and roof["peak"] == 8000.0
+    assert abs(roof["frac"] / by_hand - 1) < 0.05, (roof["frac"], by_hand)
+    # the engine's live byte accounting against the PMC bytes of the same launches
+    assert abs(roof["bytes_per_launch"] / traffic["iterate_hbm_bytes_per_launch"] - 1) < 0.02
+    assert roof["model_bytes_over_peak"] > 1.0 > roof["frac"]   # the SURVEY model is not frac
+
+
+def test_bench_line_carries_the_contract_fields():
+    d = _bench("bench_c2_final.json")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["config"]["workload"].startswith("C2")
+    cb = d["cpu_baseline"]
+    assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
+    modes = d["math_modes"]
+    for m in ("fast", "fma"):
+        e = modes[m]["epe_vs_headline_px"]
+        assert modes[m]["same_iterations"]
+        assert e["mean"] <= 1e-3 and e["p99.9"] <= 2e-2 and e["max"] <= 0.5
