@@ -105,9 +105,10 @@ def test_constant_images_give_zero_flow(engine):
 MODES = ["", "TVL1_ROLL_LONG_MIN=0", "TVL1_ROLL_LONG_MIN=0,TVL1_ROLL_SEG=8", "TVL1_ROLL_SEG=8",
          "TVL1_ROLL_SEG=64", "TVL1_ROLL_PX4_MIN=0", "TVL1_ROLL_PX4_MIN=0,TVL1_ROLL_SEG=8",
          "TVL1_FUSE_MIN=0", "TVL1_FUSE_MIN=0,TVL1_ROLL_SEG=8", "TVL1_FUSE_MIN=0,TVL1_ROLL_PX4_MIN=0",
-         "TVL1_FUSE=0,TVL1_ROLL_LONG_MIN=0", "TVL1_BUF_LIMIT=100000", "TVL1_BUF_LIMIT=0"]
+         "TVL1_FUSE=0,TVL1_ROLL_LONG_MIN=0", "TVL1_BUF_LIMIT=100000", "TVL1_BUF_LIMIT=0",
+         "TVL1_POLL=0"]   # (the last: residuals read after an event instead of the poll)
 KNOBS = ("TVL1_ROLL_SEG", "TVL1_ROLL_PX4_MIN", "TVL1_ROLL_LONG_MIN", "TVL1_FUSE", "TVL1_FUSE_MIN",
-         "TVL1_BUF_LIMIT", "TVL1_BATCH_FUSE")
+         "TVL1_BUF_LIMIT", "TVL1_BATCH_FUSE", "TVL1_POLL")
 CONFIG_CASES = [
     (250, 131, 21, dict(nscales=5, warps=5)),
     (97, 201, 22, dict(nscales=4, warps=3, gamma=0.1)),
