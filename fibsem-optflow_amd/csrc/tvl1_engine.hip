@@ -7,6 +7,7 @@
 // every stage runs on the device; the only device->host traffic inside a solve is
 // the residual of "check" iterations, read exactly where OpenCV reads it.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <chrono>
 
 #include <cfloat>
@@ -427,7 +428,12 @@ static tvl1_status read_residual(tvl1_ctx *c, hipStream_t st, int nparts, double
         if (e == hipSuccess && __atomic_load_n(seq_host, __ATOMIC_ACQUIRE) != seq)
           return set_err(c, TVL1_EHIP, "residual check: stream idle without the residual");
       }
-      __builtin_ia32_pause();
+      // spin briefly, then give the core away between reads (a caller may run many
+      // contexts and other host work, e.g. the CLI's decode threads)
+      if (spins < 2048)
+        __builtin_ia32_pause();
+      else
+        sched_yield();
     }
   }
   *out = *(volatile double *)c->pinned;
