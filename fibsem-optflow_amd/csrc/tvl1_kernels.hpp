@@ -1693,7 +1693,16 @@ template <bool G, int K, int PX, int FM>
 __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   constexpr int HALO = roll_halo<K, PX>();
   constexpr int BW = 64 * PX;            // band width (px)
-  const IterArgs &a = ra.it;
+  // The long pipelines (and the gamma ones) run at 2 waves/SIMD with VGPRs to spare but
+  // SGPRs at the 106 cap: their float parameters live in VGPRs (an opaque copy, same
+  // values), which ends the SGPR spills of k_iterate_roll<4, 2> and <2, 4>.
+  IterArgs a = ra.it;
+  if (G || K * PX >= 8) {
+    asm volatile("v_mov_b32 %0, %1" : "=v"(a.l_t) : "s"(a.l_t));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(a.theta) : "s"(a.theta));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(a.taut) : "s"(a.taut));
+    if (G) asm volatile("v_mov_b32 %0, %1" : "=v"(a.gamma) : "s"(a.gamma));
+  }
   const RollBufs &B = ra.b;
   const int lane = threadIdx.x & 63;
   const int band = wid % ra.bands, seg = wid / ra.bands;
