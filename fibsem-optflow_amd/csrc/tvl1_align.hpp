@@ -485,11 +485,88 @@ static inline double reproj_err2(const double H[9], const Pt &a, const Pt &b) {
   return (x - b.x) * (x - b.x) + (y - b.y) * (y - b.y);
 }
 
+// findHomography's last step: Levenberg-Marquardt on the 8 free entries (H[8] = 1) over the
+// inliers' reprojection residuals (HomographyRefineCallback: r = H(a) - b, analytic
+// Jacobian), at most `iters` steps.  The LM form of OpenCV's LMSolver: the normal
+// equations' diagonal scaled by (1 + lambda), lambda from 1e-3, /10 after a step that lowers
+// the error and x10 (the step rejected) otherwise.
+static void lm_refine(const std::vector<Pt> &a, const std::vector<Pt> &b, double H[9], int iters) {
+  const size_t n = a.size();
+  if (n < 4) return;
+  auto err = [&](const double *h) {
+    double e = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+      const double hh[9] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], 1.0};
+      e += reproj_err2(hh, a[i], b[i]);
+    }
+    return e;
+  };
+  double h[8];
+  for (int k = 0; k < 8; ++k) h[k] = H[k] / H[8];
+  double e = err(h), lambda = 1e-3;
+  for (int it = 0; it < iters; ++it) {
+    double A[8][8] = {}, g[8] = {};
+    for (size_t i = 0; i < n; ++i) {
+      const double x = a[i].x, y = a[i].y;
+      const double w = h[6] * x + h[7] * y + 1.0;
+      if (std::fabs(w) < 1e-12) continue;
+      const double iw = 1.0 / w;
+      const double X = (h[0] * x + h[1] * y + h[2]) * iw, Y = (h[3] * x + h[4] * y + h[5]) * iw;
+      const double rx = X - b[i].x, ry = Y - b[i].y;
+      const double jx[8] = {x * iw, y * iw, iw, 0, 0, 0, -X * x * iw, -X * y * iw};
+      const double jy[8] = {0, 0, 0, x * iw, y * iw, iw, -Y * x * iw, -Y * y * iw};
+      for (int r = 0; r < 8; ++r) {
+        g[r] += jx[r] * rx + jy[r] * ry;
+        for (int c = 0; c < 8; ++c) A[r][c] += jx[r] * jx[c] + jy[r] * jy[c];
+      }
+    }
+    for (;;) {   // solve (A + lambda diag(A)) d = -g; retry with a larger lambda on failure
+      double M[8][9];
+      for (int r = 0; r < 8; ++r) {
+        for (int c = 0; c < 8; ++c) M[r][c] = A[r][c] * (r == c ? 1.0 + lambda : 1.0);
+        M[r][8] = -g[r];
+      }
+      bool ok = true;
+      for (int c = 0; c < 8 && ok; ++c) {
+        int p = c;
+        for (int r = c + 1; r < 8; ++r)
+          if (std::fabs(M[r][c]) > std::fabs(M[p][c])) p = r;
+        if (std::fabs(M[p][c]) < 1e-300) {
+          ok = false;
+          break;
+        }
+        for (int k = 0; k < 9; ++k) std::swap(M[c][k], M[p][k]);
+        for (int r = 0; r < 8; ++r) {
+          if (r == c) continue;
+          const double f = M[r][c] / M[c][c];
+          for (int k = c; k < 9; ++k) M[r][k] -= f * M[c][k];
+        }
+      }
+      if (!ok) return;
+      double hn[8];
+      for (int k = 0; k < 8; ++k) hn[k] = h[k] + M[k][8] / M[k][k];
+      const double en = err(hn);
+      if (std::isfinite(en) && en < e) {
+        std::copy(hn, hn + 8, h);
+        e = en;
+        lambda = std::max(lambda / 10.0, 1e-16);
+        break;
+      }
+      lambda *= 10.0;
+      if (lambda > 1e16) return;
+    }
+  }
+  for (int k = 0; k < 8; ++k) H[k] = h[k];
+  H[8] = 1.0;
+}
+
 // cv::findHomography(src, dst, method, ransacReprojThreshold) restated: RANSAC (8) or LMEDS
-// (4), iteration counts as OpenCV's registrators (below), refit on the inliers.
-// Deterministic (fixed seed).  Returns false when no model is found.
+// (4), iteration counts as OpenCV's registrators (below), a DLT refit on the inliers, then
+// 10 Levenberg-Marquardt steps on their reprojection error (fundam.cpp's createLMSolver(
+// HomographyRefineCallback, 10)).  Deterministic (fixed seed).  Returns false when no model
+// is found; mask (n entries, optional) gets the inliers.
 static bool find_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, int method,
-                            double thresh, double H[9]) {
+                            double thresh, double H[9], uint8_t *mask = nullptr) {
   const int n = (int)a.size();
   if (n < 4) return false;
   std::mt19937 rng(0x12345678u);
@@ -542,13 +619,17 @@ static bool find_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, 
   // inliers of the best hypothesis, then a least-squares refit
   const double lt2 = lmeds ? 2.5 * 2.5 * 1.4826 * 1.4826 * (1 + 5.0 / std::max(1, n - 4)) * best_med : t2;
   std::vector<Pt> ia, ib;
-  for (int i = 0; i < n; ++i)
-    if (reproj_err2(best, a[i], b[i]) <= lt2) {
+  for (int i = 0; i < n; ++i) {
+    const bool in = reproj_err2(best, a[i], b[i]) <= lt2;
+    if (mask) mask[i] = in ? 1 : 0;
+    if (in) {
       ia.push_back(a[i]);
       ib.push_back(b[i]);
     }
+  }
   double h[9];
   if (ia.size() >= 4 && dlt_homography(ia, ib, h)) std::copy(h, h + 9, best);
+  if (ia.size() > 4) lm_refine(ia, ib, best, 10);
   std::copy(best, best + 9, H);
   return true;
 }

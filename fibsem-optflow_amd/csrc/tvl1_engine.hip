@@ -1758,6 +1758,27 @@ tvl1_status tvl1_calc(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const uint8
                (hipStream_t)stream);
 }
 
+tvl1_status tvl1_find_homography(const float *src_xy, const float *dst_xy, int32_t n,
+                                 int32_t method, double thresh, double H[9], uint8_t *mask) {
+  if (!src_xy || !dst_xy || !H || n < 4 || !(method == 0 || method == 4 || method == 8))
+    return set_err(nullptr, TVL1_EINVAL, "find_homography: need n >= 4 points and method 0, 4 or 8");
+  std::vector<Pt> a(n), b(n);
+  for (int i = 0; i < n; ++i) {
+    a[i] = Pt{src_xy[2 * i], src_xy[2 * i + 1]};
+    b[i] = Pt{dst_xy[2 * i], dst_xy[2 * i + 1]};
+  }
+  if (method == 0) {   // all points: the least-squares fit, then the LM refinement
+    if (!dlt_homography(a, b, H))
+      return set_err(nullptr, TVL1_ESIZE, "find_homography: degenerate points");
+    lm_refine(a, b, H, 10);
+    if (mask) std::fill(mask, mask + n, (uint8_t)1);
+    return TVL1_OK;
+  }
+  if (!find_homography(a, b, method, thresh, H, mask))
+    return set_err(nullptr, TVL1_ESIZE, "find_homography: no model found");
+  return TVL1_OK;
+}
+
 tvl1_status tvl1_calc_f32(tvl1_ctx *c, const float *I0, size_t pitch0, const float *I1,
                           size_t pitch1, int32_t W, int32_t H, float *u, float *v, size_t fpitch,
                           tvl1_stats *stats, void *stream) {

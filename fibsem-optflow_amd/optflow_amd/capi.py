@@ -18,7 +18,7 @@ REPO_ROOT = PKG_ROOT.parent
 ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
 
 TVL1_MAX_LEVELS = 32
-ABI_VERSION = 5          # TVL1_ABI_VERSION of include/tvl1.h
+ABI_VERSION = 6          # TVL1_ABI_VERSION of include/tvl1.h
 STATUS = {0: "TVL1_OK", 1: "TVL1_EINVAL", 2: "TVL1_ESIZE", 3: "TVL1_EHIP",
           4: "TVL1_ENOMEM", 5: "TVL1_ENODEV"}
 
@@ -181,6 +181,9 @@ def load_engine() -> C.CDLL:
                                         C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
                                         C.POINTER(C.c_float), C.c_void_p]
     lib.tvl1_warp_affine_u8.restype = C.c_int
+    lib.tvl1_find_homography.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_double,
+                                         C.POINTER(C.c_double), C.c_void_p]
+    lib.tvl1_find_homography.restype = C.c_int
     lib.tvl1_postprocess_affine.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                             C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
                                             C.c_int32, C.POINTER(C.c_float), C.c_void_p]
@@ -356,3 +359,20 @@ class Engine:
 def epe(u, v, u_ref, v_ref) -> np.ndarray:
     """Per-pixel end-point error."""
     return np.sqrt((u.astype(np.float64) - u_ref) ** 2 + (v.astype(np.float64) - v_ref) ** 2)
+
+
+def find_homography(src: np.ndarray, dst: np.ndarray, method: int = 8, thresh: float = 5.0):
+    """tvl1_find_homography (cv::findHomography restated, host only): src, dst (n, 2) point
+    arrays; returns (H 3x3, inlier mask) or raises TVL1Error."""
+    lib = load_engine()
+    a = np.ascontiguousarray(src, dtype=np.float32)
+    b = np.ascontiguousarray(dst, dtype=np.float32)
+    n = a.shape[0]
+    H = (C.c_double * 9)()
+    mask = np.zeros(n, np.uint8)
+    rc = lib.tvl1_find_homography(a.ctypes.data, b.ctypes.data, n, method, thresh, H,
+                                  mask.ctypes.data)
+    if rc != 0:
+        raise TVL1Error(f"tvl1_find_homography: {STATUS.get(rc, rc)}: "
+                        f"{lib.tvl1_last_error(None).decode()}")
+    return np.array(H[:], dtype=np.float64).reshape(3, 3), mask.astype(bool)

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TVL1_ABI_VERSION 5
+#define TVL1_ABI_VERSION 6
 #define TVL1_MAX_LEVELS 32
 
 typedef enum tvl1_status {
@@ -193,6 +193,16 @@ tvl1_status tvl1_find_alignment(tvl1_ctx *ctx,
                                 const uint8_t *frame0, size_t pitch0, int32_t w0, int32_t h0,
                                 const tvl1_align_params *params, float affine[6],
                                 int32_t *n_good, int32_t *outcome, void *stream);
+
+/* cv::findHomography(src, dst, method, ransacReprojThreshold) on host point lists
+ * (features.cpp:131-133; the model tvl1_find_alignment fits): method 8 = RANSAC, 4 = LMEDS,
+ * 0 = all points; a normalised DLT refit on the inliers, then 10 Levenberg-Marquardt steps
+ * on their reprojection error.  src / dst: n (x, y) pairs; H: row-major 3x3, H[8] = 1;
+ * inlier_mask: n bytes or NULL.  Host only (no GPU work, ctx not needed).  TVL1_EINVAL for
+ * n < 4 or a bad method; TVL1_ESIZE when no model is found (all hypotheses degenerate). */
+tvl1_status tvl1_find_homography(const float *src_xy, const float *dst_xy, int32_t n,
+                                 int32_t method, double ransac_threshold, double H[9],
+                                 uint8_t *inlier_mask);
 
 /* cv::cuda::warpAffine(src, dst, M, dsize, INTER_LINEAR, BORDER_CONSTANT, 0) on u8
  * (optflow.cpp:370): dst(x, y) = src(M^-1 (x, y)).  Device pointers, async on stream. */

@@ -1,0 +1,65 @@
+"""tvl1_find_homography: cv::findHomography restated on the host (features.cpp:131-133 fit
+the model tvl1_find_alignment uses): RANSAC / LMEDS / all-points, a DLT refit on the inliers,
+then OpenCV's 10 Levenberg-Marquardt steps on their reprojection error.  Parity with OpenCV
+itself is unpinned (OpenCV is absent); these are known-answer and optimality properties."""
+import numpy as np
+import pytest
+
+from optflow_amd import capi
+
+H_TRUE = np.array([[1.02, 0.03, 12.5], [-0.025, 0.985, -7.25], [2e-5, -1.5e-5, 1.0]])
+
+
+def project(H, p):
+    q = np.c_[p, np.ones(len(p))] @ H.T
+    return q[:, :2] / q[:, 2:]
+
+
+def rms(H, a, b):
+    return float(np.sqrt(np.mean(np.sum((project(H, a) - b) ** 2, axis=1))))
+
+
+def dlt(a, b):
+    """plain least-squares DLT with H[2,2] = 1 (what the refit does before LM)"""
+    rows, rhs = [], []
+    for (x, y), (u, v) in zip(a, b):
+        rows.append([x, y, 1, 0, 0, 0, -u * x, -u * y]); rhs.append(u)
+        rows.append([0, 0, 0, x, y, 1, -v * x, -v * y]); rhs.append(v)
+    h = np.linalg.lstsq(np.array(rows), np.array(rhs), rcond=None)[0]
+    return np.append(h, 1.0).reshape(3, 3)
+
+
+@pytest.mark.parametrize("method", [0, 4, 8])
+def test_exact_correspondences_give_the_homography(built, method):
+    rng = np.random.default_rng(1)
+    a = rng.uniform(0, 3000, (60, 2))
+    b = project(H_TRUE, a)
+    H, mask = capi.find_homography(a, b, method, 3.0)
+    assert mask.all()
+    assert rms(H, a.astype(np.float32), b.astype(np.float32)) < 2e-3   # float32 inputs
+    np.testing.assert_allclose(H, H_TRUE, rtol=2e-4, atol=2e-6)
+
+
+@pytest.mark.parametrize("method", [4, 8])
+def test_outliers_rejected_and_lm_not_worse_than_dlt(built, method):
+    rng = np.random.default_rng(7)
+    a = rng.uniform(0, 3000, (120, 2))
+    b = project(H_TRUE, a) + rng.normal(0, 0.7, (120, 2))
+    out = rng.choice(120, 30, replace=False)
+    b[out] += rng.uniform(40, 300, (30, 2)) * rng.choice([-1, 1], (30, 2))
+    H, mask = capi.find_homography(a, b, method, 5.0)
+    inl = np.setdiff1d(np.arange(120), out)
+    assert mask[inl].all() and not mask[out].any()
+    a32, b32 = a.astype(np.float32).astype(np.float64), b.astype(np.float32).astype(np.float64)
+    # the LM step minimises the inliers' reprojection error: at least as good as the DLT
+    assert rms(H, a32[inl], b32[inl]) <= rms(dlt(a32[inl], b32[inl]), a32[inl], b32[inl]) + 1e-9
+    assert rms(H, a32[inl], b32[inl]) < 1.0
+
+
+def test_rejects_bad_calls(built):
+    a = np.zeros((3, 2))
+    with pytest.raises(capi.TVL1Error):
+        capi.find_homography(a, a, 8)
+    b = np.random.default_rng(0).uniform(0, 10, (10, 2))
+    with pytest.raises(capi.TVL1Error):
+        capi.find_homography(b, b, 5)
