@@ -110,7 +110,7 @@ struct BatchWI {
 };
 template <int M, int FM>
 __global__ __launch_bounds__(192) void kb_warp_iter(BatchWI bw) {
-  __shared__ float ring[kWiRows * 3 * wi_ww<M, 128>()];
+  __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, 128>()];
   __shared__ float cring[2 * 5 * 128];
   const int b = bw.sel.idx[blockIdx.y];
   WarpIterArgs w = bw.w;

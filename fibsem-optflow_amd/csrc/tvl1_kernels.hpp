@@ -1821,7 +1821,16 @@ struct WarpIterArgs {
   int store_c;           // also store I1wx / I1wy / rho (ra.it.I1wx, ...) for later passes
 };
 
-constexpr int kWiRows = 16;   // window ring rows
+// window ring rows: 16 for the shipped margin M = 6 (a power of two: slot = row & 15);
+// tighter margins take 2M + 2 rows (slot = row mod R, rows >= -64R)
+template <int M>
+constexpr int wi_rows() { return M == 6 ? 16 : 2 * M + 2; }
+template <int M>
+__device__ __forceinline__ int wi_slot(int r) {
+  constexpr int R = wi_rows<M>();
+  if ((R & (R - 1)) == 0) return r & (R - 1);
+  return (int)((unsigned)(r + 64 * R) % (unsigned)R);
+}
 // band width BW (px): 128 = 64 consumer lanes x 2 px + 2 producers (default), or 64 =
 // 64 lanes x 1 px + 1 producer (consumer and producer steps of similar length)
 template <int M, int BW>
@@ -1832,7 +1841,7 @@ template <int M, int BW>
 __device__ __forceinline__ void wi_ring_put(float *__restrict__ ring, const WarpRowI &v, int r,
                                             int p, int lane) {
   constexpr int WW = wi_ww<M, BW>();
-  float *dst = ring + (r & (kWiRows - 1)) * (3 * WW);
+  float *dst = ring + wi_slot<M>(r) * (3 * WW);
   const int k0 = 64 * p + lane;
   dst[k0] = v.c0;
   dst[WW + k0] = 0.5f * (v.r0 - v.l0);
@@ -1877,7 +1886,7 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
   if (inwin) {
     warp_gather_fn<FM>(
         [&](int cy, int cx) {
-          const float *q = ring + (cy & (kWiRows - 1)) * (3 * WW) + (cx - P.xw0);
+          const float *q = ring + wi_slot<M>(cy) * (3 * WW) + (cx - P.xw0);
           return Tap3{q[0], q[WW], q[2 * WW]};
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
@@ -1963,7 +1972,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
                                                float *__restrict__ cring) {
   constexpr int K = 2, PX = BW / 64, HALO = roll_halo<2, PX>(), WW = wi_ww<M, BW>();
   static_assert(BW == 64 || BW == 128, "one producer per 64 columns, PX = 1 or 2");
-  static_assert(2 * M + 2 <= kWiRows, "window ring too small for the margin");
+  static_assert(2 * M + 2 <= wi_rows<M>(), "window ring too small for the margin");
   static_assert(2 * M <= 64, "second window slot per lane");
   static_assert(kRollAhead == 2 && kWarpAhead == 2, "the step loops are unrolled by 3");
   (void)WW;
@@ -2093,7 +2102,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
 
 template <int M, int FM = 0, int BW = 128, int PRIO = 1>
 __global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
-  __shared__ float ring[kWiRows * 3 * wi_ww<M, BW>()];
+  __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, BW>()];
   __shared__ float cring[2 * 5 * BW];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves) return;   // whole blocks

@@ -32,11 +32,19 @@ using namespace tvl1k;
 #ifndef WI_BW
 #define WI_BW 128
 #endif
-constexpr int M = 6, BW = WI_BW;
+#ifndef WI_M
+#define WI_M 6
+#endif
+constexpr int M = WI_M, BW = WI_BW;
 
+#ifdef WI_WPE
+#define WI_ATTR __attribute__((amdgpu_waves_per_eu(WI_WPE)))
+#else
+#define WI_ATTR
+#endif
 template <int FM, int PRIO>
-__global__ __launch_bounds__(64 + BW) void k_probe(WarpIterArgs w, unsigned long long *ts) {
-  __shared__ float ring[kWiRows * 3 * wi_ww<M, BW>()];
+__global__ __launch_bounds__(64 + BW) WI_ATTR void k_probe(WarpIterArgs w, unsigned long long *ts) {
+  __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, BW>()];
   __shared__ float cring[2 * 5 * BW];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves) return;
