@@ -8,6 +8,7 @@
 // the residual of "check" iterations, read exactly where OpenCV reads it.
 #include <hip/hip_runtime.h>
 #include <sched.h>
+#include <atomic>
 #include <chrono>
 
 #include <cfloat>
@@ -68,7 +69,11 @@ struct tvl1_ctx {
   int partials_cap = 0;
   double *pinned = nullptr;      // host-pinned residual landing slot (coherent, mapped)
   double *pinned_dev = nullptr;  // its device address: k_reduce stores the residual there
-  hipEvent_t ev_check = nullptr;  // recorded after each residual copy
+  hipEvent_t ev_check[2] = {};   // recorded after each residual check (by sequence parity)
+  unsigned long long *gate = nullptr;   // device word: the speculation gate
+  int spec = 1;                   // TVL1_SPEC: 0 no launches enqueued behind a check, 1 when the
+                                  // solve is alone on its device (this process), 2 always
+  int spec_trace = 0;             // TVL1_SPEC_TRACE=1: one stderr line per check and guess
   unsigned long long check_seq = 0;  // sequence number of the last residual check
   int poll = 1;                      // TVL1_POLL: wait for a residual by polling its
                                      // sequence number in host memory (0: event sync)
@@ -408,24 +413,36 @@ static double survey_bytes(const Geometry &g, int warps, const int64_t *iters) {
 // host memory, and the host reads it once the kernel is done -- by polling the check's
 // sequence number, which k_reduce stores after the residual (a few us sooner than an event
 // wait), or with c->poll = 0 by an event.  The poll gives up on a stream error.
-static tvl1_status read_residual(tvl1_ctx *c, hipStream_t st, int nparts, double *out) {
-  unsigned long long *seq_host = (unsigned long long *)(c->pinned + 1);
+//
+// Checks are split in two so that work can be enqueued behind a check before the host reads
+// it (speculation): launch_check enqueues k_reduce (residual slot and event by the
+// parity of its sequence number, so the next check cannot overwrite a residual the host has
+// not read yet), wait_check reads it.
+static tvl1_status launch_check(tvl1_ctx *c, hipStream_t st, int nparts, const CheckGate &g,
+                                unsigned long long *seq_out) {
   unsigned long long *seq_dev = (unsigned long long *)(c->pinned_dev + 1);
   const unsigned long long seq = ++c->check_seq;
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, nparts, c->pinned_dev,
-                     c->poll ? seq_dev : nullptr, seq);
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, nparts,
+                     c->pinned_dev + ((seq & 1) ? 2 : 0), c->poll ? seq_dev : nullptr, seq, g);
+  HIP_TRY(c, hipGetLastError());
+  if (!c->poll) HIP_TRY(c, hipEventRecord(c->ev_check[seq & 1], st));
+  *seq_out = seq;
+  return TVL1_OK;
+}
+
+static tvl1_status wait_check(tvl1_ctx *c, hipStream_t st, unsigned long long seq, double *out) {
+  unsigned long long *seq_host = (unsigned long long *)(c->pinned + 1);
   if (!c->poll) {
-    HIP_TRY(c, hipEventRecord(c->ev_check, st));
-    HIP_TRY(c, hipEventSynchronize(c->ev_check));
+    HIP_TRY(c, hipEventSynchronize(c->ev_check[seq & 1]));
   } else {
-    HIP_TRY(c, hipGetLastError());
+    // a later (speculative) check may already have stored its own, larger number
     for (unsigned spins = 1;; ++spins) {
-      if (__atomic_load_n(seq_host, __ATOMIC_ACQUIRE) == seq) break;
+      if (__atomic_load_n(seq_host, __ATOMIC_ACQUIRE) >= seq) break;
       if ((spins & 4095) == 0) {   // now and then: has the stream failed or finished?
         const hipError_t e = hipStreamQuery(st);
         if (e != hipSuccess && e != hipErrorNotReady)
           return set_err(c, TVL1_EHIP, "residual check: %s", hipGetErrorString(e));
-        if (e == hipSuccess && __atomic_load_n(seq_host, __ATOMIC_ACQUIRE) != seq)
+        if (e == hipSuccess && __atomic_load_n(seq_host, __ATOMIC_ACQUIRE) < seq)
           return set_err(c, TVL1_EHIP, "residual check: stream idle without the residual");
       }
       // spin briefly, then give the core away between reads (a caller may run many
@@ -436,8 +453,16 @@ static tvl1_status read_residual(tvl1_ctx *c, hipStream_t st, int nparts, double
         sched_yield();
     }
   }
-  *out = *(volatile double *)c->pinned;
+  *out = *(volatile double *)(c->pinned + ((seq & 1) ? 2 : 0));
   return TVL1_OK;
+}
+
+static tvl1_status read_residual(tvl1_ctx *c, hipStream_t st, int nparts, double *out) {
+  CheckGate g{};
+  unsigned long long seq = 0;
+  const tvl1_status r = launch_check(c, st, nparts, g, &seq);
+  if (r != TVL1_OK) return r;
+  return wait_check(c, st, seq, out);
 }
 
 // resize(): an exact 2x downscale of INTER_LINEAR takes the INTER_AREA fast path
@@ -603,10 +628,21 @@ static tvl1_status solve_dualtvl1(tvl1_ctx *c, const Frames &in, int W, int H, f
   return TVL1_OK;
 }
 
+// Solves in progress per device in this process.  Speculation pays only for a
+// solve alone on its device: with other pairs in flight their kernels already fill the
+// check round trips, and a wrong guess would cost them GPU time.
+static std::atomic<int> g_solving[64];
+struct SolveCount {
+  int d;
+  explicit SolveCount(int dev) : d(dev & 63) { g_solving[d].fetch_add(1, std::memory_order_relaxed); }
+  ~SolveCount() { g_solving[d].fetch_sub(1, std::memory_order_relaxed); }
+};
+
 static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, float *v,
                          size_t fpitch, tvl1_stats *stats, hipStream_t st) {
   const tvl1_params &prm = c->prm;
   if (prm.profile == 1) return solve_dualtvl1(c, in, W, H, u, v, fpitch, stats, st);
+  const SolveCount active(c->device);
   const Geometry &g = c->geo;
   const int L = g.L;
   const bool gam = g.gamma;
@@ -662,6 +698,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
 
   int64_t level_iters[TVL1_MAX_LEVELS] = {};
   int64_t checks = 0;
+  int32_t spec_misses = 0;   // speculative launches that ran empty
 
   // ---- launch helpers
   // The streaming kernels (k_iterate_roll, k_warp_ring, k_warp_iter) take 32-bit buffer
@@ -748,6 +785,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     if (r_ != TVL1_OK) return r_;      \
   } while (0)
 
+  double w0_hint = 50.0;   // speculation: residual / (eps^2 W H) at a level's first check
   for (int s = L - 1; s >= 0; --s) {
     const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
     const double Nl = (double)lw * lh;
@@ -774,43 +812,12 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     const bool roll_ok = buffer_ok(s);
     const bool roll_long = roll_ok && (long)((lw + 55) / 56) * ((lh + 31) / 32) >= c->roll_long_min;
 
-    int last_warp_n = -1;   // iterations of the level's previous warp
-    for (int wp = 0; wp < prm.warps; ++wp) {
-      if (median) {
-        hipLaunchKernelGGL(k_median, grid2(lw, lh, 2), kBlk2, 0, st, c->U[ui][0], c->U[ui][1],
-                           lw, lh, P, prm.median_filtering, c->U[ui ^ 1][0], c->U[ui ^ 1][1]);
-        if (gam) {
-          const size_t n = (size_t)P * lh * sizeof(float);
-          HIP_TRY(c, hipMemcpyAsync(c->U[ui ^ 1][2], c->U[ui][2], n, hipMemcpyDeviceToDevice, st));
-        }
-        ui ^= 1;
-      }
-      // warpBackward fused into the warp's first pass (2 iterations ending in the first
-      // check) when that pass would stream through k_iterate_roll anyway
-      const bool fuse = c->fuse && !gam && !exact_div && roll_ok && prm.epsilon > 0 &&
-                        prm.iterations >= 2 && (long)lw * lh >= c->fuse_min;
-      bool fused_nostore = false;   // k_warp_iter ran without storing the constants
-      if (!fuse) TRY(gather(s, ui, cb, wp));
-      a.I1wx = c->C[cb][0];
-      a.I1wy = c->C[cb][1];
-      a.rho = c->C[cb][2];
-      double error = DBL_MAX;
-      double prevError = 0.0;
-      int n = 0;
-      while (error > scaledEps && n < prm.iterations) {
-        int k = 0;
-        bool calc_end = false;
-        double prev_sim = prevError;
-        const int kmax = exact_div ? 1 : roll_ok ? kRollMax : kTbMax;
-        while (k < kmax && n + k < prm.iterations) {
-          const bool calcError = (prm.epsilon > 0) && ((n + k) & 1) && (prev_sim < scaledEps);
-          ++k;
-          if (calcError) {
-            calc_end = true;
-            break;
-          }
-          prev_sim -= scaledEps;
-        }
+    // one iteration pass of k iterations (ending in a check if calc_end) from the buffer sets
+    // (ui, pi) with the constants of set cb; witer: the warp's first pass as k_warp_iter
+    // (storing the constants if store_c).  gate: a speculative launch
+    auto launch_pass = [&](int k, bool calc_end, bool witer, bool store_c, int ui, int pi, int cb,
+                           bool p_zero, const unsigned long long *gate, unsigned long long gseq,
+                           int wp, int n, int &blocks_out) -> tvl1_status {
         a.u1s = c->U[ui][0]; a.u2s = c->U[ui][1]; a.u3s = c->U[ui][2];
         a.u1d = c->U[ui ^ 1][0]; a.u2d = c->U[ui ^ 1][1]; a.u3d = c->U[ui ^ 1][2];
         a.p11s = c->Pd[pi][0]; a.p12s = c->Pd[pi][1]; a.p21s = c->Pd[pi][2];
@@ -819,13 +826,18 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
         a.p22d = c->Pd[pi ^ 1][3]; a.p31d = c->Pd[pi ^ 1][4]; a.p32d = c->Pd[pi ^ 1][5];
         a.calc_err = calc_end ? 1 : 0;
         a.p_zero = p_zero ? 1 : 0;
+        a.I1wx = c->C[cb][0];
+        a.I1wy = c->C[cb][1];
+        a.rho = c->C[cb][2];
+        a.gate = gate;
+        a.gate_seq = gseq;
         int blocks = nblk;
-        tk = prof_begin(c, st);
+        const size_t tkp = prof_begin(c, st);
         double hbm;
         const int nu = gam ? 3 : 2, np = gam ? 6 : 4;
         const double ld_planes = 3 + nu + (p_zero ? 0 : np), st_planes = nu + np;
         double alg_extra = 0.0;   // the fused warpBackward's algorithmic bytes
-        if (fuse && n == 0 && k == 2 && calc_end) {
+        if (witer) {
           WarpIterArgs w;
           w.ra.b = roll_bufs(s, ui, pi, cb);
           w.ra.it = a;
@@ -837,8 +849,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           // the constants go to HBM only when the warp may run further passes: always for
           // a level's first warp, else when the previous warp did not stop at its first
           // check (a wrong guess recomputes them with the warp kernel after the check)
-          w.store_c = wp == 0 || last_warp_n != 2;
-          fused_nostore = !w.store_c;
+          w.store_c = store_c ? 1 : 0;
           constexpr int M = 6, BW = 128;
           w.ra.bands = (lw + BW - 5) / (BW - 4);
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
@@ -953,33 +964,270 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
         }
         // algorithmic: 64 B/px per executed iteration (+ 40 B/px for a
         // fused warpBackward)
-        prof_end(c, st, tk, 0, Nl * 64.0 * k + alg_extra, hbm);
+        prof_end(c, st, tkp, 0, Nl * 64.0 * k + alg_extra, hbm);
         DIAG(c, st, "iteration pass", s, wp, n);
-        p_zero = false;
-        ui ^= 1;
-        pi ^= 1;
-        n += k;
-        if (calc_end) {
-          // the residual lands in coherent host memory (no copy launch); the event below
-          // orders the host's read after the kernel
-          TRY(read_residual(c, st, blocks, &error));   // the cuda::sum -> host read
-          prevError = error;
-          ++checks;
-          const bool ends = !(error > scaledEps && n < prm.iterations);
-          // k_warp_iter guessed that this warp stops here; it continues: compute its
-          // constants (from its input u, the set the pass just read) before the next pass
-          if (fused_nostore && !ends) TRY(gather(s, ui ^ 1, cb, wp));
-          fused_nostore = false;
-        } else {
-          error = DBL_MAX;
-          prevError = prev_sim;
+        blocks_out = blocks;
+        return TVL1_OK;
+    };
+
+    // warpBackward fused into the warp's first pass (2 iterations ending in the first
+    // check) when that pass would stream through k_iterate_roll anyway
+    const bool fuse = c->fuse && !gam && !exact_div && roll_ok && prm.epsilon > 0 &&
+                      prm.iterations >= 2 && (long)lw * lh >= c->fuse_min;
+    const int kmax = exact_div ? 1 : roll_ok ? kRollMax : kTbMax;
+    // Speculation: behind each residual check the host enqueues the launch it
+    // expects to follow, gated on the device by the check's own evaluation of the stopping
+    // rule, and only then waits for the residual.  A right guess hides the host round trip;
+    // a wrong one costs an empty launch, and the host enqueues the right work as before.
+    const bool spec_ok = c->spec && !exact_div && roll_ok && prm.epsilon > 0;
+    const bool spec_stop_ok = spec_ok && !median && prm.iterations >= 2;
+    // Guesses.  A warp's residual (in units of eps^2 W H) after its first check falls steadily,
+    // so: the action the level's previous warp took at the same iteration count; else the
+    // next residual extrapolated from the last two (the check after a long run of unchecked
+    // iterations comes where the schedule's linear model crosses 1: guess a stop); a level's
+    // first warp starts where the previous level's did.
+    struct Hist {
+      double r0 = -1.0, r1 = -1.0;   // the warp's last two residuals / (eps^2 W H); < 0: none
+      int n0 = -1, n_last = -1;      // iteration counts at those checks
+    };
+    // the residual expected at the check after one at n (the warp's history up to that check)
+    auto extrapolate = [&](const Hist &h, int n, int wp) {
+      if (h.r1 < 0) return wp == 0 ? w0_hint : 1.5;
+      if (n - h.n_last > 2) return 0.9;   // a long unchecked run ends near the model's crossing
+      if (h.r0 >= 0 && h.n_last - h.n0 == 2) return h.r1 * (h.r1 / h.r0);   // steady decay
+      return h.n_last == 2 ? h.r1 * 0.6 : h.r1 * 0.93;   // after a warp's first check: a drop
+    };
+    std::vector<int> act_prev(prm.iterations + 1, -2), act_cur(prm.iterations + 1, -2);
+    auto act_of = [&](double e, int n) {   // 0: stop, else k << 1 | calc_end
+      if (!(e > scaledEps && n < prm.iterations)) return 0;
+      bool ce;
+      double pe;
+      return sched_after(e, scaledEps, n, prm.iterations, kmax, 1, &ce, &pe) << 1 | (ce ? 1 : 0);
+    };
+    // what to predict after a check at iteration count n of warp wp: pk = 0 the warp stops
+    // (its successor's first pass follows), pk > 0 it continues with (pk, pcalc), -1 nothing
+    auto predict = [&](int wp, int n, bool nostore, int last_n, const Hist &h,
+                       const std::vector<int> *prevw, int &pk, int &pcalc) {
+      pk = -1;
+      pcalc = 0;
+      if (!spec_ok) return;
+      if (c->spec == 1 && g_solving[c->device & 63].load(std::memory_order_relaxed) > 1) return;
+      const bool can_stop = spec_stop_ok && wp + 1 < prm.warps;
+      const bool can_cont = !nostore && n < prm.iterations;
+      if (can_stop && (n >= prm.iterations || (n == 2 && last_n == 2))) {
+        pk = 0;
+        return;
+      }
+      const int ap = prevw && wp >= 2 && n < (int)prevw->size() ? (*prevw)[n] : -2;
+      if (ap == 0 && can_stop) {
+        pk = 0;
+        return;
+      }
+      if (ap > 0 && can_cont) {
+        pk = ap >> 1;
+        pcalc = ap & 1;
+        return;
+      }
+      const double r = extrapolate(h, n, wp);
+      if (r <= 1.0 && can_stop) {
+        pk = 0;
+      } else if (can_cont) {
+        const int a = act_of(std::max(r, 1.0 + 1e-9) * scaledEps, n);
+        pk = a >> 1;
+        pcalc = a & 1;
+      } else if (can_stop) {
+        pk = 0;
+      }
+    };
+    auto gate_of = [&](int wp, int n, int pk, int pcalc, unsigned long long gin_seq, bool gated) {
+      CheckGate gt{};
+      if (gated) {
+        gt.in = c->gate;
+        gt.in_seq = gin_seq;
+      }
+      if (pk >= 0) {
+        gt.out = c->gate;
+        gt.thr = scaledEps;
+        gt.n = n;
+        gt.iters = prm.iterations;
+        gt.kmax = kmax;
+        gt.eps_pos = 1;
+        gt.pk = pk;
+        gt.pcalc = pcalc;
+      }
+      (void)wp;
+      return gt;
+    };
+
+    int last_warp_n = -1;   // iterations of the level's previous warp
+    // a warp whose first pass (and check) the previous warp enqueued speculatively
+    bool pre = false;
+    bool pre_nostore = false;
+    unsigned long long pre_seq = 0;
+    int pre_pk = -1, pre_pcalc = 0;
+    for (int wp = 0; wp < prm.warps; ++wp) {
+      bool fused_nostore = false;   // k_warp_iter ran without storing the constants
+      double error = DBL_MAX;
+      double prevError = 0.0;
+      int n = 0;
+      // a check enqueued but not yet read: its sequence number and prediction
+      bool pending = false;
+      unsigned long long pend_seq = 0;
+      int pend_pk = -1, pend_pcalc = 0;
+      Hist h;
+      if (pre) {
+        n = 2;
+        fused_nostore = pre_nostore;
+        pending = true;
+        pend_seq = pre_seq;
+        pend_pk = pre_pk;
+        pend_pcalc = pre_pcalc;
+        pre = false;
+      } else {
+        if (median) {
+          hipLaunchKernelGGL(k_median, grid2(lw, lh, 2), kBlk2, 0, st, c->U[ui][0], c->U[ui][1],
+                             lw, lh, P, prm.median_filtering, c->U[ui ^ 1][0], c->U[ui ^ 1][1]);
+          if (gam) {
+            const size_t n = (size_t)P * lh * sizeof(float);
+            HIP_TRY(c, hipMemcpyAsync(c->U[ui ^ 1][2], c->U[ui][2], n, hipMemcpyDeviceToDevice, st));
+          }
+          ui ^= 1;
         }
+        if (!fuse) TRY(gather(s, ui, cb, wp));
+      }
+      a.I1wx = c->C[cb][0];
+      a.I1wy = c->C[cb][1];
+      a.rho = c->C[cb][2];
+      bool next_pre = false;   // this warp stopped where predicted: the next warp has begun
+      while (pending || (error > scaledEps && n < prm.iterations)) {
+        if (!pending) {
+          bool calc_end = false;
+          double prev_sim = prevError;
+          const int k = sched_after(prevError, scaledEps, n, prm.iterations, kmax,
+                                    prm.epsilon > 0, &calc_end, &prev_sim);
+          const bool witer = fuse && n == 0 && k == 2 && calc_end;
+          // the constants go to HBM only when the warp may run further passes: always for
+          // a level's first warp, else when the previous warp did not stop at its first
+          // check (a wrong guess recomputes them with the warp kernel after the check)
+          const bool store_c = wp == 0 || last_warp_n != 2;
+          int blocks = 0;
+          TRY(launch_pass(k, calc_end, witer, store_c, ui, pi, cb, p_zero, nullptr, 0, wp, n, blocks));
+          if (witer) fused_nostore = !store_c;
+          p_zero = false;
+          ui ^= 1;
+          pi ^= 1;
+          n += k;
+          if (!calc_end) {
+            error = DBL_MAX;
+            prevError = prev_sim;
+            continue;
+          }
+          predict(wp, n, fused_nostore, last_warp_n, h, &act_prev, pend_pk, pend_pcalc);
+          TRY(launch_check(c, st, blocks, gate_of(wp, n, pend_pk, pend_pcalc, 0, false), &pend_seq));
+        }
+        pending = false;
+        // the predicted launch(es) behind the check, gated on it
+        const int sp_pk = pend_pk, sp_pcalc = pend_pcalc;
+        const size_t marks0 = c->marks.size(), ev0 = c->ev_used;
+        const unsigned long long seq0 = c->check_seq;
+        unsigned long long sp_seq = 0;   // the speculative launch's own check
+        int sp_pk2 = -1, sp_pcalc2 = 0;
+        bool sp_nostore = false;
+        if (sp_pk == 0) {   // the next warp's first pass and check
+          const int w2 = wp + 1, cb2 = cb ^ 1;
+          const bool store2 = n != 2;   // k_warp_iter's store rule, if this warp stops here
+          int blocks = 0;
+          // the gather is not gated (a gate check costs k_warp_ring 34 VGPRs): after a wrong
+          // guess it has only filled the constants set the next warp recomputes anyway
+          if (!fuse) TRY(gather(s, ui, cb2, w2));
+          TRY(launch_pass(2, true, fuse, store2, ui, pi, cb2, false, c->gate, pend_seq, w2, 0, blocks));
+          sp_nostore = fuse && !store2;
+          act_cur[n] = 0;   // (as guessed; the real action is recorded after the read)
+          predict(w2, 2, sp_nostore, n, Hist{}, &act_cur, sp_pk2, sp_pcalc2);
+          TRY(launch_check(c, st, blocks, gate_of(w2, 2, sp_pk2, sp_pcalc2, pend_seq, true), &sp_seq));
+        } else if (sp_pk > 0) {   // this warp's next pass
+          int blocks = 0;
+          TRY(launch_pass(sp_pk, sp_pcalc != 0, false, false, ui, pi, cb, false, c->gate, pend_seq,
+                          wp, n, blocks));
+          if (sp_pcalc) {
+            Hist h2;   // with check j's residual extrapolated
+            h2.r0 = h.r1;
+            h2.n0 = h.n_last;
+            h2.r1 = h.r1 < 0 ? -1.0 : extrapolate(h, n, wp);
+            h2.n_last = n;
+            predict(wp, n + sp_pk, false, last_warp_n, h2, &act_prev, sp_pk2, sp_pcalc2);
+            TRY(launch_check(c, st, blocks, gate_of(wp, n + sp_pk, sp_pk2, sp_pcalc2, pend_seq, true),
+                             &sp_seq));
+          }
+        }
+        TRY(wait_check(c, st, pend_seq, &error));   // the cuda::sum -> host read
+        prevError = error;
+        ++checks;
+        const bool ends = !(error > scaledEps && n < prm.iterations);
+        if (wp == 0 && h.r1 < 0) w0_hint = error / scaledEps;
+        h.r0 = h.r1;
+        h.n0 = h.n_last;
+        h.r1 = error / scaledEps;
+        h.n_last = n;
+        act_cur[n] = act_of(error, n);
+        bool right = false;
+        double sp_prev = 0.0;
+        if (sp_pk == 0) {
+          right = ends;
+        } else if (sp_pk > 0 && !ends) {
+          bool ce;
+          right = sched_after(error, scaledEps, n, prm.iterations, kmax, 1, &ce, &sp_prev) == sp_pk &&
+                  (int)ce == sp_pcalc;
+        }
+        if (c->spec_trace)
+          fprintf(stderr, "spec level %d warp %d n %d E/thr %.3f guess %d/%d %s\n", s, wp, n,
+                  error / scaledEps, sp_pk, sp_pcalc, sp_pk < 0 ? "-" : right ? "hit" : "miss");
+        if (sp_pk >= 0 && !right) {   // the gated launches ran empty: forget them
+          ++spec_misses;
+          c->marks.resize(marks0);
+          c->ev_used = ev0;
+          c->check_seq = seq0;
+        }
+        if (right && sp_pk == 0) {   // the next warp's first pass is done, its check pending
+          ui ^= 1;
+          pi ^= 1;
+          p_zero = false;
+          next_pre = true;
+          pre_nostore = sp_nostore;
+          pre_seq = sp_seq;
+          pre_pk = sp_pk2;
+          pre_pcalc = sp_pcalc2;
+          break;
+        }
+        if (right) {   // the warp's next pass is done
+          p_zero = false;
+          ui ^= 1;
+          pi ^= 1;
+          n += sp_pk;
+          if (sp_pcalc) {
+            pending = true;
+            pend_seq = sp_seq;
+            pend_pk = sp_pk2;
+            pend_pcalc = sp_pcalc2;
+          } else {
+            error = DBL_MAX;
+            prevError = sp_prev;
+          }
+          continue;
+        }
+        // k_warp_iter guessed that this warp stops here; it continues: compute its
+        // constants (from its input u, the set the pass just read) before the next pass
+        if (fused_nostore && !ends) TRY(gather(s, ui ^ 1, cb, wp));
+        fused_nostore = false;
       }
       level_iters[s] += n;
       last_warp_n = n;
       if (stats && stats->warp_iterations && s * prm.warps + wp < stats->warp_iterations_capacity)
         stats->warp_iterations[s * prm.warps + wp] = n;
       cb ^= 1;  // every warp gets the other constants buffer
+      pre = next_pre;
+      act_prev.swap(act_cur);
+      std::fill(act_cur.begin(), act_cur.end(), -2);
     }
     HIP_TRY(c, hipGetLastError());
     if (s == 0) break;
@@ -1026,7 +1274,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     }
     stats->iterations_total = tot;
     stats->checks_total = checks;
-    stats->speculation_misses = 0;
+    stats->speculation_misses = spec_misses;
     stats->algorithmic_bytes = survey_bytes(g, prm.warps, level_iters);
   }
   return TVL1_OK;
@@ -1212,7 +1460,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
 #undef KB_WITER
         hipLaunchKernelGGL(kb_reduce, dim3(n), dim3(kBlock), 0, st, c->bpartials, wi.w.ra.waves,
                            all, c->pinned_dev + 8);
-        HIP_TRY(c, hipEventRecord(c->ev_check, st));
+        HIP_TRY(c, hipEventRecord(c->ev_check[0], st));
       } else {   // k_warp_ring's streaming LDS-ring gather, per pair
         BatchRing br{};
         br.wa.W = lw;
@@ -1244,7 +1492,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         nact += act[b];
       }
       if (fuse) {   // the fused first pass: n = 0 (no check), n = 1 (check)
-        HIP_TRY(c, hipEventSynchronize(c->ev_check));
+        HIP_TRY(c, hipEventSynchronize(c->ev_check[0]));
         nact = 0;
         for (int b = 0; b < n; ++b) {
           nit[b] = 2;
@@ -1345,8 +1593,8 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         if (chk.n > 0) {
           hipLaunchKernelGGL(kb_reduce, dim3(chk.n), dim3(kBlock), 0, st, c->bpartials, blocks,
                              chk, c->pinned_dev + 8);
-          HIP_TRY(c, hipEventRecord(c->ev_check, st));
-          HIP_TRY(c, hipEventSynchronize(c->ev_check));
+          HIP_TRY(c, hipEventRecord(c->ev_check[0], st));
+          HIP_TRY(c, hipEventSynchronize(c->ev_check[0]));
           for (int j = 0; j < chk.n; ++j) {
             const int b = chk.idx[j];
             err[b] = c->pinned[8 + b];
@@ -1683,6 +1931,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_ROLL_PX4_MIN")) c->roll_px4_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_POLL")) c->poll = atoi(m);
+  if (const char *m = getenv("TVL1_SPEC")) c->spec = atoi(m);
+  if (const char *m = getenv("TVL1_SPEC_TRACE")) c->spec_trace = atoi(m);
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
   if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
@@ -1694,7 +1944,10 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
       hipHostMalloc((void **)&c->pinned, sizeof(double) * (8 + kBatchMax),
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&c->pinned_dev, c->pinned, 0) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_check, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_check[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_check[1], hipEventDisableTiming) != hipSuccess ||
+      hipMalloc((void **)&c->gate, 256) != hipSuccess ||
+      hipMemset(c->gate, 0, 256) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return set_err(nullptr, TVL1_EHIP, "HIP initialisation failed on device %d", device);
@@ -2075,7 +2328,9 @@ void tvl1_destroy(tvl1_ctx *c) {
   if (c->align_pat) (void)hipFree(c->align_pat);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-  if (c->ev_check) (void)hipEventDestroy(c->ev_check);
+  for (hipEvent_t e : c->ev_check)
+    if (e) (void)hipEventDestroy(e);
+  if (c->gate) (void)hipFree(c->gate);
   if (c->ev_order) (void)hipEventDestroy(c->ev_order);
   delete c;
 }

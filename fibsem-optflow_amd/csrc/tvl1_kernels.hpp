@@ -540,6 +540,11 @@ __device__ __forceinline__ void lds_barrier() {
 // exact formula at the clamped slot coordinate (the texture-clamp value of the gradient
 // image), so there is no G plane: HBM per px and warp is I1 (4 B x 1 + 2M/64) + u1, u2,
 // I0 + the three outputs, instead of 16 B of G.  Taps are 2-cycle ds_read_b32s.
+// true when a speculative launch's prediction failed: every wave of the grid returns at once
+__device__ __forceinline__ bool gated_off(const unsigned long long *gate, unsigned long long seq) {
+  return gate != nullptr && *gate != seq;   // a uniform load at entry (written by an earlier launch)
+}
+
 struct WarpRingArgs {
   const float *I0, *I1;
   const float *u1, *u2;
@@ -832,7 +837,12 @@ struct IterArgs {
   int segs, strip_rows;
   float l_t, theta, gamma, taut;
   int calc_err, p_zero;
+  // speculation gate: a launch enqueued behind a residual check runs only if
+  // that check's k_reduce found the predicted schedule (*gate == gate_seq); null: always
+  const unsigned long long *gate;
+  unsigned long long gate_seq;
 };
+
 
 template <bool G, int PX = 4>
 struct Row {
@@ -1417,6 +1427,7 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
   constexpr int NPL = G ? 6 : 4;                 // LDS planes
   __shared__ typename VecT<PX>::type lds[NPL * RH * LPR];
   const IterArgs &a = t.it;
+  if (gated_off(a.gate, a.gate_seq)) return;   // whole grid
   const int tid = threadIdx.x;
   const int c4 = tid % LPR;
   const int rr = tid / LPR;
@@ -1790,7 +1801,7 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
   // wave-uniform (scalar) band / segment
   const int wid =
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
-  if (wid >= ra.waves) return;                       // whole wavefronts only
+  if (wid >= ra.waves || gated_off(ra.it.gate, ra.it.gate_seq)) return;   // whole wavefronts
   roll_body<G, K, PX, FM>(ra, wid);
 }
 
@@ -2105,7 +2116,7 @@ __global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
   __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, BW>()];
   __shared__ float cring[2 * 5 * BW];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
-  if (wid >= w.ra.waves) return;   // whole blocks
+  if (wid >= w.ra.waves || gated_off(w.ra.it.gate, w.ra.it.gate_seq)) return;   // whole blocks
   warp_iter_body<M, FM, BW, PRIO>(w, wid, ring, cring);
 }
 
@@ -2113,8 +2124,46 @@ __global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
 // The residual goes to coherent host memory; with seq_out set, the check's sequence number
 // follows it there (after a system-scope fence), so the host can poll for it instead of
 // waiting on an event.
+//
+// Speculation.  A check enqueued behind an earlier one runs only if that
+// check's prediction held (g.in: *g.in == g.in_seq).  With g.out set, the reduce also
+// evaluates the stopping rule for the launch enqueued behind it, exactly as the host does
+// (engine: procOneScale's loop, in double), and writes its own sequence number to *g.out if
+// the predicted next step is the one the host will take, 0 otherwise.  Predictions: pk = 0,
+// the warp stops here; pk > 0, it continues with a pass of pk iterations ending in a check
+// (pcalc) or not.
+struct CheckGate {
+  const unsigned long long *in;
+  unsigned long long in_seq;
+  unsigned long long *out;
+  double thr;         // eps^2 * W * H
+  int n, iters, kmax, eps_pos;
+  int pk, pcalc;
+};
+
+// procOneScale's schedule from a residual: iterations up to and including the next check
+// (the host's copy is sched_after in tvl1_engine.hip; the same double operations)
+__host__ __device__ inline int sched_after(double prev, double thr, int n, int iters, int kmax,
+                                           int eps_pos, bool *calc_end, double *prev_end) {
+  int k = 0;
+  bool ce = false;
+  while (k < kmax && n + k < iters) {
+    const bool calc = eps_pos && ((n + k) & 1) && prev < thr;
+    ++k;
+    if (calc) {
+      ce = true;
+      break;
+    }
+    prev -= thr;
+  }
+  *calc_end = ce;
+  *prev_end = prev;
+  return k;
+}
+
 __global__ void k_reduce(const double *__restrict__ partials, int n, double *__restrict__ out,
-                         unsigned long long *seq_out, unsigned long long seq) {
+                         unsigned long long *seq_out, unsigned long long seq, CheckGate g) {
+  if (gated_off(g.in, g.in_seq)) return;
   __shared__ double s[kBlock];
   double acc = 0.0;
   for (int i = threadIdx.x; i < n; i += kBlock) acc += partials[i];
@@ -2125,7 +2174,19 @@ __global__ void k_reduce(const double *__restrict__ partials, int n, double *__r
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    out[0] = s[0];
+    const double e = s[0];
+    out[0] = e;
+    if (g.out) {
+      const bool ends = !(e > g.thr && g.n < g.iters);
+      bool ok = ends;
+      if (g.pk > 0) {
+        bool ce;
+        double pe;
+        const int k = sched_after(e, g.thr, g.n, g.iters, g.kmax, g.eps_pos, &ce, &pe);
+        ok = !ends && k == g.pk && (int)ce == g.pcalc;
+      }
+      *g.out = ok ? seq : 0ull;
+    }
     if (seq_out) {
       __threadfence_system();
       *(volatile unsigned long long *)seq_out = seq;

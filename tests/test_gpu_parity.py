@@ -106,9 +106,11 @@ MODES = ["", "TVL1_ROLL_LONG_MIN=0", "TVL1_ROLL_LONG_MIN=0,TVL1_ROLL_SEG=8", "TV
          "TVL1_ROLL_SEG=64", "TVL1_ROLL_PX4_MIN=0", "TVL1_ROLL_PX4_MIN=0,TVL1_ROLL_SEG=8",
          "TVL1_FUSE_MIN=0", "TVL1_FUSE_MIN=0,TVL1_ROLL_SEG=8", "TVL1_FUSE_MIN=0,TVL1_ROLL_PX4_MIN=0",
          "TVL1_FUSE=0,TVL1_ROLL_LONG_MIN=0", "TVL1_BUF_LIMIT=100000", "TVL1_BUF_LIMIT=0",
-         "TVL1_POLL=0"]   # (the last: residuals read after an event instead of the poll)
+         "TVL1_POLL=0", "TVL1_POLL=0,TVL1_FUSE_MIN=0", "TVL1_SPEC=0", "TVL1_SPEC=0,TVL1_FUSE_MIN=0"]
+# (TVL1_POLL=0: residuals read after an event instead of the poll; TVL1_SPEC=0: nothing
+# enqueued behind a check before the host reads it)
 KNOBS = ("TVL1_ROLL_SEG", "TVL1_ROLL_PX4_MIN", "TVL1_ROLL_LONG_MIN", "TVL1_FUSE", "TVL1_FUSE_MIN",
-         "TVL1_BUF_LIMIT", "TVL1_BATCH_FUSE", "TVL1_POLL")
+         "TVL1_BUF_LIMIT", "TVL1_BATCH_FUSE", "TVL1_POLL", "TVL1_SPEC")
 CONFIG_CASES = [
     (250, 131, 21, dict(nscales=5, warps=5)),
     (97, 201, 22, dict(nscales=4, warps=3, gamma=0.1)),
@@ -155,6 +157,35 @@ def test_fma_mode_bit_identical(built, monkeypatch, env, W, H, seed, kw):
     assert bits_equal(u, ur) and bits_equal(v, vr)
     ui, vi, _, _ = checker.oracle_calc(I0, I1, capi.make_params(**kw))
     assert not (bits_equal(u, ui) and bits_equal(v, vi)), "fma mode computed the IEEE result"
+
+
+# Speculation: launches enqueued behind a residual check, gated on the device by
+# that check's own evaluation of the stopping rule.  Same bits, iterations and checks as with
+# nothing enqueued ahead; the guesses are mostly right.
+@pytest.mark.parametrize("env", ["", "TVL1_FUSE_MIN=0", "TVL1_POLL=0,TVL1_FUSE_MIN=0",
+                                 "TVL1_FUSE_MIN=0,TVL1_ROLL_LONG_MIN=0"])
+@pytest.mark.parametrize("W,H,seed,kw", [(320, 240, 31, dict(nscales=4, warps=10)),
+                                         (256, 200, 32, dict(nscales=3, warps=6, epsilon=0.002)),
+                                         (200, 150, 33, dict(nscales=3, warps=4, gamma=0.2))])
+def test_speculation_same_schedule(built, monkeypatch, env, W, H, seed, kw):
+    p = capi.make_params(**kw)
+    I0, I1 = synth.gen_pair(W, H, seed=seed)
+    res = {}
+    for spec in ("1", "0"):
+        set_knobs(monkeypatch, env + ",TVL1_SPEC=" + spec)
+        eng = capi.Engine(p)
+        res[spec] = eng.calc_host(I0, I1)
+        eng.close()
+    (u, v, st, wi), (u0, v0, st0, wi0) = res["1"], res["0"]
+    np.testing.assert_array_equal(wi, wi0)
+    assert bits_equal(u, u0) and bits_equal(v, v0)
+    assert st["checks_total"] == st0["checks_total"]
+    assert st0["speculation_misses"] == 0
+    print(f"checks {st['checks_total']} misses {st['speculation_misses']}")
+    assert st["speculation_misses"] < st["checks_total"]
+    ur, vr, _, wr = checker.oracle_calc(I0, I1, p)
+    np.testing.assert_array_equal(wi, wr)
+    assert bits_equal(u, ur) and bits_equal(v, vr)
 
 
 GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
