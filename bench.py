@@ -450,7 +450,7 @@ def main():
     for j in range(F):
         I0h, I1h = synth.gen_pair(W, H, seed=0x5EED, z=1 + rank * F + j)
         eng = capi.Engine(params, device=local_rank)
-        eng.set_profiling(not args.no_kernel_timing)
+        eng.set_profiling(False)   # no per-launch events in the timed steps (they cost time)
         # F == 1: torch's current stream; F > 1: each ctx on its own non-blocking stream
         st = eng.stream if F > 1 else torch.cuda.current_stream(dev).cuda_stream
         slots.append(dict(I0h=I0h, I1h=I1h, eng=eng, stream=st,
@@ -500,14 +500,22 @@ def main():
 
     elapsed, stats = timed(args.warmup, args.steps)
     I0h, I1h = slots[0]["I0h"], slots[0]["I1h"]
-    # one extra solve alone on the GPU (not timed): clean per-kernel durations, no
-    # interleaving with the other in-flight pair
+    # one pair alone on the GPU, twice (not timed): with HIP events around every launch for
+    # clean per-kernel-class durations (the roofline; no interleaving with other pairs), then
+    # without them for the wall time -- the events themselves cost ~2.7 ms per C2 pair
+    iso = None
+    single_pair_instr_ms = None
+    if not args.no_kernel_timing:
+        slots[0]["eng"].set_profiling(True)
+        t_iso = time.perf_counter()
+        iso = solve(slots[0])
+        torch.cuda.synchronize(dev)
+        single_pair_instr_ms = 1e3 * (time.perf_counter() - t_iso)
+        slots[0]["eng"].set_profiling(False)
     t_iso = time.perf_counter()
-    iso = solve(slots[0])
+    solve(slots[0])
     torch.cuda.synchronize(dev)
     single_pair_ms = 1e3 * (time.perf_counter() - t_iso)
-    if F == 1 or args.no_kernel_timing:
-        iso = None
 
     # secondary measurement in the other math mode (same pairs, same K): the IEEE run is
     # the headline unless --fast-math; its flow is the reference for the EPE figures
@@ -543,12 +551,7 @@ def main():
                                        "max": float(e.max())}}
 
     # aggregate per-kernel timing of this rank (rank 0 reports its own kernel roofline)
-    k_ms = sum(s["kernel_ms"][0] for s in stats)
-    k_bytes = sum(s["kernel_bytes"][0] for s in stats)
-    k_launch = sum(s["kernel_launches"][0] for s in stats)
-    k_hbm = sum(s["kernel_hbm_bytes"][0] for s in stats)
     pair_bytes = sum(s["algorithmic_bytes"] for s in stats) / len(stats)
-    cls_ms = [sum(s["kernel_ms"][i] for s in stats) / args.steps for i in range(3)]
     iters = [s["iterations_total"] for s in stats]
 
     # the production workload beside the C2 headline, every rank taking part
@@ -607,15 +610,6 @@ def main():
         roof = roofline(src["kernel_bytes"][0], src["kernel_hbm_bytes"][0], src["kernel_ms"][0],
                         src["kernel_launches"][0])
         roof["timing"] = "one pair alone on the GPU (the isolated solve after the timed steps)"
-    elif F == 1 and k_ms > 0:
-        roof = roofline(k_bytes, k_hbm, k_ms, k_launch)
-        roof["timing"] = "every iteration-pass launch of the timed steps (one stream)"
-    roof_inflight = None
-    if F > 1 and k_ms > 0:
-        roof_inflight = roofline(k_bytes, k_hbm, k_ms, k_launch)
-        roof_inflight["note"] = (f"{F} pairs in flight: launch durations overlap the other "
-                                 f"stream's kernels (busy share {k_ms / (1e3 * elapsed):.2f}), so "
-                                 f"this understates per-launch bandwidth")
     out = {
         "metric": METRIC,
         "value": round(value, 4),
@@ -625,6 +619,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "single_pair_ms": round(single_pair_ms, 3),
+        "single_pair_ms_with_events": None if single_pair_instr_ms is None else round(single_pair_instr_ms, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -652,17 +647,14 @@ def main():
             "pair_roofline_frac": round(pair_bytes * args.steps * F / elapsed / 1e9 / HBM_PEAK_GBS, 4),
         },
         "roofline": roof,
-        "roofline_inflight": roof_inflight,
         # per-pair breakdown of one solve alone on the GPU (F > 1: the isolated solve;
         # F == 1: the timed steps)
-        "pair_breakdown_ms": None if k_ms <= 0 else (
+        # kernel classes from the instrumented solve, host syncs and gaps against the wall
+        # time of the uninstrumented one
+        "pair_breakdown_ms": None if iso is None else
             {"iterate": round(iso["kernel_ms"][0], 2), "warp": round(iso["kernel_ms"][1], 2),
              "other_kernels": round(iso["kernel_ms"][2], 2),
-             "host_sync_and_gaps": round(single_pair_ms - sum(iso["kernel_ms"][:3]), 2)}
-            if iso is not None else
-            {"iterate": round(cls_ms[0], 2), "warp": round(cls_ms[1], 2),
-             "other_kernels": round(cls_ms[2], 2),
-             "host_sync_and_gaps": round(ms_per_step - sum(cls_ms), 2)}),
+             "host_sync_and_gaps": round(single_pair_ms - sum(iso["kernel_ms"][:3]), 2)},
         "cpu_baseline": None,
         "math_modes": modes,
         "production_strips": strips,
