@@ -18,19 +18,25 @@ def _bench(name):
     return json.loads(Path(PROF / "r2" / name).read_text().splitlines()[-1])
 
 
-@pytest.mark.parametrize("stats,bench", [("kernel_stats_single_pair_prio.csv", "bench_c2_final.json")])
-def test_roofline_frac_matches_rocprof_and_pmc(stats, bench):
-    traffic = json.loads((PROF / "traffic.json").read_text())
+# (kernel stats of one pair alone, the bench line of the same tree, the PMC traffic record);
+# the last triple is the final r2 engine, and profiles/traffic.json (bench.py's `traffic`) is it
+@pytest.mark.parametrize("stats,bench,traffic", [
+    ("kernel_stats_single_pair_prio.csv", "bench_c2_final.json", "traffic_prio.json"),
+    ("latest/kernel_stats_single_pair.csv", "bench_c2_latest.json", "latest/traffic.json")])
+def test_roofline_frac_matches_rocprof_and_pmc(stats, bench, traffic):
+    traffic = json.loads((PROF / "r2" / traffic).read_text())
     calls = ns = 0.0
     for r in csv.DictReader(open(PROF / "r2" / stats)):
         name = r["Name"].split("(")[0].replace("void ", "").replace("tvl1k::", "")
         if name.startswith(ITER):
             calls += int(r["Calls"])
             ns += float(r["TotalDurationNs"])
-    assert calls == traffic["dispatches"]
+    roof = _bench(bench)["roofline"]
+    # whole solves of the same schedule in both runs (the traced run solves the isolated pair
+    # once more, with events)
+    assert calls % roof["launches"] == 0 and traffic["dispatches"] % roof["launches"] == 0
     avg_us = ns / calls / 1e3
     by_hand = traffic["iterate_hbm_bytes_per_launch"] / (avg_us * 1e-6) / 8e12
-    roof = _bench(bench)["roofline"]
     assert roof["unit"] == "GB/s" and roof["peak"] == 8000.0
     assert abs(roof["frac"] / by_hand - 1) < 0.05, (roof["frac"], by_hand)
     # the engine's live byte accounting against the PMC bytes of the same launches
@@ -38,8 +44,9 @@ def test_roofline_frac_matches_rocprof_and_pmc(stats, bench):
     assert roof["model_bytes_over_peak"] > 1.0 > roof["frac"]   # the SURVEY model is not frac
 
 
-def test_bench_line_carries_the_contract_fields():
-    d = _bench("bench_c2_final.json")
+@pytest.mark.parametrize("bench", ["bench_c2_final.json", "bench_c2_latest.json"])
+def test_bench_line_carries_the_contract_fields(bench):
+    d = _bench(bench)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
               "roofline", "cpu_baseline"):
