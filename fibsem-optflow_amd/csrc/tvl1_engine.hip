@@ -997,7 +997,9 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
       if (h.r0 >= 0 && h.n_last - h.n0 == 2) return h.r1 * (h.r1 / h.r0);   // steady decay
       return h.n_last == 2 ? h.r1 * 0.6 : h.r1 * 0.93;   // after a warp's first check: a drop
     };
-    std::vector<int> act_prev(prm.iterations + 1, -2), act_cur(prm.iterations + 1, -2);
+    // (remembered up to 4096 iterations: a huge `iterations` must not size a huge table)
+    const size_t nact = (size_t)std::min(prm.iterations, 4096) + 1;
+    std::vector<int> act_prev(nact, -2), act_cur(nact, -2);
     auto act_of = [&](double e, int n) {   // 0: stop, else k << 1 | calc_end
       if (!(e > scaledEps && n < prm.iterations)) return 0;
       bool ce;
@@ -1142,7 +1144,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           if (!fuse) TRY(gather(s, ui, cb2, w2));
           TRY(launch_pass(2, true, fuse, store2, ui, pi, cb2, false, c->gate, pend_seq, w2, 0, blocks));
           sp_nostore = fuse && !store2;
-          act_cur[n] = 0;   // (as guessed; the real action is recorded after the read)
+          if ((size_t)n < nact) act_cur[n] = 0;   // (as guessed; recorded after the read)
           predict(w2, 2, sp_nostore, n, Hist{}, &act_cur, sp_pk2, sp_pcalc2);
           TRY(launch_check(c, st, blocks, gate_of(w2, 2, sp_pk2, sp_pcalc2, pend_seq, true), &sp_seq));
         } else if (sp_pk > 0) {   // this warp's next pass
@@ -1169,7 +1171,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
         h.n0 = h.n_last;
         h.r1 = error / scaledEps;
         h.n_last = n;
-        act_cur[n] = act_of(error, n);
+        if ((size_t)n < nact) act_cur[n] = act_of(error, n);
         bool right = false;
         double sp_prev = 0.0;
         if (sp_pk == 0) {
