@@ -14,12 +14,17 @@ torch.distributed (nccl = RCCL) is used only for the start/stop barrier and the
 max-over-ranks reduction of the elapsed time.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
-  roofline: dominant kernel = the fused primal-dual iteration (k_iterate).
-            achieved = its algorithmic bytes (planes each launch must move, see
-            DESIGN.md) / its HIP-event time, summed over every launch in the
-            timed region; peak = 8000 GB/s (MI355X HBM3E spec).
-  cpu_baseline: the oracle (CPU restatement, oracle/) timed on this host on a
-            the benchmark pair itself (one full C2 solve, 10-20 s on the box's cores).
+  roofline: dominant kernel class = the iteration passes (k_iterate_roll, k_iterate_tb
+            and k_warp_iter, warpBackward fused into each warp's first pass).
+            achieved = the bytes those launches move (the engine's live per-launch
+            accounting of its tiling, checked against rocprofv3 PMC bytes: `traffic`)
+            / their average HIP-event launch duration on ONE pair alone, measured after
+            the timed steps (no events inside them); peak = 8000 GB/s (MI355X HBM3E).
+  cpu_baseline: the oracle (CPU restatement, oracle/) timed on this host on the
+            benchmark pair itself (one full C2 solve, 10-20 s on the box's cores),
+            compiled for this host's CPU at bench time when a compiler is present.
+  production_strips: the production ROI-strip workload through
+            tvl1_calc_batch, with its own roofline for the batched iteration class.
 """
 from __future__ import annotations
 
@@ -36,12 +41,12 @@ sys.path.insert(0, str(ROOT / "fibsem-optflow_amd"))
 HBM_PEAK_GBS = 8000.0
 
 
-def _traffic():
+def _traffic(name="traffic.json"):
     """PMC-measured HBM bytes per iteration-pass launch (rocprofv3 FETCH_SIZE x 2 per the
     gfx950 correction + WRITE_SIZE, separate passes, one pair alone: tools/pmc_single.sh +
     tools/pmc_summary.py --emit-traffic) and the class's VALU utilisation, committed under
     profiles/ for the engine build the bench runs.  None if not measured."""
-    p = ROOT / "profiles" / "traffic.json"
+    p = ROOT / "profiles" / name
     try:
         return json.loads(p.read_text())
     except Exception:
@@ -49,10 +54,53 @@ def _traffic():
 
 
 TRAFFIC = _traffic()
+TRAFFIC_STRIPS = _traffic("traffic_strips.json")
 RED_CPU = False   # reductions on CPU tensors (gloo rehearsal, BENCH_DIST_BACKEND=gloo)
+DIST_BACKEND = None   # the torch.distributed backend in use (None: no process group)
 MATH = {0: "IEEE (bit-identical to oracle/)", 1: "fast (CUDA_FAST_MATH semantics)",
         2: "fma (nvcc -fmad=true contraction, IEEE division; bit-identical to oracle/'s fma mode)"}
 METRIC = "slice-pairs/sec (6k×4k, 5 scales, 30 warps) at 1/2/4/8 GPUs; % HBM roofline"
+
+
+PAIR_KERNEL = ("iteration passes: estimateU + estimateDualVariables + residual partials, <= 4 "
+               "iterations per HBM pass (k_iterate_roll wavefront pipeline / k_iterate_tb blocked "
+               "regions; on levels >= 5 Mpx each warp's first pass is k_warp_iter, warpBackward "
+               "fused in)")
+STRIP_KERNEL = ("batched iteration passes of one tvl1_calc_batch call: kb_iterate_roll<K, 2> "
+                "(<= 4 iterations per HBM pass, a pair index per launch) and kb_warp_iter "
+                "(warpBackward fused with each warp's first pass)")
+
+
+def roofline(k_bytes, k_hbm, k_ms, k_launch, traffic, kernel):
+    """The dominant kernel class against HBM: achieved = the bytes these launches must move
+    (the engine's per-launch accounting of its tiling: band loads with halos + interior
+    stores, checked against the rocprofv3 FETCH_SIZE / WRITE_SIZE passes in profiles/, see
+    `traffic`) / their average HIP-event launch time.  SURVEY 8(d)'s one-pass-per-iteration
+    model (64 B/px per iteration) does not describe a temporally blocked kernel (it would
+    exceed the peak), so it is reported beside the fraction as `model_bytes_over_peak`,
+    never as `frac`."""
+    achieved = k_hbm / (k_ms * 1e-3) / 1e9
+    model = k_bytes / (k_ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+         "traffic": traffic.get("iterate_hbm_bytes_per_launch") if traffic else None,
+         "kernel": kernel,
+         "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
+         "bytes_per_launch": round(k_hbm / k_launch),
+         "bytes_basis": "engine accounting of the tiling's compulsory HBM bytes (live)",
+         "model_bytes_per_launch": round(k_bytes / k_launch),
+         "model": "SURVEY 8(d): 64 B/px per executed iteration (+ 40 B/px for a fused "
+                  "warpBackward)",
+         "model_bytes_over_peak": round(model / HBM_PEAK_GBS, 4)}
+    if traffic:
+        r["traffic_source"] = traffic.get("source")
+        r["traffic_over_bytes"] = round(traffic["iterate_hbm_bytes_per_launch"] /
+                                        (k_hbm / k_launch), 4)
+        if traffic.get("iterate_valu_frac") is not None:
+            # SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), same class,
+            # same workload alone (tools/pmc_single.sh + tools/valu_util.py)
+            r["valu_frac"] = traffic["iterate_valu_frac"]
+    return r
 
 
 def parse():
@@ -112,6 +160,47 @@ def parse():
     return args
 
 
+_NATIVE_ORACLE = None
+
+
+def native_oracle():
+    """SURVEY 8(d)'s CPU-baseline recipe: the oracle compiled on the bench host for its own
+    CPU (-O3 -march=native -fopenmp; -ffp-contract=off keeps the float32 operation order,
+    so the bits do not change) into a temp dir.  Falls back to the portable in-tree build
+    (no -march=native: it travels between hosts) when no compiler is present.  Returns
+    (path or None, description of the build)."""
+    global _NATIVE_ORACLE
+    if _NATIVE_ORACLE is not None:
+        return _NATIVE_ORACLE
+    import platform
+    import subprocess
+    import tempfile
+    cpu = platform.processor() or "unknown CPU"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                cpu = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    flags = ["-O3", "-march=native", "-std=c11", "-fPIC", "-fopenmp", "-ffp-contract=off",
+             "-fno-fast-math"]
+    d = Path(tempfile.mkdtemp(prefix="orc_native_"))
+    so = d / "liboracle_tvl1_native.so"
+    src = ROOT / "oracle"
+    try:
+        subprocess.run(["gcc", *flags, "-shared", "-o", str(so), str(src / "tvl1_oracle.c"),
+                        str(src / "tvl1_oracle_dualtvl1.c"), "-lm"], check=True,
+                       capture_output=True, timeout=120)
+        _NATIVE_ORACLE = (str(so), f"gcc {' '.join(flags)} on the bench host ({cpu}, "
+                                   f"{os.cpu_count()} logical CPUs)")
+    except Exception as e:   # no compiler: the portable build
+        _NATIVE_ORACLE = (None, f"portable in-tree build (oracle/Makefile, no -march=native; "
+                                f"host build failed: {type(e).__name__}) on {cpu}, "
+                                f"{os.cpu_count()} logical CPUs")
+    return _NATIVE_ORACLE
+
+
 def cpu_baseline(I0, I1, params, sample: str):
     """Oracle (CPU restatement of OpenCV 3.4.1 CUDA TV-L1) on the benchmark pair itself (or
     a crop of it, extrapolated by pixel count, with --cpu-sample)."""
@@ -122,10 +211,11 @@ def cpu_baseline(I0, I1, params, sample: str):
     sw, sh = min(sw, W), min(sh, H)
     a = np.ascontiguousarray(I0[:sh, :sw])
     b = np.ascontiguousarray(I1[:sh, :sw])
-    lib = checker.load_oracle()
+    so, build = native_oracle()
+    lib = checker.load_oracle(so)
     threads = int(lib.orc_num_threads())
     t0 = time.perf_counter()
-    _, _, st, _ = checker.oracle_calc(a, b, params, warp_iters=False)
+    _, _, st, _ = checker.oracle_calc(a, b, params, warp_iters=False, so=so)
     dt = time.perf_counter() - t0
     scale = (W * H) / float(sw * sh)
     return {
@@ -133,6 +223,7 @@ def cpu_baseline(I0, I1, params, sample: str):
         "unit": "slice-pairs/s",
         "cores": threads,
         "kind": "port",
+        "build": build,
         "sample": ((f"oracle/ CPU restatement, {threads} OpenMP threads, one {sw}x{sh} crop of "
                     f"the benchmark pair, same TV-L1 parameters ({st['iterations_total']} "
                     f"iterations over {st['levels']} levels) in {dt:.2f} s, extrapolated "
@@ -270,6 +361,7 @@ def run_stack(args, rank, world, local_rank, dist):
             "parallelism": (f"{world} rank(s), {F} chunk(s) in flight per GPU, chunks of "
                             f"{args.chunk} pairs from one shared work queue"),
             "step": "the whole stack",
+            "process_group": DIST_BACKEND,
             "pairs": int(pairs_done),
             "iterations_per_pair": round(iters_done / max(1.0, pairs_done), 1),
         },
@@ -334,6 +426,17 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # one batch alone on the GPU after the timed steps, with HIP events around every launch
+    # (tvl1_set_profiling): the batched iteration class's roofline
+    roof = None
+    if not args.no_kernel_timing:
+        slots[0]["eng"].set_profiling(True)
+        s0 = solve(slots[0])[0]
+        slots[0]["eng"].set_profiling(False)
+        if s0["kernel_ms"][0] > 0:
+            roof = roofline(s0["kernel_bytes"][0], s0["kernel_hbm_bytes"][0], s0["kernel_ms"][0],
+                            s0["kernel_launches"][0], TRAFFIC_STRIPS, STRIP_KERNEL)
+            roof["timing"] = f"one batch of {B} strip pairs alone on the GPU, after the timed steps"
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if RED_CPU else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -352,14 +455,15 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
         from oracle import checker   # cpu_baseline leg only
         st0 = slots[0]["stack"]
         a, c = st0[0].cpu().numpy(), st0[1].cpu().numpy()
-        lib = checker.load_oracle()
+        so, build = native_oracle()
+        lib = checker.load_oracle(so)
         t1 = time.perf_counter()
         n_rep = 4
         for _ in range(n_rep):
-            checker.oracle_calc(a, c, params, warp_iters=False)
+            checker.oracle_calc(a, c, params, warp_iters=False, so=so)
         dt = (time.perf_counter() - t1) / n_rep
         cpu = {"value": round(1.0 / dt, 3), "unit": "strip solves/s",
-               "cores": int(lib.orc_num_threads()), "kind": "port",
+               "cores": int(lib.orc_num_threads()), "kind": "port", "build": build,
                "sample": f"oracle/ CPU restatement, {n_rep} solves of one {W}x{H} strip pair"}
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "strip solves/s",
@@ -374,6 +478,7 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
                    "slice_pairs_per_s": round(value / 2, 2),
                    "batch": B, "batches_in_flight_per_gpu": F,
                    "iterations_per_strip": round(iters / (args.steps * F * B), 1)},
+        "roofline": roof,
         "cpu_baseline": cpu,
     }
     if standalone:
@@ -396,6 +501,7 @@ def strips_line(args, rank, world, local_rank, dist):
             "slice_pairs_per_s": o["config"]["slice_pairs_per_s"],
             "ms_per_step": o["ms_per_step"], "batch": a.batch, "batches_in_flight_per_gpu": a.inflight,
             "iterations_per_strip": o["config"]["iterations_per_strip"],
+            "roofline": o["roofline"],
             "cpu_baseline": o["cpu_baseline"],
             "api": "tvl1_calc_batch (DESIGN.md 4.6)"}
 
@@ -417,7 +523,10 @@ def main():
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     if backend == "gloo":
         local_rank = local_rank % max(1, torch.cuda.device_count())
-    if world > 1:
+    # a process group whenever a launcher (torch.distributed.run) set WORLD_SIZE, N = 1
+    # included: the RCCL init, barrier and device-tensor reductions then run on every
+    # torchrun launch, not first on the driver's 8-GPU node (tests/test_gpu_rccl.py)
+    if "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         if backend == "gloo":
@@ -426,8 +535,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(local_rank)
-    global RED_CPU
+    global RED_CPU, DIST_BACKEND
     RED_CPU = backend == "gloo"
+    DIST_BACKEND = dist.get_backend() if dist else None
     if args.workload == "stack":
         return run_stack(args, rank, world, local_rank, dist)
     if args.workload == "strips":
@@ -568,47 +678,13 @@ def main():
 
     value = world * args.steps * F / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
-    def roofline(k_bytes, k_hbm, k_ms, k_launch):
-        """The dominant kernel class (iteration passes, incl. k_warp_iter) against HBM:
-        achieved = the bytes these launches must move (the engine's per-launch accounting of
-        its tiling: tile loads with halos + interior stores, checked against the rocprofv3
-        FETCH_SIZE / WRITE_SIZE pass in profiles/, see `traffic`) / their HIP-event time.
-        SURVEY 8(d)'s one-pass-per-iteration model (64 B/px per iteration) does not describe
-        a temporally blocked kernel (it would exceed the peak), so it is reported beside
-        the fraction as `model_bytes_over_peak`, never as `frac`."""
-        achieved = k_hbm / (k_ms * 1e-3) / 1e9
-        model = k_bytes / (k_ms * 1e-3) / 1e9
-        r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-             "traffic": TRAFFIC.get("iterate_hbm_bytes_per_launch") if TRAFFIC else None,
-             "kernel": "iteration passes: estimateU + estimateDualVariables + residual "
-                       "partials, <= 4 iterations per HBM pass (k_iterate_roll wavefront "
-                       "pipeline / k_iterate_tb blocked regions; on levels >= 5 Mpx each "
-                       "warp's first pass is k_warp_iter, warpBackward fused in)",
-             "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
-             "bytes_per_launch": round(k_hbm / k_launch),
-             "bytes_basis": "engine accounting of the tiling's compulsory HBM bytes (live)",
-             "model_bytes_per_launch": round(k_bytes / k_launch),
-             "model": "SURVEY 8(d): 64 B/px per executed iteration (+ 40 B/px for a fused "
-                      "warpBackward)",
-             "model_bytes_over_peak": round(model / HBM_PEAK_GBS, 4)}
-        if TRAFFIC:
-            r["traffic_source"] = TRAFFIC.get("source")
-            r["traffic_over_bytes"] = round(TRAFFIC["iterate_hbm_bytes_per_launch"] /
-                                            (k_hbm / k_launch), 4)
-            if TRAFFIC.get("iterate_valu_frac") is not None:
-                # SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), same class,
-                # one pair alone (tools/pmc_single.sh + tools/valu_util.py)
-                r["valu_frac"] = TRAFFIC["iterate_valu_frac"]
-        return r
-
     # the roofline is measured on ONE stream: with F > 1 in flight the launch durations
     # interleave with the other pair's kernels, so they come from the isolated solve
     src = iso if iso is not None else None
     roof = None
     if src is not None and src["kernel_ms"][0] > 0:
         roof = roofline(src["kernel_bytes"][0], src["kernel_hbm_bytes"][0], src["kernel_ms"][0],
-                        src["kernel_launches"][0])
+                        src["kernel_launches"][0], TRAFFIC, PAIR_KERNEL)
         roof["timing"] = "one pair alone on the GPU (the isolated solve after the timed steps)"
     out = {
         "metric": METRIC,
@@ -638,6 +714,7 @@ def main():
                           f"{args.median}, epsilon {args.epsilon}")),
             "pair": f"{W}x{H}",
             "parallelism": f"pairs sharded over {world} GPU(s), no data-path collective",
+            "process_group": DIST_BACKEND,
             "pairs_in_flight_per_gpu": F,
             "step": f"one batch of {F} pair(s) solved concurrently per GPU (one ctx + stream each)",
             "iterations_per_pair": iters[0],

@@ -361,14 +361,22 @@ struct PairResult {
   Value stats;
 };
 
+// An engine status that leaves the device context in doubt (a HIP call failed, memory ran
+// out): the pair is retried on a rebuilt context.  TVL1_EINVAL / TVL1_ESIZE are input or
+// config errors (a bad medianFiltering, an ROI the solver rejects): reported like the
+// reference's input errors, without a context rebuild.
+static bool device_fault(tvl1_status s) {
+  return s == TVL1_EHIP || s == TVL1_ENOMEM || s == TVL1_ENODEV;
+}
+
 // solve_wrapper (optflow.cpp:395-496) for one ROI.
 bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1, const Rect &r0,
                    const Rect &r1, Value &im, const Value &args, bool features,
                    const float *affine, PairResult &res, std::string &err) {
   const int W = r0.width, H = r0.height;
   tvl1_params prm = generate_TV_args(im, args);
-  if (tvl1_set_params(dc.ctx, &prm) != TVL1_OK) {
-    err = tvl1_last_error(dc.ctx), dc.faulted = true;
+  if (const tvl1_status s = tvl1_set_params(dc.ctx, &prm); s != TVL1_OK) {
+    err = tvl1_last_error(dc.ctx), dc.faulted = device_fault(s);
     return false;
   }
   const size_t pitch = (size_t)f0.width;  // device frames are packed, pitch = width
@@ -381,7 +389,7 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
   const auto t0 = std::chrono::steady_clock::now();
   tvl1_status s = tvl1_calc(dc.ctx, a, pitch, b, pitch1, W, H, dc.du, dc.dv, fp, &st, dc.stream);
   if (s != TVL1_OK) {
-    err = tvl1_last_error(dc.ctx), dc.faulted = true;
+    err = tvl1_last_error(dc.ctx), dc.faulted = device_fault(s);
     return false;
   }
   const std::string otype = output_type_of(im, args);
@@ -395,7 +403,7 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
   else
     s = tvl1_postprocess(dc.ctx, dc.du, dc.dv, fp, b, pitch1, W, H, mode, dc.stream);
   if (s != TVL1_OK) {
-    err = tvl1_last_error(dc.ctx), dc.faulted = true;
+    err = tvl1_last_error(dc.ctx), dc.faulted = device_fault(s);
     return false;
   }
   const bool sampled = otype == "random_points" && !args.get("debug", false).asBool();
@@ -501,7 +509,7 @@ bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1,
                                       (size_t)f0.width, f0.width, f0.height, &p, affine, &n_good,
                                       &outcome, dc.stream);
   if (s != TVL1_OK) {
-    err = std::string("find_alignment: ") + tvl1_last_error(dc.ctx), dc.faulted = true;
+    err = std::string("find_alignment: ") + tvl1_last_error(dc.ctx), dc.faulted = device_fault(s);
     return false;
   }
   if (args.get("debug", Value(false)).asBool())
@@ -513,7 +521,7 @@ bool align_frame1(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1,
   s = tvl1_warp_affine_u8(dc.ctx, dc.d1, (size_t)w1, w1, h1, dc.dw,
                           (size_t)f0.width, f0.width, f0.height, affine, dc.stream);
   if (s != TVL1_OK) {
-    err = std::string("warpAffine: ") + tvl1_last_error(dc.ctx), dc.faulted = true;
+    err = std::string("warpAffine: ") + tvl1_last_error(dc.ctx), dc.faulted = device_fault(s);
     return false;
   }
   aligned.width = f0.width;

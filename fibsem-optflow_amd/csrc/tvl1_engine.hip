@@ -78,7 +78,12 @@ struct tvl1_ctx {
   int poll = 1;                      // TVL1_POLL: wait for a residual by polling its
                                      // sequence number in host memory (0: event sync)
   hipEvent_t ev_order = nullptr;  // orders work on the caller's stream after a zero fill
-  std::vector<char *> retired;    // arenas outgrown while possibly in use (arena_alloc)
+  struct Retired {                // an arena outgrown while possibly in use (arena_alloc)
+    char *p;
+    std::vector<hipEvent_t> done;   // recorded on every stream the ctx has worked on
+  };
+  std::vector<Retired> retired;
+  std::vector<hipStream_t> streams;   // streams the ctx's work was enqueued on (note_stream)
   // dispatch: the defaults are the measured best; the environment knobs are
   // for tests (named in tests/test_gpu_parity.py) and diagnostics
   int roll_seg = 0;          // TVL1_ROLL_SEG: k_iterate_roll rows per segment (0 = auto)
@@ -251,25 +256,83 @@ static int iterate_blocks(int W, int H) {
 // (Re)allocate one of the ctx's scratch arenas, zero-filled, for work on stream `use`.
 // The old allocation may still be read by work the ctx enqueued (tvl1_calc is
 // asynchronous), and hipFree would wait for every stream on the device -- every other
-// context's pair in flight.  So the old arena is retired, not freed: it is released at
-// tvl1_destroy.  Growth therefore never drains the device; a ctx holds at most the sizes it
-// grew through (one growth in the usual fixed-size workloads).  The work on `use` is
+// context's pair in flight.  So the old arena is retired, not freed: events recorded on the
+// ctx's streams mark its last use, and it is released once they are done (reap_retired; at
+// most kRetiredMax are held, older ones are waited for) or at tvl1_destroy.  Growth
+// therefore never drains the device.  The arenas are only ever grown: a smaller layout
+// re-lays the existing allocation (ensure_geometry, ensure_batch).  The work on `use` is
 // ordered after the zero fill by an event, not by a host wait.  (The stream-ordered
 // allocator, hipMallocAsync / hipFreeAsync, would release in stream order too, but it
 // deadlocked against a concurrent hipStreamDestroy on this ROCm, so it is not used.)
+// Remember a stream the ctx enqueues work on, so a retired arena can be released once every
+// such stream has passed the point of its retirement.
+static void note_stream(tvl1_ctx *c, hipStream_t s) {
+  for (size_t i = 0; i < c->streams.size(); ++i)
+    if (c->streams[i] == s) {   // most recent last
+      c->streams.erase(c->streams.begin() + i);
+      break;
+    }
+  c->streams.push_back(s);
+  if (c->streams.size() > 8) c->streams.erase(c->streams.begin());
+}
+
+static void free_retired(tvl1_ctx::Retired &r) {
+  (void)hipFree(r.p);
+  for (hipEvent_t e : r.done) (void)hipEventDestroy(e);
+  r.done.clear();
+}
+
+// Release the retired arenas whose work has finished (every event done); with `wait`, the
+// oldest ones are waited for too until at most kRetiredMax remain.  A caller that alternates
+// geometries therefore holds a bounded number of old arenas.
+static constexpr size_t kRetiredMax = 2;
+static void reap_retired(tvl1_ctx *c, bool wait) {
+  size_t keep = 0;
+  for (size_t i = 0; i < c->retired.size(); ++i) {
+    tvl1_ctx::Retired &r = c->retired[i];
+    bool done = true;
+    const bool must = wait && c->retired.size() - i > kRetiredMax;
+    for (hipEvent_t e : r.done) {
+      if (must) (void)hipEventSynchronize(e);
+      else if (hipEventQuery(e) != hipSuccess) done = false;
+    }
+    (void)hipGetLastError();   // hipErrorNotReady is not an error
+    if (done) free_retired(r);
+    else c->retired[keep++] = r;
+  }
+  c->retired.resize(keep);
+}
+
 static tvl1_status arena_alloc(tvl1_ctx *c, char **arena, size_t *have, size_t bytes,
                                hipStream_t use) {
+  note_stream(c, use);
   if (*arena) {
-    c->retired.push_back(*arena);
+    tvl1_ctx::Retired r{*arena, {}};
+    note_stream(c, c->own_stream);
+    for (hipStream_t s : c->streams) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        continue;
+      }
+      if (hipEventRecord(e, s) != hipSuccess) {   // a destroyed stream: nothing left on it
+        (void)hipGetLastError();
+        (void)hipEventDestroy(e);
+        continue;
+      }
+      r.done.push_back(e);
+    }
+    c->retired.push_back(r);
     *arena = nullptr;
     *have = 0;
+    reap_retired(c, true);
   }
   hipError_t e = hipMalloc((void **)arena, bytes);
   if (e != hipSuccess && !c->retired.empty()) {
     // out of memory with outgrown arenas held: release them (hipFree waits for the device;
     // a rare path, better than failing) and try once more
     (void)hipGetLastError();
-    for (char *r : c->retired) (void)hipFree(r);
+    for (auto &r : c->retired) free_retired(r);
     c->retired.clear();
     e = hipMalloc((void **)arena, bytes);
   }
@@ -292,6 +355,8 @@ static tvl1_status arena_alloc(tvl1_ctx *c, char **arena, size_t *have, size_t b
 // Carve the arena for a geometry; grows (never shrinks) the device allocation.  The
 // calls's work goes to stream st.
 static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H, hipStream_t st) {
+  note_stream(c, st);
+  if (!c->retired.empty()) reap_retired(c, false);
   Geometry g;
   g.W = W;
   g.H = H;
@@ -1310,7 +1375,9 @@ static tvl1_status ensure_batch(tvl1_ctx *c, int W, int H, int n, hipStream_t st
   bytes += (ps * n * sizeof(float) + 256) * (4 + 8 + 3);   // U + P + C
   bytes += (size_t)tb_blocks * n * sizeof(double) + 4096;
   c->bW = c->bH = c->bL = c->bn = 0;
-  {
+  // a layout that fits re-lays the existing arena (stream-ordered like ensure_geometry's):
+  // only growth allocates, so alternating batch geometries hold one arena
+  if (bytes > c->barena_bytes) {
     const tvl1_status r = arena_alloc(c, &c->barena, &c->barena_bytes, bytes, st);
     if (r != TVL1_OK) return r;   // TVL1_ENOMEM: the caller retries a smaller chunk
   }
@@ -1359,6 +1426,10 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
   BatchSel all{};
   all.n = n;
   for (int b = 0; b < n; ++b) all.idx[b] = (uint8_t)b;
+  if (c->profiling) {   // per-class HIP events of this chunk's launches (shared by its pairs)
+    c->ev_used = 0;
+    c->marks.clear();
+  }
 
   // [A.1] convertTo + [A.2] pyramid
   hipLaunchKernelGGL(kb_convert, grid2(W, H, 2 * n), kBlk2, 0, st, I0, pitch0, stride0, I1,
@@ -1456,10 +1527,27 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         wi.sel.ubit = ubit;
         wi.sel.pbit = pbit;
         wi.sel.pzero = pzero;
+        const size_t tkw = prof_begin(c, st);
 #define KB_WITER(FM) \
   hipLaunchKernelGGL((kb_warp_iter<6, FM>), dim3(wi.w.ra.waves, n), dim3(192), 0, st, wi);
         MATH_SWITCH(math, KB_WITER)
 #undef KB_WITER
+        if (tkw) {   // k_warp_iter's accounting per pair (constants always stored), x n
+          const int seg = wi.w.ra.seg_rows, segs = (lh + seg - 1) / seg;
+          double rows = 0.0;
+          for (int sg = 0; sg < segs; ++sg) {
+            const int ys = sg * seg, ye = std::min(ys + seg, lh);
+            rows += std::min(ye - 1 + 2, lh - 1) - std::max(ys - 2, 0) + 1;
+          }
+          const double Nl = (double)lw * lh;
+          int nz = 0;   // pairs whose p is zero (a level's first warp): p not loaded
+          for (int b = 0; b < n; ++b) nz += pzero.test(b) ? 1 : 0;
+          const double band_bytes = (double)wi.w.ra.bands * 128 * rows * 4.0;
+          const double hbm = band_bytes * ((double)nz * 3 + (double)(n - nz) * 7 +
+                                           (double)n * (128 + 2 * 6) / 128) +
+                             (double)n * Nl * 4.0 * 9.0;
+          prof_end(c, st, tkw, 0, (double)n * Nl * (64.0 * 2 + 40.0), hbm);
+        }
         hipLaunchKernelGGL(kb_reduce, dim3(n), dim3(kBlock), 0, st, c->bpartials, wi.w.ra.waves,
                            all, c->pinned_dev + 8);
         HIP_TRY(c, hipEventRecord(c->ev_check[0], st));
@@ -1480,10 +1568,12 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         br.ps = ps;
         br.sel = all;
         br.sel.ubit = ubit;
+        const size_t tkr = prof_begin(c, st);
 #define KB_RING(FM) \
   hipLaunchKernelGGL((kb_warp_ring<6, 2, FM>), dim3(br.wa.waves, n), dim3(128), 0, st, br);
         MATH_SWITCH(math, KB_RING)
 #undef KB_RING
+        prof_end(c, st, tkr, 1, (double)n * lw * lh * 40.0, (double)n * lw * lh * 28.0);
       }
       int nact = 0;
       for (int b = 0; b < n; ++b) {
@@ -1567,6 +1657,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           br.nblk = blocks;
           br.sel = sel;
           const dim3 grid((br.ra.waves + 3) / 4, sel.n);
+          const size_t tkp = prof_begin(c, st);
 #define KB_ROLL_M(FM) hipLaunchKernelGGL((kb_iterate_roll<KK, 2, FM>), grid, dim3(256), 0, st, br);
 #define KB_ROLL(K_)                 \
   {                                 \
@@ -1581,6 +1672,21 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           }
 #undef KB_ROLL
 #undef KB_ROLL_M
+          if (tkp) {   // k_iterate_roll's accounting (PX = 2 bands) per pair of the launch
+            const int seg = br.ra.seg_rows, segs = (lh + seg - 1) / seg;
+            double rows = 0.0;
+            for (int sg = 0; sg < segs; ++sg) {
+              const int ys = sg * seg, ye = std::min(ys + seg, lh);
+              rows += std::min(ye - 1 + K, lh - 1) - std::max(ys - K, 0) + 1;
+            }
+            const double Nl = (double)lw * lh;
+            int nz = 0;
+            for (int j = 0; j < sel.n; ++j) nz += pzero.test(sel.idx[j]) ? 1 : 0;
+            const double band_bytes = (double)br.ra.bands * 128 * rows * 4.0;
+            const double hbm = band_bytes * ((double)sel.n * 5 + (double)(sel.n - nz) * 4) +
+                               (double)sel.n * Nl * 4.0 * 6.0;
+            prof_end(c, st, tkp, 0, (double)sel.n * Nl * 64.0 * K, hbm);
+          }
         }
         for (int j = 0; j < sel.n; ++j) {
           const int b = sel.idx[j];
@@ -1680,6 +1786,29 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         sb.kernel_hbm_bytes[k] = 0.0;
       }
     }
+  }
+  // with tvl1_set_profiling: every pair of the chunk reports the chunk's launches (each
+  // launch serves all its pairs; bytes are summed over them)
+  if (c->profiling && !c->marks.empty()) {
+    HIP_TRY(c, hipEventSynchronize(c->ev_pool[c->marks.back().b]));
+    double ms[4] = {}, by[4] = {}, hb[4] = {};
+    int64_t nl[4] = {};
+    for (const auto &m : c->marks) {
+      float t = 0.f;
+      HIP_TRY(c, hipEventElapsedTime(&t, c->ev_pool[m.a], c->ev_pool[m.b]));
+      ms[m.cls] += t;
+      nl[m.cls] += 1;
+      by[m.cls] += m.bytes;
+      hb[m.cls] += m.hbm_bytes;
+    }
+    if (stats)
+      for (int b = 0; b < n; ++b)
+        for (int k = 0; k < 4; ++k) {
+          stats[b].kernel_ms[k] = ms[k];
+          stats[b].kernel_launches[k] = nl[k];
+          stats[b].kernel_bytes[k] = by[k];
+          stats[b].kernel_hbm_bytes[k] = hb[k];
+        }
   }
   return TVL1_OK;
 }
@@ -1954,6 +2083,9 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     delete c;
     return set_err(nullptr, TVL1_EHIP, "HIP initialisation failed on device %d", device);
   }
+  // hipHostMalloc does not promise zeroed memory: a stale sequence word >= the first check's
+  // would let the residual poll return before k_reduce wrote
+  memset(c->pinned, 0, sizeof(double) * (8 + kBatchMax));
   // resident wavefronts / blocks of the streaming kernels, for their segment sizing
   {
     auto blocks_of = [&](const void *fn, int threads) {
@@ -2326,7 +2458,7 @@ void tvl1_destroy(tvl1_ctx *c) {
   if (c->barena) (void)hipFree(c->barena);
   if (c->align_scratch) (void)hipFree(c->align_scratch);
   if (c->map_scratch) (void)hipFree(c->map_scratch);
-  for (char *r : c->retired) (void)hipFree(r);
+  for (auto &r : c->retired) free_retired(r);
   if (c->align_pat) (void)hipFree(c->align_pat);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

@@ -15,11 +15,13 @@ from optflow_amd.capi import (STATUS, TVL1_MAX_LEVELS, TVL1Error, TVL1Params, TV
 ORACLE_SO = Path(__file__).resolve().parent / "liboracle_tvl1.so"
 
 
-def load_oracle() -> C.CDLL:
-    """The CPU restatement (oracle/tvl1_oracle.c) behind the engine's host-call shape."""
-    if not ORACLE_SO.exists():
-        raise FileNotFoundError(f"{ORACLE_SO} not built (run __graft_entry__.build())")
-    lib = C.CDLL(str(ORACLE_SO))
+def load_oracle(so: str | Path | None = None) -> C.CDLL:
+    """The CPU restatement (oracle/tvl1_oracle.c) behind the engine's host-call shape;
+    `so`: another build of the same sources (bench.py's host-tuned cpu_baseline build)."""
+    path = Path(so) if so else ORACLE_SO
+    if not path.exists():
+        raise FileNotFoundError(f"{path} not built (run __graft_entry__.build())")
+    lib = C.CDLL(str(path))
     lib.orc_tvl1_calc.restype = C.c_int
     lib.orc_tvl1_calc.argtypes = [C.POINTER(TVL1Params), C.POINTER(C.c_uint8), C.c_size_t,
                                   C.POINTER(C.c_uint8), C.c_size_t, C.c_int, C.c_int,
@@ -36,10 +38,11 @@ def load_oracle() -> C.CDLL:
 
 
 def oracle_calc(I0: np.ndarray, I1: np.ndarray, params: TVL1Params | None = None,
-                warp_iters: bool = True, threads: int | None = None):
+                warp_iters: bool = True, threads: int | None = None,
+                so: str | Path | None = None):
     """Run the CPU restatement on host u8 images (or float32 images: tvl1_calc_f32's
     contract, values scaled by 255); returns (u, v, stats, warp_iters)."""
-    lib = load_oracle()
+    lib = load_oracle(so)
     if threads:
         lib.orc_set_num_threads(int(threads))
     params = params or make_params()

@@ -236,3 +236,26 @@ def test_device_fault_recovery(tmp_path, built, rois):
     assert outs["clean"] and outs["clean"].keys() == outs["fault"].keys()
     for name, a in outs["clean"].items():
         assert np.array_equal(a.view(np.uint32), outs["fault"][name].view(np.uint32)), name
+
+
+def test_config_error_is_not_a_device_fault(tmp_path, built):
+    """A pair whose TV-L1 parameters the engine rejects (TVL1_EINVAL from tvl1_set_params:
+    medianFiltering 4) is an input error: reported with "Error:" like the reference's input
+    errors, without a device-context rebuild or retry; the other pairs are solved."""
+    zs = [synth.gen_pair(120, 90, seed=90 + k)[0] for k in range(3)]
+    for k, z in enumerate(zs):
+        Image.fromarray(z).save(tmp_path / f"s{k}.png")
+    images = [{"p": str(tmp_path / f"s{k}.png"), "q": str(tmp_path / f"s{k + 1}.png"),
+               "output_name": f"z{k}"} for k in range(2)]
+    images[0]["medianFiltering"] = 4
+    cfg = {"output_dir": str(tmp_path), "scale": 1, "output_type": "flow", "nscales": 3,
+           "warps": 2, "inflight": 1, "rois": {"custom": [0, 0, 120, 90]}, "images": images}
+    p = tmp_path / "bad.json"
+    p.write_text(json.dumps(cfg))
+    r = subprocess.run([str(OPTFLOW), str(p)], capture_output=True, text=True, timeout=300)
+    assert "retrying on a fresh device context" not in r.stderr, r.stderr
+    assert "Error: pair 0" in r.stderr and "medianFiltering" in r.stderr, r.stderr
+    assert not list(tmp_path.glob("z0_*.tiff"))
+    u, v = oracle_post(zs[1], zs[2], capi.make_params(nscales=3, warps=2), 0)
+    (fx,) = tmp_path.glob("z1_*_x.tiff")
+    assert np.array_equal(tif(fx).view(np.uint32), u.view(np.uint32))

@@ -261,3 +261,24 @@ def test_arena_growth_keeps_other_contexts_running(built):
     assert bits_equal(ub.cpu().numpy(), us) and bits_equal(vb.cpu().numpy(), vs)
     ea.close()
     eb.close()
+
+
+def test_batch_profiling_classes_and_same_bits(built):
+    """tvl1_set_profiling on a batch: every pair reports the chunk's per-class launch times,
+    launches and accounted bytes (the production_strips roofline of bench.py), and the
+    events change no bit."""
+    p = capi.make_params(nscales=10, warps=5)
+    eng = capi.Engine(p)
+    I0s, I1s = pairs(6, 300, 100, seed=121)
+    u0, v0, st0 = run_batch(eng, I0s, I1s)
+    eng.set_profiling(True)
+    u1, v1, st1 = run_batch(eng, I0s, I1s)
+    eng.set_profiling(False)
+    eng.close()
+    assert bits_equal(u0, u1) and bits_equal(v0, v1)
+    for b in range(6):
+        np.testing.assert_array_equal(st0[b]["warp_iters"], st1[b]["warp_iters"])
+        assert st0[b]["kernel_launches"][0] == 0
+        assert st1[b]["kernel_launches"][0] > 0 and st1[b]["kernel_ms"][0] > 0
+        assert st1[b]["kernel_hbm_bytes"][0] > 0 and st1[b]["kernel_bytes"][0] > 0
+        assert st1[b]["kernel_ms"] == st1[0]["kernel_ms"]   # one chunk: shared launches

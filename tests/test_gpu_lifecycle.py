@@ -1,0 +1,119 @@
+"""Context lifecycle and concurrency: re-created contexts, contexts solving at
+once with speculation, and batch arenas under alternating geometries.  Every result is held
+to the same bar as tests/test_gpu_parity.py: bit-identical to the oracle, same per-warp
+iteration counts."""
+import threading
+
+import numpy as np
+import pytest
+
+from optflow_amd import capi, synth
+from oracle import checker
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def bits_equal(a, b):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_recreated_ctx_bit_identical(built):
+    """tvl1_create after tvl1_destroy in one process: the new ctx's pinned residual slots
+    (sequence word included) may come from the freed ctx's block; they must start at zero,
+    or the residual poll would read a stale residual and the stopping rule act on it."""
+    I0, I1 = synth.gen_pair(320, 240, seed=51)
+    p = capi.make_params(nscales=4, warps=8)
+    ur, vr, _, wr = checker.oracle_calc(I0, I1, p)
+    for rep in range(4):
+        eng = capi.Engine(p)
+        for _ in range(1 + rep % 2):   # a later ctx inherits a larger sequence number
+            u, v, st, wi = eng.calc_host(I0, I1)
+            np.testing.assert_array_equal(wi, wr, err_msg=f"ctx {rep}")
+            assert bits_equal(u, ur) and bits_equal(v, vr), f"ctx {rep}"
+        eng.close()
+
+
+@pytest.mark.parametrize("spec", ["2", "1"])
+def test_concurrent_contexts_with_speculation(built, monkeypatch, spec):
+    """3 contexts solving at once on their own streams.  TVL1_SPEC=2: every check enqueues
+    its guess even while the other solves share the device, so misses (the rewind path) do
+    happen; TVL1_SPEC=1 (default): speculation switches on and off mid-solve as the count of
+    solves in progress changes.  Every result equals the oracle's."""
+    monkeypatch.setenv("TVL1_SPEC", spec)
+    cases = [(256, 200, 61, dict(nscales=3, warps=6, epsilon=0.002)),
+             (320, 240, 62, dict(nscales=4, warps=10)),
+             (200, 150, 63, dict(nscales=3, warps=4, gamma=0.2))]
+    engines = [capi.Engine(capi.make_params(**kw)) for (_, _, _, kw) in cases]
+    inputs = [synth.gen_pair(W, H, seed=s) for (W, H, s, _) in cases]
+    out = [None] * len(cases)
+    errs = []
+
+    def run(i):
+        try:
+            res = []
+            for _ in range(3):
+                res.append(engines[i].calc_host(*inputs[i]))
+            out[i] = res
+        except Exception as e:   # reported below, in the test thread
+            errs.append(e)
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(cases))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for e in engines:
+        e.close()
+    assert not errs, errs
+    misses = 0
+    for i, (W, H, s, kw) in enumerate(cases):
+        ur, vr, _, wr = checker.oracle_calc(*inputs[i], capi.make_params(**kw))
+        for (u, v, st, wi) in out[i]:
+            np.testing.assert_array_equal(wi, wr, err_msg=f"case {i}")
+            assert bits_equal(u, ur) and bits_equal(v, vr), f"case {i}"
+            misses += st["speculation_misses"]
+    print(f"TVL1_SPEC={spec}: {misses} speculation misses over 9 solves")
+    if spec == "2":
+        assert misses > 0, "the miss / rewind path was not reached"
+
+
+def test_batch_alternating_geometries_hold_one_arena(built):
+    """Two strip geometries alternated on one ctx: the batch arena is re-laid, not
+    re-allocated, once it is large enough, so device memory stops falling after the first
+    round; every batch stays bit-identical to the oracle."""
+    p = capi.make_params(nscales=4, warps=3)
+    eng = capi.Engine(p)
+    dev = torch.device("cuda", 0)
+    shapes = [(300, 100, 6), (200, 60, 9)]
+    data = {}
+    for (w, h, n) in shapes:
+        I0s = np.stack([synth.gen_pair(w, h, seed=80 + b)[0] for b in range(n)])
+        I1s = np.stack([synth.gen_pair(w, h, seed=80 + b)[1] for b in range(n)])
+        data[(w, h, n)] = (I0s, I1s)
+    free = []
+    for rnd in range(4):
+        for (w, h, n) in shapes:
+            I0s, I1s = data[(w, h, n)]
+            d0 = torch.from_numpy(I0s).to(dev)
+            d1 = torch.from_numpy(I1s).to(dev)
+            du = torch.zeros((n, h, w), dtype=torch.float32, device=dev)
+            dv = torch.zeros_like(du)
+            torch.cuda.synchronize()
+            st = eng.calc_batch_device(n, d0.data_ptr(), w, w * h, d1.data_ptr(), w, w * h, w, h,
+                                       du.data_ptr(), dv.data_ptr(), 4 * w, 4 * w * h,
+                                       warp_iters=True)
+            torch.cuda.synchronize()
+            if rnd in (0, 3):
+                u, v = du.cpu().numpy(), dv.cpu().numpy()
+                for b in range(n):
+                    ur, vr, _, wr = checker.oracle_calc(I0s[b], I1s[b], p)
+                    np.testing.assert_array_equal(st[b]["warp_iters"], wr)
+                    assert bits_equal(u[b], ur) and bits_equal(v[b], vr), (w, h, b)
+            del d0, d1, du, dv
+        torch.cuda.empty_cache()
+        free.append(torch.cuda.mem_get_info(0)[0])
+    eng.close()
+    # after round 0 the arena has its final size: no further device memory is taken
+    assert min(free[1:]) >= free[0] - (8 << 20), free
