@@ -101,7 +101,9 @@ struct tvl1_ctx {
   long fuse_min = 5000000;   // TVL1_FUSE_MIN: k_warp_iter on levels of >= this many px; smaller
                              // levels: k_warp_ring + the pass (as fast, and their warps mostly
                              // run past the first check)
-  int witer_slots = 0;       // resident k_warp_iter<6, -, 128> blocks per device
+  int witer_slots = 0;       // resident k_warp_iter<6, -, 128, 1, wi_nc> blocks per device
+  int wi_nc = 2;             // TVL1_WI_NC: k_warp_iter consumer wavefronts (2: one per
+                             // iteration of the pass; 1: both on one wave)
   // batch arena (tvl1_calc_batch): per logical plane, kBatchMax pairs' copies
   char *barena = nullptr;
   size_t barena_bytes = 0;
@@ -926,8 +928,11 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
                            c->partials_cap);
-#define WITER(FM) \
-  hipLaunchKernelGGL((k_warp_iter<M, FM, BW>), dim3(w.ra.waves), dim3(64 + BW), 0, st, w);
+#define WITER(FM)                                                                           \
+  if (c->wi_nc == 2)                                                                       \
+    hipLaunchKernelGGL((k_warp_iter<M, FM, BW, 1, 2>), dim3(w.ra.waves), dim3(128 + BW), 0, st, w); \
+  else                                                                                     \
+    hipLaunchKernelGGL((k_warp_iter<M, FM, BW, 1, 1>), dim3(w.ra.waves), dim3(64 + BW), 0, st, w);
           MATH_SWITCH(math, WITER)
 #undef WITER
           // compulsory: p, u, I0 and the I1 window (x 1 + 2M/BW) per band column and row;
@@ -2061,6 +2066,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_ROLL_SEG")) c->roll_seg = atoi(m);
   if (const char *m = getenv("TVL1_ROLL_PX4_MIN")) c->roll_px4_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_WI_NC")) c->wi_nc = atoi(m) == 1 ? 1 : 2;
   if (const char *m = getenv("TVL1_POLL")) c->poll = atoi(m);
   if (const char *m = getenv("TVL1_SPEC")) c->spec = atoi(m);
   if (const char *m = getenv("TVL1_SPEC_TRACE")) c->spec_trace = atoi(m);
@@ -2100,7 +2106,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     ROLL_SLOTS(false, 1, 4) ROLL_SLOTS(false, 2, 4) ROLL_SLOTS(true, 1, 4) ROLL_SLOTS(true, 2, 4)
 #undef ROLL_SLOTS
     c->warp_ring_slots = blocks_of((const void *)k_warp_ring<6, 2>, 128);
-    c->witer_slots = blocks_of((const void *)k_warp_iter<6>, 192);
+    c->witer_slots = c->wi_nc == 2 ? blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 2>, 256)
+                                   : blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 1>, 192);
     // >= 3-iteration passes stream when the level has at least 4 wavefronts' worth of 56 x 32
     // tiles per SIMD (the measured crossover against 64 x 32 blocked regions)
     c->roll_long_min = 16L * prop.multiProcessorCount;

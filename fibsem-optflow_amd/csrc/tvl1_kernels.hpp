@@ -1978,20 +1978,201 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
   roll_advance<false, 2, PX, true, FM>(S, in, a, B, r, L, rowb, acc);
 }
 
-template <int M, int FM, int BW, int PRIO = 0>
+// ---- the two-consumer form (NC = 2): one wavefront per iteration of the pass.
+// The single consumer's step (2 iterations x 2 px, ~480 VALU) was the block's critical
+// path against the producers' ~290.  Here stage 1 and stage 2 of the
+// k_iterate_roll<false, 2, 2> pipeline run on two wavefronts, each over the whole band (so
+// the x-neighbours stay DPP shifts inside the wave), stage 2 one step behind stage 1.  They
+// evaluate exactly roll_advance's operations on exactly its operands; only the wave doing
+// them changes.  Stage 1 also does iteration 2's TH step (pointwise on u^1 and the row's
+// constants: estimate_u_px = th_px then u_from_v), so the steps balance (~250 / ~180).
+// Hand-off ring (LDS, 2 slots of kWiH planes x BW floats): for input row r, stage 1 writes
+// v^2(r) (u^1(r) + TH step), u^1(r) (the residual's old u) and p^1(r-1); stage 2 reads the
+// slot one barrier later.  A slot is overwritten two steps after it was written, after the
+// read at the step between.
+constexpr int kWiH = 8;
+
+template <int PX>
+struct WiS1 {   // stage 1 registers (k_iterate_roll's RollPipe stage 0 / 1 entries)
+  float U1c[PX], U2c[PX];                        // u^1(r)
+  float U1p[PX], U2p[PX];                        // u^1(r-1)
+  float P11c[PX], P12c[PX], P21c[PX], P22c[PX];  // p^0(r)
+  float P11p[PX], P12p[PX], P21p[PX], P22p[PX];  // p^0(r-1)
+};
+
+template <int PX>
+struct WiS2 {   // stage 2 registers (RollPipe stage 1 / 2 entries)
+  float V1p[PX], V2p[PX];                        // v^2(r-1)
+  float W1p[PX], W2p[PX];                        // u^1(r-1)
+  float Q11c[PX], Q12c[PX], Q21c[PX], Q22c[PX];  // p^1(r-1)
+  float Q11p[PX], Q12p[PX], Q21p[PX], Q22p[PX];  // p^1(r-2)
+  float U1c[PX], U2c[PX];                        // u^2(r-1)
+  float U1p[PX], U2p[PX];                        // u^2(r-2)
+};
+
+template <int PX>
+__device__ __forceinline__ void lds_put(float *__restrict__ p, const float (&v)[PX]) {
+  if constexpr (PX == 2) *reinterpret_cast<float2 *>(p) = make_float2(v[0], v[1]);
+  else
+#pragma unroll
+    for (int j = 0; j < PX; ++j) p[j] = v[j];
+}
+template <int PX>
+__device__ __forceinline__ void lds_get(float (&v)[PX], const float *__restrict__ p) {
+  if constexpr (PX == 2) {
+    const float2 t = *reinterpret_cast<const float2 *>(p);
+    v[0] = t.x;
+    v[1] = t.y;
+  } else {
+#pragma unroll
+    for (int j = 0; j < PX; ++j) v[j] = p[j];
+  }
+}
+
+// Stage 1 at input row r: u^1(r) = v(r) + theta div p^0 (roll_advance's VIN stage 1),
+// p^1(r-1) from u^1(r-1), u^1(r) and p^0(r-1), and iteration 2's TH step on u^1(r).
+template <int FM, int PX>
+__device__ __forceinline__ void wi_s1_step(WiS1<PX> &S, const float *__restrict__ cring,
+                                           float *__restrict__ hring, const WiP<PX> &cur,
+                                           WiP<PX> &ahead, const IterArgs &a, const RollBufs &B,
+                                           int r, const RollLane &L, int lane, unsigned rowb) {
+  wi_p_load(ahead, B, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vload);
+  __builtin_amdgcn_sched_barrier(0);
+  lds_barrier();   // C ring row r was written at the previous step; hand-off slot r & 1 read
+  constexpr int BW = 64 * PX;
+  const float *c = cring + (r & 1) * (5 * BW) + PX * lane;
+  float wx[PX], wy[PX], rh[PX], v1[PX], v2[PX];
+  lds_get<PX>(wx, c);
+  lds_get<PX>(wy, c + BW);
+  lds_get<PX>(rh, c + 2 * BW);
+  lds_get<PX>(v1, c + 3 * BW);
+  lds_get<PX>(v2, c + 4 * BW);
+  const bool z = a.p_zero;
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    S.U1p[j] = S.U1c[j]; S.U2p[j] = S.U2c[j];
+    S.P11p[j] = S.P11c[j]; S.P12p[j] = S.P12c[j]; S.P21p[j] = S.P21c[j]; S.P22p[j] = S.P22c[j];
+    S.P11c[j] = z ? 0.0f : cur.p11[j]; S.P12c[j] = z ? 0.0f : cur.p12[j];
+    S.P21c[j] = z ? 0.0f : cur.p21[j]; S.P22c[j] = z ? 0.0f : cur.p22[j];
+  }
+  const int yU = r;
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    float n1, n2, n3;
+    u_from_v<false, FM>(v1[j], v2[j], 0.0f, S.P11c[j], left_of<PX>(S.P11c, j), S.P12c[j],
+                        S.P12p[j], S.P21c[j], left_of<PX>(S.P21c, j), S.P22c[j], S.P22p[j], 0.0f,
+                        0.0f, 0.0f, 0.0f, L.X + j, yU, a, n1, n2, n3);
+    S.U1c[j] = n1; S.U2c[j] = n2;
+  }
+  const int yD = r - 1;
+  const bool has_down = yD + 1 < a.H;
+  float q11[PX], q12[PX], q21[PX], q22[PX], t1[PX], t2[PX];
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    const bool has_right = L.X + j + 1 < a.W;
+    dual_px<false, false, FM>(S.U1p[j], right_of<PX>(S.U1p, j), S.U1c[j], has_right, has_down,
+                              a.taut, S.P11p[j], S.P12p[j], q11[j], q12[j]);
+    dual_px<false, false, FM>(S.U2p[j], right_of<PX>(S.U2p, j), S.U2c[j], has_right, has_down,
+                              a.taut, S.P21p[j], S.P22p[j], q21[j], q22[j]);
+    float t3;
+    th_px<false, FM>(wx[j], wy[j], rh[j], S.U1c[j], S.U2c[j], 0.0f, a, t1[j], t2[j], t3);
+  }
+  float *h = hring + (r & 1) * (kWiH * BW) + PX * lane;
+  lds_put<PX>(h, t1);
+  lds_put<PX>(h + BW, t2);
+  lds_put<PX>(h + 2 * BW, S.U1c);
+  lds_put<PX>(h + 3 * BW, S.U2c);
+  lds_put<PX>(h + 4 * BW, q11);
+  lds_put<PX>(h + 5 * BW, q12);
+  lds_put<PX>(h + 6 * BW, q21);
+  lds_put<PX>(h + 7 * BW, q22);
+}
+
+// Stage 2 at input row r (one barrier after stage 1's step r): u^2(r-1) = v^2(r-1) +
+// theta div p^1, the residual term (u^1(r-1) - u^2(r-1))^2, p^2(r-2); stores u^2 and p^2.
+template <int FM, int PX>
+__device__ __forceinline__ void wi_s2_step(WiS2<PX> &S, const float *__restrict__ hring,
+                                           const IterArgs &a, const RollBufs &B, int r,
+                                           const RollLane &L, int lane, unsigned rowb,
+                                           double &acc) {
+  lds_barrier();   // hand-off row r was written at the previous step
+  constexpr int BW = 64 * PX;
+  const unsigned ps = B.pstride;
+  const float *h = hring + (r & 1) * (kWiH * BW) + PX * lane;
+  float v1[PX], v2[PX], w1[PX], w2[PX];
+  lds_get<PX>(v1, h);
+  lds_get<PX>(v2, h + BW);
+  lds_get<PX>(w1, h + 2 * BW);
+  lds_get<PX>(w2, h + 3 * BW);
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    S.U1p[j] = S.U1c[j]; S.U2p[j] = S.U2c[j];
+    S.Q11p[j] = S.Q11c[j]; S.Q12p[j] = S.Q12c[j]; S.Q21p[j] = S.Q21c[j]; S.Q22p[j] = S.Q22c[j];
+  }
+  lds_get<PX>(S.Q11c, h + 4 * BW);
+  lds_get<PX>(S.Q12c, h + 5 * BW);
+  lds_get<PX>(S.Q21c, h + 6 * BW);
+  lds_get<PX>(S.Q22c, h + 7 * BW);
+  const int yU = r - 1;
+  const bool stU = L.out && yU >= L.ys && yU < L.ye;
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    float n1, n2, n3;
+    u_from_v<false, FM>(S.V1p[j], S.V2p[j], 0.0f, S.Q11c[j], left_of<PX>(S.Q11c, j), S.Q12c[j],
+                        S.Q12p[j], S.Q21c[j], left_of<PX>(S.Q21c, j), S.Q22c[j], S.Q22p[j], 0.0f,
+                        0.0f, 0.0f, 0.0f, L.X + j, yU, a, n1, n2, n3);
+    if (a.calc_err) {
+      const float e = residual_px<FM>(S.W1p[j] - n1, S.W2p[j] - n2);
+      acc += stU && L.X + j < a.W ? (double)e : 0.0;
+    }
+    S.U1c[j] = n1; S.U2c[j] = n2;
+  }
+  {
+    const unsigned vo = stU ? (unsigned)yU * rowb + L.vst : kOOB;
+    bstorev<PX>(B.ud, B.ub, vo, S.U1c);
+    bstorev<PX>(B.ud, B.ub, vo, S.U2c, ps);
+  }
+  const int yD = r - 2;
+  const bool has_down = yD + 1 < a.H;
+  float o11[PX], o12[PX], o21[PX], o22[PX];
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    const bool has_right = L.X + j + 1 < a.W;
+    dual_px<false, false, FM>(S.U1p[j], right_of<PX>(S.U1p, j), S.U1c[j], has_right, has_down,
+                              a.taut, S.Q11p[j], S.Q12p[j], o11[j], o12[j]);
+    dual_px<false, false, FM>(S.U2p[j], right_of<PX>(S.U2p, j), S.U2c[j], has_right, has_down,
+                              a.taut, S.Q21p[j], S.Q22p[j], o21[j], o22[j]);
+  }
+  {
+    const unsigned vo = L.out && yD >= L.ys && yD < L.ye ? (unsigned)yD * rowb + L.vst : kOOB;
+    bstorev<PX>(B.pd, B.pb, vo, o11);
+    bstorev<PX>(B.pd, B.pb, vo, o12, ps);
+    bstorev<PX>(B.pd, B.pb, vo, o21, 2 * ps);
+    bstorev<PX>(B.pd, B.pb, vo, o22, 3 * ps);
+  }
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {   // row r's hand-off values are row r-1's at the next step
+    S.V1p[j] = v1[j]; S.V2p[j] = v2[j];
+    S.W1p[j] = w1[j]; S.W2p[j] = w2[j];
+  }
+}
+
+template <int M, int FM, int BW, int PRIO = 0, int NC = 1>
 __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, float *__restrict__ ring,
-                                               float *__restrict__ cring) {
+                                               float *__restrict__ cring,
+                                               float *__restrict__ hring = nullptr) {
   constexpr int K = 2, PX = BW / 64, HALO = roll_halo<2, PX>(), WW = wi_ww<M, BW>();
   static_assert(BW == 64 || BW == 128, "one producer per 64 columns, PX = 1 or 2");
   static_assert(2 * M + 2 <= wi_rows<M>(), "window ring too small for the margin");
   static_assert(2 * M <= 64, "second window slot per lane");
   static_assert(kRollAhead == 2 && kWarpAhead == 2, "the step loops are unrolled by 3");
+  static_assert(NC == 1 || NC == 2, "one consumer wave, or one per iteration");
   (void)WW;
   const RollArgs &ra = w.ra;
   const IterArgs &a = ra.it;
   const int lane = threadIdx.x & 63;
   // wave 0 consumer, 1-2 producers (measured: a consumer on wave 1 or 2 of some blocks, or
-  // a raised s_setprio for it, is slower)
+  // a raised s_setprio for it, is slower).  NC = 2: waves 0 / 1 stages 1 / 2, 2-3 producers
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int band = wid % ra.bands, seg = wid / ra.bands;
   const int X0 = band * (BW - 2 * HALO) - HALO;   // the band's first px
@@ -2002,7 +2183,63 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
   // consumer steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K; the producers run one row ahead
   // and 3 (thirds + 1) steps, the consumer 1 + 3 thirds + 2 barriers
   const int thirds = (ye + K - r0 + 2) / 3;
-  if (wv == 0) {
+  if (NC == 2 && wv < 2) {
+    // stage 1: barriers 0 (prologue), 1 .. 3 thirds (steps), 2 final; stage 2: barriers
+    // 0, 1 (prologue), 2 .. 3 thirds + 1 (steps), 1 final -- as many as the producers'
+    RollLane L;
+    L.X = X0 + PX * lane;
+    L.vload = 4u * imin(imax(L.X, 0), a.P - PX);
+    L.out = PX * lane >= HALO && PX * lane < BW - HALO && L.X < a.W;
+    L.vst = 4u * (unsigned)imax(L.X, 0);
+    L.ys = ys;
+    L.ye = ye;
+    const RollBufs &Bf = ra.b;
+    if (wv == 0) {
+      WiS1<PX> S;
+#pragma unroll
+      for (int j = 0; j < PX; ++j) {
+        S.U1c[j] = S.U2c[j] = S.U1p[j] = S.U2p[j] = 0.0f;
+        S.P11c[j] = S.P12c[j] = S.P21c[j] = S.P22c[j] = 0.0f;
+        S.P11p[j] = S.P12p[j] = S.P21p[j] = S.P22p[j] = 0.0f;
+      }
+      WiP<PX> A, B, C;
+      wi_p_load(A, Bf, (unsigned)r0 * rowb, L.vload);
+      wi_p_load(B, Bf, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
+      lds_barrier();   // the producers' first step (row r0)
+      for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
+        progress_prio<PRIO>(h, thirds);
+        wi_s1_step<FM, PX>(S, cring, hring, A, C, a, Bf, r, L, lane, rowb);
+        wi_s1_step<FM, PX>(S, cring, hring, B, A, a, Bf, r + 1, L, lane, rowb);
+        wi_s1_step<FM, PX>(S, cring, hring, C, B, a, Bf, r + 2, L, lane, rowb);
+      }
+      lds_barrier();
+      lds_barrier();
+    } else {
+      WiS2<PX> S;
+#pragma unroll
+      for (int j = 0; j < PX; ++j) {
+        S.V1p[j] = S.V2p[j] = S.W1p[j] = S.W2p[j] = 0.0f;
+        S.Q11c[j] = S.Q12c[j] = S.Q21c[j] = S.Q22c[j] = 0.0f;
+        S.Q11p[j] = S.Q12p[j] = S.Q21p[j] = S.Q22p[j] = 0.0f;
+        S.U1c[j] = S.U2c[j] = S.U1p[j] = S.U2p[j] = 0.0f;
+      }
+      lds_barrier();
+      lds_barrier();
+      double acc = 0.0;
+      for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
+        progress_prio<PRIO>(h, thirds);
+        wi_s2_step<FM, PX>(S, hring, a, Bf, r, L, lane, rowb, acc);
+        wi_s2_step<FM, PX>(S, hring, a, Bf, r + 1, L, lane, rowb, acc);
+        wi_s2_step<FM, PX>(S, hring, a, Bf, r + 2, L, lane, rowb, acc);
+      }
+      lds_barrier();
+      if (a.calc_err) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == 0) a.partials[wid] = acc;
+      }
+    }
+  } else if (NC == 1 && wv == 0) {
     RollLane L;
     L.X = X0 + PX * lane;
     L.vload = 4u * imin(imax(L.X, 0), a.P - PX);
@@ -2058,7 +2295,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
       if (lane == 0) a.partials[wid] = acc;
     }
   } else {
-    const int p = wv - 1;
+    const int p = wv - NC;
     WarpRingArgs wa;
     wa.I0 = w.I0;
     wa.I1 = w.I1;
@@ -2111,13 +2348,14 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
   }
 }
 
-template <int M, int FM = 0, int BW = 128, int PRIO = 1>
-__global__ __launch_bounds__(64 + BW) void k_warp_iter(WarpIterArgs w) {
+template <int M, int FM = 0, int BW = 128, int PRIO = 1, int NC = 1>
+__global__ __launch_bounds__(64 * NC + BW) void k_warp_iter(WarpIterArgs w) {
   __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, BW>()];
   __shared__ float cring[2 * 5 * BW];
+  __shared__ float hring[NC == 2 ? 2 * kWiH * BW : 1];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves || gated_off(w.ra.it.gate, w.ra.it.gate_seq)) return;   // whole blocks
-  warp_iter_body<M, FM, BW, PRIO>(w, wid, ring, cring);
+  warp_iter_body<M, FM, BW, PRIO, NC>(w, wid, ring, cring, hring);
 }
 
 // K7: fixed-order sum of the per-block partials (one block).
