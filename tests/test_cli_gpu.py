@@ -259,3 +259,26 @@ def test_config_error_is_not_a_device_fault(tmp_path, built):
     u, v = oracle_post(zs[1], zs[2], capi.make_params(nscales=3, warps=2), 0)
     (fx,) = tmp_path.glob("z1_*_x.tiff")
     assert np.array_equal(tif(fx).view(np.uint32), u.view(np.uint32))
+
+
+@pytest.mark.parametrize("scale", [0.75, 0.3])
+def test_prescale_generic_linear(tmp_path, pair, scale):
+    """A pre-scale other than 0.5 (OpenCV's generic INTER_LINEAR, /root/reference/src/
+    optflow.cpp:113,125): the solve on the resized frames equals the oracle on the same
+    decoded + resized frames, bit for bit."""
+    cfg = {"output_dir": str(tmp_path), "output_type": "flow", "nscales": 3, "warps": 2,
+           "scale": scale, "images": [{"p": str(tmp_path / "p.png"), "q": str(tmp_path / "q.png"),
+                                       "output_name": "g"}]}
+    dec = []
+    for n in ("p", "q"):
+        subprocess.run([str(OPTFLOW), "--decode", str(tmp_path / f"{n}.png"),
+                        str(tmp_path / f"{n}_s.tif"), str(scale)], check=True)
+        dec.append(np.array(Image.open(tmp_path / f"{n}_s.tif")))
+    h, w = dec[0].shape
+    cfg["rois"] = {"custom": [0, 0, w, h]}
+    run_cli(cfg, tmp_path)
+    u, v = oracle_post(dec[0], dec[1], capi.make_params(nscales=3, warps=2), 0)
+    (fx,) = tmp_path.glob("g_*_x.tiff")
+    (fy,) = tmp_path.glob("g_*_y.tiff")
+    assert np.array_equal(tif(fx).view(np.uint32), u.view(np.uint32))
+    assert np.array_equal(tif(fy).view(np.uint32), v.view(np.uint32))
