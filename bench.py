@@ -190,7 +190,8 @@ def native_oracle():
     src = ROOT / "oracle"
     try:
         subprocess.run(["gcc", *flags, "-shared", "-o", str(so), str(src / "tvl1_oracle.c"),
-                        str(src / "tvl1_oracle_dualtvl1.c"), "-lm"], check=True,
+                        str(src / "tvl1_oracle_dualtvl1.c"), str(src / "tvl1_oracle_align.c"),
+                        "-lm"], check=True,
                        capture_output=True, timeout=120)
         _NATIVE_ORACLE = (str(so), f"gcc {' '.join(flags)} on the bench host ({cpu}, "
                                    f"{os.cpu_count()} logical CPUs)")

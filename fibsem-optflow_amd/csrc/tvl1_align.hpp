@@ -6,9 +6,9 @@
 //     (scaleFactor, nlevels), FAST-9 corners (fastThreshold) at least edgeThreshold px from
 //     the border, ranked by the Harris response (k = 0.04, 7x7 window) after 3x3
 //     non-maximum suppression, the best nfeatures kept with ORB's per-level quota;
-//     orientation by the intensity centroid of the radius-15 disc; 256-bit rotated-BRIEF
-//     descriptors (WTA_K = 2) from a fixed pseudo-random pattern of point pairs in the
-//     31x31 patch;
+//     orientation by the intensity centroid of the radius-15 disc (its unit vector, no
+//     trigonometry); 256-bit rotated-BRIEF descriptors (WTA_K = 2) from a fixed
+//     pseudo-random pattern of point pairs in the 31x31 patch;
 //   * matching: brute-force Hamming 2-NN on the GPU (cuda::DescriptorMatcher::
 //     createBFMatcher(NORM_HAMMING)->knnMatch(.., 2)), the reference's ratio test and
 //     distance sort (features.cpp:98-113);
@@ -17,17 +17,18 @@
 //     a least-squares DLT refit on the inliers; then the reference's zoom check and the
 //     top 2x3 of the homography as the affine (features.cpp:131-166).
 //
-// PARITY UNPINNED and approximate by construction: OpenCV's ORB bit pattern
-// (bit_pattern_31_), its FAST score, its RNG and its Levenberg-Marquardt refinement are not
-// restated, and SURF (features = 2, non-free) is served by the same ORB path with a
-// warning.  The contract kept is the reference's: the same inputs (JSON keys with their
-// defaults), an affine that maps frame1 onto frame0, the same rejection rules and messages.
-// tests/test_align_gpu.py recovers known affine motions of synthetic slices.
+// PARITY UNPINNED against OpenCV and approximate by construction: OpenCV's ORB bit pattern
+// (bit_pattern_31_), its FAST score and its RNG are not restated, and SURF (features = 2,
+// non-free) is served by the same ORB path with a warning.  The contract kept is the
+// reference's: the same inputs (JSON keys with their defaults), an affine that maps frame1
+// onto frame0, the same rejection rules and messages.  This pipeline itself is restated
+// bit for bit by oracle/tvl1_oracle_align.c (test infrastructure): keypoints, descriptors,
+// the 2-NN match list, the fit and the warps are compared exactly (tests/test_align_gpu.py),
+// and known affine motions of synthetic slices are recovered.
 #pragma once
 
 #include <algorithm>
 #include <cmath>
-#include <random>
 #include <vector>
 
 namespace tvl1k {
@@ -259,10 +260,14 @@ __global__ void ka_describe(const float *const *__restrict__ levels, const int *
       m10 += u * val;
       m01 += v * val;
     }
-  const float ang = atan2f(m01, m10);
-  k.angle = ang;
+  // the rotation of the intensity-centroid direction as (cos, sin) = (m10, m01) / |m|:
+  // correctly rounded IEEE operations only, so oracle/tvl1_oracle_align.c restates the
+  // descriptor bit for bit (atan2f / cosf / sinf differ between the device library and
+  // glibc).  The angle is reported for the caller, never used.
+  const float r = sqrtf(m10 * m10 + m01 * m01);
+  const float cs = r > 0.f ? m10 / r : 1.f, sn = r > 0.f ? m01 / r : 0.f;
+  k.angle = atan2f(m01, m10);
   kps[i] = k;
-  const float cs = cosf(ang), sn = sinf(ang);
   for (int w = 0; w < kOrbBits / 32; ++w) {
     uint32_t bits = 0;
     for (int j = 0; j < 32; ++j) {
@@ -565,12 +570,21 @@ static void lm_refine(const std::vector<Pt> &a, const std::vector<Pt> &b, double
 // 10 Levenberg-Marquardt steps on their reprojection error (fundam.cpp's createLMSolver(
 // HomographyRefineCallback, 10)).  Deterministic (fixed seed).  Returns false when no model
 // is found; mask (n entries, optional) gets the inliers.
+// The minimal-sample generator: a 64-bit LCG (Knuth's MMIX constants), its high 32 bits
+// reduced mod n -- fully specified, so the oracle draws the same samples.
+struct SampleRng {
+  uint64_t s = 0x12345678u;
+  int operator()(int n) {
+    s = s * 6364136223846793005ull + 1442695040888963407ull;
+    return (int)((uint32_t)(s >> 32) % (uint32_t)n);
+  }
+};
+
 static bool find_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, int method,
                             double thresh, double H[9], uint8_t *mask = nullptr) {
   const int n = (int)a.size();
   if (n < 4) return false;
-  std::mt19937 rng(0x12345678u);
-  std::uniform_int_distribution<int> pick(0, n - 1);
+  SampleRng pick;
   const bool lmeds = method == 4;
   const double t2 = thresh * thresh;
   double best[9];
@@ -586,7 +600,7 @@ static bool find_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, 
     for (int k = 0; k < 4; ++k) {
       bool dup;
       do {
-        s[k] = pick(rng);
+        s[k] = pick(n);
         dup = false;
         for (int j = 0; j < k; ++j) dup |= s[j] == s[k];
       } while (dup);
@@ -634,16 +648,19 @@ static bool find_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, 
   return true;
 }
 
-// ORB's fixed test pattern stand-in: 256 point pairs in the 31x31 patch, isotropic Gaussian
-// (sigma = patch / 5) clipped to the disc that stays inside the patch under rotation.
+// ORB's fixed test pattern stand-in: 256 point pairs in the 31x31 patch, each coordinate the
+// sum of three uniform integers in [-6, 6] (near-Gaussian, sigma 6.5 ~ patch / 5), pairs
+// outside the radius-13 disc redrawn (|rotated offset| <= 13 < 15).  Integer arithmetic
+// from SampleRng's generator only, so the oracle regenerates the same table.
 static std::vector<int> orb_pattern() {
-  std::mt19937 rng(0x0B5EEDu);
-  std::normal_distribution<double> g(0.0, kOrbPatch / 5.0);
+  SampleRng rng;
+  rng.s = 0x0B5EEDu;
+  auto coord = [&]() { return rng(13) + rng(13) + rng(13) - 18; };
   std::vector<int> p;
   p.reserve(kOrbBits * 4);
   while ((int)p.size() < kOrbBits * 4) {
-    const int x = (int)std::lround(g(rng)), y = (int)std::lround(g(rng));
-    if (x * x + y * y > 13 * 13) continue;   // |rotated offset| <= 13 < 15
+    const int x = coord(), y = coord();
+    if (x * x + y * y > 13 * 13) continue;
     p.push_back(x);
     p.push_back(y);
   }

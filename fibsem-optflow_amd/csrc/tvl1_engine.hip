@@ -1823,8 +1823,9 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
 // find_alignment (features.cpp:46-167) on the GPU + host (tvl1_align.hpp).
 namespace {
 struct OrbSet {
-  std::vector<OrbKp> kps;     // level coordinates
+  std::vector<OrbKp> kps;     // level coordinates (angle filled when asked, orb_detect)
   std::vector<Pt> pts;        // level-0 coordinates
+  std::vector<float> resp;    // Harris responses
   uint32_t *desc = nullptr;   // device, 8 words per keypoint (in the ctx's align scratch)
 };
 
@@ -1919,7 +1920,7 @@ static size_t align_carve(char *base, const OrbGeom &g, bool blur, int nfeat, Al
 // the selected keys, one for the descriptors.
 static tvl1_status orb_detect(tvl1_ctx *c, const uint8_t *img, size_t pitch, const OrbGeom &g,
                               const tvl1_align_params &ap, const AlignCarve &cv, uint32_t *desc,
-                              OrbSet &out, hipStream_t st) {
+                              OrbSet &out, hipStream_t st, bool angles = false) {
   const int L = g.L, W = g.w[0], H = g.h[0];
   std::vector<float *> lev(L);
   {
@@ -1971,6 +1972,10 @@ static tvl1_status orb_detect(tvl1_ctx *c, const uint8_t *img, size_t pitch, con
       const float x = (float)(pos % (unsigned)g.w[l]), y = (float)(pos / (unsigned)g.w[l]);
       out.kps.push_back(OrbKp{x, y, 0.0f, l});
       out.pts.push_back(Pt{x * scale, y * scale});
+      const uint32_t rb = (uint32_t)(k[i] >> 32);   // the key's score bits
+      float rf;
+      memcpy(&rf, &rb, sizeof rf);
+      out.resp.push_back(rf);
     }
   }
   if (ap.blur_for_descriptor) {
@@ -1992,9 +1997,28 @@ static tvl1_status orb_detect(tvl1_ctx *c, const uint8_t *img, size_t pitch, con
     hipLaunchKernelGGL(ka_describe, dim3((nk + 63) / 64), dim3(64), 0, st,
                        (const float *const *)cv.dlev, cv.dlp, cv.kps, nk, c->align_pat, desc);
     HIP_TRY(c, hipGetLastError());
+    if (angles)
+      HIP_TRY(c, hipMemcpyAsync(out.kps.data(), cv.kps, nk * sizeof(OrbKp), hipMemcpyDeviceToHost, st));
     // the host vectors above are the copy sources: they must outlive the copies
     HIP_TRY(c, hipStreamSynchronize(st));
   }
+  return TVL1_OK;
+}
+
+// the rBRIEF pair pattern on the device (set once per ctx)
+static tvl1_status ensure_pattern(tvl1_ctx *c) {
+  if (c->align_pat) return TVL1_OK;
+  static const std::vector<int> pat = orb_pattern();
+  HIP_TRY(c, hipMalloc((void **)&c->align_pat, pat.size() * sizeof(int)));
+  HIP_TRY(c, hipMemcpy(c->align_pat, pat.data(), pat.size() * sizeof(int), hipMemcpyHostToDevice));
+  return TVL1_OK;
+}
+
+static tvl1_status check_orb_params(tvl1_ctx *c, const tvl1_align_params *ap) {
+  if (ap->nlevels <= 0 || !(ap->scale_factor > 1.0f) || ap->nfeatures <= 0)
+    return set_err(c, TVL1_EINVAL, "bad ORB parameters");
+  if (ap->wta_k != 2 || ap->patch_size != 31)
+    return set_err(c, TVL1_EINVAL, "only WTA_K = 2 and patchSize = 31 are supported");
   return TVL1_OK;
 }
 
@@ -2281,16 +2305,15 @@ tvl1_status tvl1_find_alignment(tvl1_ctx *c, const uint8_t *frame1, size_t pitch
   if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
   if (!frame1 || !frame0 || !ap || !affine) return set_err(c, TVL1_EINVAL, "null argument");
   if (w1 <= 0 || h1 <= 0 || w0 <= 0 || h0 <= 0) return set_err(c, TVL1_ESIZE, "bad frame size");
-  if (ap->nlevels <= 0 || !(ap->scale_factor > 1.0f) || ap->nfeatures <= 0)
-    return set_err(c, TVL1_EINVAL, "bad ORB parameters");
-  if (ap->wta_k != 2 || ap->patch_size != 31)
-    return set_err(c, TVL1_EINVAL, "only WTA_K = 2 and patchSize = 31 are supported");
+  {
+    const tvl1_status r = check_orb_params(c, ap);
+    if (r != TVL1_OK) return r;
+  }
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
-  if (!c->align_pat) {
-    static const std::vector<int> pat = orb_pattern();
-    HIP_TRY(c, hipMalloc((void **)&c->align_pat, pat.size() * sizeof(int)));
-    HIP_TRY(c, hipMemcpy(c->align_pat, pat.data(), pat.size() * sizeof(int), hipMemcpyHostToDevice));
+  {
+    const tvl1_status r = ensure_pattern(c);
+    if (r != TVL1_OK) return r;
   }
   const OrbGeom g1 = orb_geom(w1, h1, *ap), g0 = orb_geom(w0, h0, *ap);
   const bool blur = ap->blur_for_descriptor != 0;
@@ -2366,6 +2389,92 @@ tvl1_status tvl1_find_alignment(tvl1_ctx *c, const uint8_t *frame1, size_t pitch
     fprintf(stderr, "[align] detect1 %.2f ms, detect0 %.2f ms, match %.2f ms, model %.2f ms "
                     "(%d / %d keypoints, %zu good)\n",
             ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, now()), nq, nt, good.size());
+  return TVL1_OK;
+}
+
+tvl1_status tvl1_orb_detect(tvl1_ctx *c, const uint8_t *frame, size_t pitch, int32_t w, int32_t h,
+                            const tvl1_align_params *ap, float *kp, uint8_t *desc, int32_t cap,
+                            int32_t *n, void *stream) {
+  if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  if (!frame || !ap || !n || cap < 0 || (cap > 0 && (!kp || !desc)))
+    return set_err(c, TVL1_EINVAL, "null argument");
+  if (w <= 0 || h <= 0 || pitch < (size_t)w) return set_err(c, TVL1_ESIZE, "bad frame size");
+  {
+    const tvl1_status r = check_orb_params(c, ap);
+    if (r != TVL1_OK) return r;
+  }
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  {
+    const tvl1_status r = ensure_pattern(c);
+    if (r != TVL1_OK) return r;
+  }
+  const OrbGeom g = orb_geom(w, h, *ap);
+  const bool blur = ap->blur_for_descriptor != 0;
+  AlignCarve cv;
+  const size_t need = align_carve(nullptr, g, blur, ap->nfeatures, cv);
+  if (need > c->align_bytes) {
+    const tvl1_status r = arena_alloc(c, &c->align_scratch, &c->align_bytes, need, st);
+    if (r != TVL1_OK) return r;
+  }
+  align_carve(c->align_scratch, g, blur, ap->nfeatures, cv);
+  OrbSet q;
+  {
+    const tvl1_status r = orb_detect(c, frame, pitch, g, *ap, cv, cv.desc[0], q, st, true);
+    if (r != TVL1_OK) return r;
+  }
+  const int nk = (int)q.kps.size(), m = std::min(nk, cap);
+  *n = nk;
+  if (m > 0) {
+    HIP_TRY(c, hipMemcpyAsync(desc, cv.desc[0], (size_t)m * 32, hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    for (int i = 0; i < m; ++i) {
+      float deg = q.kps[i].angle * (float)(180.0 / M_PI);   // cv::KeyPoint::angle
+      if (deg < 0.f) deg += 360.f;
+      if (deg >= 360.f) deg = 0.f;   // -tiny + 360 rounds to 360
+      kp[5 * i + 0] = (float)q.pts[i].x;
+      kp[5 * i + 1] = (float)q.pts[i].y;
+      kp[5 * i + 2] = (float)q.kps[i].level;
+      kp[5 * i + 3] = deg;
+      kp[5 * i + 4] = q.resp[i];
+    }
+  }
+  return TVL1_OK;
+}
+
+tvl1_status tvl1_match_knn2(tvl1_ctx *c, const uint8_t *query, int32_t nq, const uint8_t *train,
+                            int32_t nt, int32_t *idx, int32_t *dist, void *stream) {
+  if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  if (nq < 0 || nt < 0 || (nq > 0 && (!query || !idx || !dist)) || (nt > 0 && !train))
+    return set_err(c, TVL1_EINVAL, "bad argument");
+  if (nq == 0) return TVL1_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int nseg = std::max(1, std::min(kMatchSegs, (nt + 255) / 256));
+  const int seg = (int)align_up((size_t)((std::max(nt, 1) + nseg - 1) / nseg), 64);
+  // scratch: query and train descriptors, the per-segment top-2, the merged top-2
+  const size_t oq = 0, ot = align_up((size_t)nq * 32, 256);
+  const size_t op = ot + align_up((size_t)std::max(nt, 1) * 32, 256);
+  const size_t ob = op + align_up((size_t)nq * nseg * sizeof(Top2), 256);
+  const size_t od = ob + align_up((size_t)nq * sizeof(int2), 256);
+  const size_t need = od + align_up((size_t)nq * sizeof(int2), 256);
+  if (need > c->align_bytes) {
+    const tvl1_status r = arena_alloc(c, &c->align_scratch, &c->align_bytes, need, st);
+    if (r != TVL1_OK) return r;
+  }
+  char *b = c->align_scratch;
+  uint32_t *dq = (uint32_t *)(b + oq), *dt = (uint32_t *)(b + ot);
+  Top2 *part = (Top2 *)(b + op);
+  int2 *best = (int2 *)(b + ob), *dd = (int2 *)(b + od);
+  HIP_TRY(c, hipMemcpyAsync(dq, query, (size_t)nq * 32, hipMemcpyHostToDevice, st));
+  if (nt > 0) HIP_TRY(c, hipMemcpyAsync(dt, train, (size_t)nt * 32, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(ka_match2, dim3((nq + 63) / 64, nseg), dim3(64), 0, st, dq, nq, dt, nt, seg, part);
+  hipLaunchKernelGGL(ka_match2_merge, dim3((nq + 255) / 256), dim3(256), 0, st, part, nq, nseg, best, dd);
+  HIP_TRY(c, hipGetLastError());
+  static_assert(sizeof(int2) == 2 * sizeof(int32_t), "int2 layout");
+  HIP_TRY(c, hipMemcpyAsync(idx, best, (size_t)nq * sizeof(int2), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(dist, dd, (size_t)nq * sizeof(int2), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
   return TVL1_OK;
 }
 

@@ -18,7 +18,7 @@ REPO_ROOT = PKG_ROOT.parent
 ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
 
 TVL1_MAX_LEVELS = 32
-ABI_VERSION = 6          # TVL1_ABI_VERSION of include/tvl1.h
+ABI_VERSION = 7          # TVL1_ABI_VERSION of include/tvl1.h
 STATUS = {0: "TVL1_OK", 1: "TVL1_EINVAL", 2: "TVL1_ESIZE", 3: "TVL1_EHIP",
           4: "TVL1_ENOMEM", 5: "TVL1_ENODEV"}
 
@@ -177,6 +177,13 @@ def load_engine() -> C.CDLL:
                                         C.POINTER(TVL1AlignParams), C.POINTER(C.c_float),
                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_void_p]
     lib.tvl1_find_alignment.restype = C.c_int
+    lib.tvl1_orb_detect.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
+                                    C.POINTER(TVL1AlignParams), C.c_void_p, C.c_void_p, C.c_int32,
+                                    C.POINTER(C.c_int32), C.c_void_p]
+    lib.tvl1_orb_detect.restype = C.c_int
+    lib.tvl1_match_knn2.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                                    C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.tvl1_match_knn2.restype = C.c_int
     lib.tvl1_warp_affine_u8.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
                                         C.c_void_p, C.c_size_t, C.c_int32, C.c_int32,
                                         C.POINTER(C.c_float), C.c_void_p]
@@ -214,6 +221,15 @@ def load_engine() -> C.CDLL:
 
 class TVL1Error(RuntimeError):
     pass
+
+
+def align_params(lib, **kw) -> TVL1AlignParams:
+    """tvl1_align_params_default (orb_defaults, features.cpp:19-31) with overrides."""
+    ap = TVL1AlignParams()
+    lib.tvl1_align_params_default(C.byref(ap))
+    for k, v in kw.items():
+        setattr(ap, k, v)
+    return ap
 
 
 class Engine:
@@ -325,10 +341,7 @@ class Engine:
                        w0: int, h0: int, **kw):
         """tvl1_find_alignment(frame1, frame0) on device frames -> (affine (2, 3), n_good,
         outcome)."""
-        ap = TVL1AlignParams()
-        self.lib.tvl1_align_params_default(C.byref(ap))
-        for k, v in kw.items():
-            setattr(ap, k, v)
+        ap = align_params(self.lib, **kw)
         aff = (C.c_float * 6)()
         ng, oc = C.c_int32(0), C.c_int32(0)
         rc = self.lib.tvl1_find_alignment(self.ctx, C.c_void_p(d1), pitch1, w1, h1, C.c_void_p(d0),
@@ -336,6 +349,30 @@ class Engine:
                                           C.byref(oc), None)
         self._check(rc, "tvl1_find_alignment")
         return np.array(list(aff), np.float32).reshape(2, 3), int(ng.value), int(oc.value)
+
+    def orb_detect(self, d: int, pitch: int, w: int, h: int, cap: int = 10000, **kw):
+        """tvl1_orb_detect on a device frame -> (kp (n, 5): x, y, octave, angle, response;
+        desc (n, 32) u8)."""
+        ap = align_params(self.lib, **kw)
+        kp = np.zeros((cap, 5), np.float32)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int32(0)
+        self._check(self.lib.tvl1_orb_detect(self.ctx, C.c_void_p(d), pitch, w, h, C.byref(ap),
+                                             kp.ctypes.data, desc.ctypes.data, cap, C.byref(n),
+                                             None), "tvl1_orb_detect")
+        m = min(n.value, cap)
+        return kp[:m], desc[:m]
+
+    def match_knn2(self, query: np.ndarray, train: np.ndarray):
+        """tvl1_match_knn2 on host descriptor arrays (n, 32) u8 -> (idx (nq, 2), dist (nq, 2))."""
+        q = np.ascontiguousarray(query, np.uint8)
+        t = np.ascontiguousarray(train, np.uint8)
+        idx = np.zeros((len(q), 2), np.int32)
+        dist = np.zeros((len(q), 2), np.int32)
+        self._check(self.lib.tvl1_match_knn2(self.ctx, q.ctypes.data, len(q), t.ctypes.data,
+                                             len(t), idx.ctypes.data, dist.ctypes.data, None),
+                    "tvl1_match_knn2")
+        return idx, dist
 
     def warp_affine_u8(self, src: int, sp: int, sw: int, sh: int, dst: int, dp: int, dw: int,
                        dh: int, affine) -> None:

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TVL1_ABI_VERSION 6
+#define TVL1_ABI_VERSION 7
 #define TVL1_MAX_LEVELS 32
 
 typedef enum tvl1_status {
@@ -194,6 +194,28 @@ tvl1_status tvl1_find_alignment(tvl1_ctx *ctx,
                                 const uint8_t *frame0, size_t pitch0, int32_t w0, int32_t h0,
                                 const tvl1_align_params *params, float affine[6],
                                 int32_t *n_good, int32_t *outcome, void *stream);
+
+/* The two stages of tvl1_find_alignment as calls of their own (ABI 7):
+ *
+ * cv::cuda::ORB::detectAndCompute(frame, noArray(), keypoints, descriptors)
+ * (features.cpp:56-61) of one device u8 frame: the keypoints tvl1_find_alignment uses, levels
+ * in order, best response first within a level.  kp: 5 floats per keypoint -- x, y (level-0
+ * px, cv::KeyPoint::pt), octave (the pyramid level), angle (degrees in [0, 360)), response;
+ * desc: 32 bytes per keypoint (rBRIEF, 256 bits, bit j of byte k = test 8k + j).  Host
+ * outputs for up to cap keypoints; *n = how many were found (may exceed cap: the first cap
+ * are written).  Synchronous on stream. */
+tvl1_status tvl1_orb_detect(tvl1_ctx *ctx, const uint8_t *frame, size_t pitch, int32_t w,
+                            int32_t h, const tvl1_align_params *params, float *kp,
+                            uint8_t *desc, int32_t cap, int32_t *n, void *stream);
+
+/* cv::cuda::DescriptorMatcher::createBFMatcher(NORM_HAMMING)->knnMatch(query, train, k = 2)
+ * (features.cpp:97-104) on host descriptor lists (32 bytes each), on the GPU: for query i,
+ * idx[2i], idx[2i+1] = the nearest and second-nearest train index (ties: the lower index;
+ * -1, with distance 2^30, where the train set has no such descriptor), dist[2i], dist[2i+1]
+ * = their Hamming distances.  Synchronous on stream. */
+tvl1_status tvl1_match_knn2(tvl1_ctx *ctx, const uint8_t *query, int32_t nq,
+                            const uint8_t *train, int32_t nt, int32_t *idx, int32_t *dist,
+                            void *stream);
 
 /* cv::findHomography(src, dst, method, ransacReprojThreshold) on host point lists
  * (features.cpp:131-133; the model tvl1_find_alignment fits): method 8 = RANSAC, 4 = LMEDS,

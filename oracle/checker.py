@@ -72,3 +72,92 @@ def oracle_calc(I0: np.ndarray, I1: np.ndarray, params: TVL1Params | None = None
     if wi is not None:
         wi = wi[: sd["levels"] * params.warps].reshape(sd["levels"], params.warps)
     return u, v, sd, wi
+
+
+# ---- feature pre-alignment restatement (oracle/tvl1_oracle_align.c)
+def _align_params(**kw):
+    from optflow_amd import capi
+    return capi.align_params(capi.load_engine(), **kw)   # tvl1_align_params_default + kw
+
+
+def oracle_orb_detect(img: np.ndarray, cap: int = 10000, **kw):
+    """orc_orb_detect on a host u8 frame -> (kp (n, 5), desc (n, 32))."""
+    lib = load_oracle()
+    a = np.ascontiguousarray(img, np.uint8)
+    h, w = a.shape
+    kp = np.zeros((cap, 5), np.float32)
+    desc = np.zeros((cap, 32), np.uint8)
+    ap = _align_params(**kw)
+    lib.orc_orb_detect.restype = C.c_int
+    n = lib.orc_orb_detect(a.ctypes.data_as(C.c_void_p), C.c_size_t(w), w, h, C.byref(ap),
+                           kp.ctypes.data_as(C.c_void_p), desc.ctypes.data_as(C.c_void_p), cap)
+    if n < 0:
+        raise TVL1Error("oracle: orb_detect out of memory")
+    m = min(n, cap)
+    return kp[:m], desc[:m]
+
+
+def oracle_match_knn2(query: np.ndarray, train: np.ndarray):
+    lib = load_oracle()
+    q = np.ascontiguousarray(query, np.uint8)
+    t = np.ascontiguousarray(train, np.uint8)
+    idx = np.zeros((len(q), 2), np.int32)
+    dist = np.zeros((len(q), 2), np.int32)
+    lib.orc_match_knn2(q.ctypes.data_as(C.c_void_p), len(q), t.ctypes.data_as(C.c_void_p), len(t),
+                       idx.ctypes.data_as(C.c_void_p), dist.ctypes.data_as(C.c_void_p))
+    return idx, dist
+
+
+def oracle_find_homography(src: np.ndarray, dst: np.ndarray, method: int = 8,
+                           thresh: float = 5.0):
+    lib = load_oracle()
+    a = np.ascontiguousarray(src, np.float64)
+    b = np.ascontiguousarray(dst, np.float64)
+    H = np.zeros(9, np.float64)
+    mask = np.zeros(len(a), np.uint8)
+    lib.orc_find_homography.restype = C.c_int
+    ok = lib.orc_find_homography(a.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p),
+                                 len(a), method, C.c_double(thresh), H.ctypes.data_as(C.c_void_p),
+                                 mask.ctypes.data_as(C.c_void_p))
+    return bool(ok), H.reshape(3, 3), mask.astype(bool)
+
+
+def oracle_find_alignment(frame1: np.ndarray, frame0: np.ndarray, **kw):
+    """orc_find_alignment(frame1, frame0) -> (affine (2, 3) f32, n_good, outcome)."""
+    lib = load_oracle()
+    f1 = np.ascontiguousarray(frame1, np.uint8)
+    f0 = np.ascontiguousarray(frame0, np.uint8)
+    ap = _align_params(**kw)
+    aff = np.zeros(6, np.float32)
+    ng, oc = C.c_int(0), C.c_int(0)
+    rc = lib.orc_find_alignment(f1.ctypes.data_as(C.c_void_p), C.c_size_t(f1.shape[1]),
+                                f1.shape[1], f1.shape[0], f0.ctypes.data_as(C.c_void_p),
+                                C.c_size_t(f0.shape[1]), f0.shape[1], f0.shape[0], C.byref(ap),
+                                aff.ctypes.data_as(C.c_void_p), C.byref(ng), C.byref(oc))
+    if rc != 0:
+        raise TVL1Error("oracle: find_alignment out of memory")
+    return aff.reshape(2, 3), int(ng.value), int(oc.value)
+
+
+def oracle_warp_affine_u8(src: np.ndarray, dw: int, dh: int, M) -> np.ndarray:
+    lib = load_oracle()
+    s = np.ascontiguousarray(src, np.uint8)
+    d = np.zeros((dh, dw), np.uint8)
+    m = np.ascontiguousarray(np.asarray(M, np.float32).ravel())
+    lib.orc_warp_affine_u8(s.ctypes.data_as(C.c_void_p), C.c_size_t(s.shape[1]), s.shape[1],
+                           s.shape[0], d.ctypes.data_as(C.c_void_p), C.c_size_t(dw), dw, dh,
+                           m.ctypes.data_as(C.c_void_p))
+    return d
+
+
+def oracle_postprocess_affine(u: np.ndarray, v: np.ndarray, I1: np.ndarray, flow_output: int, M):
+    lib = load_oracle()
+    uu = np.array(u, np.float32, copy=True, order="C")
+    vv = np.array(v, np.float32, copy=True, order="C")
+    i1 = np.ascontiguousarray(I1, np.uint8)
+    H, W = uu.shape
+    m = np.ascontiguousarray(np.asarray(M, np.float32).ravel())
+    lib.orc_postprocess_affine(uu.ctypes.data_as(C.c_void_p), vv.ctypes.data_as(C.c_void_p),
+                               C.c_size_t(4 * W), i1.ctypes.data_as(C.c_void_p), C.c_size_t(W), W,
+                               H, int(flow_output), m.ctypes.data_as(C.c_void_p))
+    return uu, vv

@@ -95,6 +95,27 @@ int orc_tvl1_calc_f32(const tvl1_params *params, const float *I0, size_t pitch0,
 void orc_postprocess(float *u, float *v, size_t flow_pitch, const uint8_t *I1, size_t pitch1,
                      int w, int h, int mode);
 
+/* ---- feature pre-alignment: this build's pipeline restated
+ * (tvl1_oracle_align.c; the contracts of tvl1_orb_detect, tvl1_match_knn2,
+ * tvl1_find_alignment, tvl1_warp_affine_u8 and tvl1_postprocess_affine in include/tvl1.h) */
+/* keypoints (5 floats each: x, y, octave, 0 (angle not restated), response) and 32-byte
+ * descriptors of up to cap keypoints; returns how many were found (-1 on no memory) */
+int orc_orb_detect(const uint8_t *img, size_t pitch, int w, int h, const tvl1_align_params *ap,
+                   float *kp, uint8_t *desc, int cap);
+void orc_match_knn2(const uint8_t *query, int nq, const uint8_t *train, int nt, int32_t *idx,
+                    int32_t *dist);
+/* 1 when a model was found; src / dst: n (x, y) pairs in double */
+int orc_find_homography(const double *src_xy, const double *dst_xy, int n, int method,
+                        double thresh, double H[9], uint8_t *mask);
+int orc_find_alignment(const uint8_t *frame1, size_t pitch1, int w1, int h1,
+                       const uint8_t *frame0, size_t pitch0, int w0, int h0,
+                       const tvl1_align_params *ap, float affine[6], int *n_good,
+                       int *outcome);
+void orc_warp_affine_u8(const uint8_t *src, size_t sp, int sw, int sh, uint8_t *dst, size_t dp,
+                        int dw, int dh, const float affine[6]);
+void orc_postprocess_affine(float *u, float *v, size_t flow_pitch, const uint8_t *I1,
+                            size_t pitch1, int w, int h, int flow_output, const float affine[6]);
+
 /* number of OpenMP threads the oracle uses (1 when built without OpenMP) */
 int orc_num_threads(void);
 void orc_set_num_threads(int n);
