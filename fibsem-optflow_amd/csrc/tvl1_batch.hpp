@@ -95,8 +95,9 @@ __global__ __launch_bounds__(64 * NW) void kb_warp_ring(BatchRing br) {
 }
 
 // K5 + the warp's first pass (2 iterations ending in the first check) fused, as
-// k_warp_iter (warp_iter_body), on each selected pair (blockIdx.y = entry of sel).  The
-// warp constants are always stored (pairs that continue read them in later passes).
+// k_warp_iter (warp_iter_body; NC consumer wavefronts), on each selected pair (blockIdx.y =
+// entry of sel).  The warp constants are always stored (pairs that continue read them in
+// later passes).
 struct BatchWI {
   WarpIterArgs w;            // geometry and scalars; pointers set per pair
   const float *I0, *I1;      // level s images of pair 0 (pair stride ips)
@@ -108,10 +109,11 @@ struct BatchWI {
   int nblk;
   BatchSel sel;
 };
-template <int M, int FM>
-__global__ __launch_bounds__(192) void kb_warp_iter(BatchWI bw) {
+template <int M, int FM, int NC = 2>
+__global__ __launch_bounds__(64 * NC + 128) void kb_warp_iter(BatchWI bw) {
   __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, 128>()];
   __shared__ float cring[2 * 5 * 128];
+  __shared__ float hring[NC == 2 ? 2 * kWiH * 128 : 1];
   const int b = bw.sel.idx[blockIdx.y];
   WarpIterArgs w = bw.w;
   IterArgs &a = w.ra.it;
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(192) void kb_warp_iter(BatchWI bw) {
   }
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves) return;
-  warp_iter_body<M, FM, 128>(w, wid, ring, cring);
+  warp_iter_body<M, FM, 128, 0, NC>(w, wid, ring, cring, hring);
 }
 
 // K6+K8(+K7 partials): one pass of K iterations as a k_iterate_roll<false, K, PX> wavefront

@@ -1533,8 +1533,11 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         wi.sel.pbit = pbit;
         wi.sel.pzero = pzero;
         const size_t tkw = prof_begin(c, st);
-#define KB_WITER(FM) \
-  hipLaunchKernelGGL((kb_warp_iter<6, FM>), dim3(wi.w.ra.waves, n), dim3(192), 0, st, wi);
+#define KB_WITER(FM)                                                                             \
+  if (c->wi_nc == 2)                                                                            \
+    hipLaunchKernelGGL((kb_warp_iter<6, FM, 2>), dim3(wi.w.ra.waves, n), dim3(256), 0, st, wi); \
+  else                                                                                          \
+    hipLaunchKernelGGL((kb_warp_iter<6, FM, 1>), dim3(wi.w.ra.waves, n), dim3(192), 0, st, wi);
         MATH_SWITCH(math, KB_WITER)
 #undef KB_WITER
         if (tkw) {   // k_warp_iter's accounting per pair (constants always stored), x n
