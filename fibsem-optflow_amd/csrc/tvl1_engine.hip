@@ -98,9 +98,10 @@ struct tvl1_ctx {
   size_t buf_limit = ((size_t)1 << 31) - 4096;   // TVL1_BUF_LIMIT: plane bytes the
                              // buffer-addressed kernels take (tests force the fallbacks)
   int fuse = 1;              // TVL1_FUSE=0: no k_warp_iter (warp + first pass as two kernels)
-  long fuse_min = 5000000;   // TVL1_FUSE_MIN: k_warp_iter on levels of >= this many px; smaller
+  long fuse_min = 4000000;   // TVL1_FUSE_MIN: k_warp_iter on levels of >= this many px; smaller
                              // levels: k_warp_ring + the pass (as fast, and their warps mostly
-                             // run past the first check)
+                             // run past the first check).  4 M since the two-consumer form
+                             // (C2's 4.2 Mpx level 4: one pair alone -3.7 %, in flight +0.3 %)
   int witer_slots = 0;       // resident k_warp_iter<6, -, 128, 1, wi_nc> blocks per device
   int wi_nc = 2;             // TVL1_WI_NC: k_warp_iter consumer wavefronts (2: one per
                              // iteration of the pass; 1: both on one wave)

@@ -530,7 +530,7 @@ __device__ __forceinline__ void lds_barrier() {
 #ifdef TVL1_BARRIER_PROBE
   const unsigned long long dt = __builtin_amdgcn_s_memtime() - t0;
   if ((threadIdx.x & 63) == 0)
-    __hip_atomic_fetch_add(tvl1_probe_bar + 3 * blockIdx.x + (threadIdx.x >> 6), dt,
+    __hip_atomic_fetch_add(tvl1_probe_bar + (blockDim.x >> 6) * blockIdx.x + (threadIdx.x >> 6), dt,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
 }
@@ -1872,7 +1872,10 @@ struct WiLane {
   bool outc;
 };
 
-template <int M, int FM, int BW>
+// THP: the producer also does the first iteration's TH step and the C ring carries v (one
+// consumer wavefront); otherwise it carries u^0 and stage 1's wavefront does the step (two
+// consumers, where the producers set the block's pace: 1.5 % faster, tools/wi_probe.hip)
+template <int M, int FM, int BW, bool THP = true>
 __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__restrict__ cring,
                                              const WarpRowI &cur, WarpRowI &ahead,
                                              const WarpRingArgs &wa, const WarpIterArgs &w,
@@ -1920,8 +1923,8 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
   const float rh = rho_c<FM>(I1wv, I1wxv, I1wyv, cur.u1, cur.u2, cur.i0);
   // the first iteration's TH step is pointwise: the producer does it (the consumer sets
   // the block's pace), and the C ring carries v = u^0 + d instead of u^0
-  float v1, v2, v3;
-  th_px<false, FM>(I1wxv, I1wyv, rh, cur.u1, cur.u2, 0.0f, w.ra.it, v1, v2, v3);
+  float v1 = cur.u1, v2 = cur.u2, v3;
+  if (THP) th_px<false, FM>(I1wxv, I1wyv, rh, cur.u1, cur.u2, 0.0f, w.ra.it, v1, v2, v3);
   float *c = cring + (g & 1) * (5 * BW) + P.ci;
   c[0] = I1wxv;
   c[BW] = I1wyv;
@@ -1984,8 +1987,9 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
 // k_iterate_roll<false, 2, 2> pipeline run on two wavefronts, each over the whole band (so
 // the x-neighbours stay DPP shifts inside the wave), stage 2 one step behind stage 1.  They
 // evaluate exactly roll_advance's operations on exactly its operands; only the wave doing
-// them changes.  Stage 1 also does iteration 2's TH step (pointwise on u^1 and the row's
-// constants: estimate_u_px = th_px then u_from_v), so the steps balance (~250 / ~180).
+// them changes.  Stage 1 also does both TH steps (pointwise: iteration 1's on u^0, which the
+// producers then pass instead of v, and iteration 2's on u^1; estimate_u_px = th_px then
+// u_from_v), which leaves the producers' gather as the shortest critical path measured.
 // Hand-off ring (LDS, 2 slots of kWiH planes x BW floats): for input row r, stage 1 writes
 // v^2(r) (u^1(r) + TH step), u^1(r) (the residual's old u) and p^1(r-1); stage 2 reads the
 // slot one barrier later.  A slot is overwritten two steps after it was written, after the
@@ -2031,7 +2035,7 @@ __device__ __forceinline__ void lds_get(float (&v)[PX], const float *__restrict_
 
 // Stage 1 at input row r: u^1(r) = v(r) + theta div p^0 (roll_advance's VIN stage 1),
 // p^1(r-1) from u^1(r-1), u^1(r) and p^0(r-1), and iteration 2's TH step on u^1(r).
-template <int FM, int PX>
+template <int FM, int PX, bool THP = true>
 __device__ __forceinline__ void wi_s1_step(WiS1<PX> &S, const float *__restrict__ cring,
                                            float *__restrict__ hring, const WiP<PX> &cur,
                                            WiP<PX> &ahead, const IterArgs &a, const RollBufs &B,
@@ -2045,8 +2049,15 @@ __device__ __forceinline__ void wi_s1_step(WiS1<PX> &S, const float *__restrict_
   lds_get<PX>(wx, c);
   lds_get<PX>(wy, c + BW);
   lds_get<PX>(rh, c + 2 * BW);
-  lds_get<PX>(v1, c + 3 * BW);
+  lds_get<PX>(v1, c + 3 * BW);   // v = u^0 + TH step, or u^0 (!THP: the step is done here)
   lds_get<PX>(v2, c + 4 * BW);
+  if (!THP) {
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      float t3;
+      th_px<false, FM>(wx[j], wy[j], rh[j], v1[j], v2[j], 0.0f, a, v1[j], v2[j], t3);
+    }
+  }
   const bool z = a.p_zero;
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
@@ -2157,6 +2168,7 @@ __device__ __forceinline__ void wi_s2_step(WiS2<PX> &S, const float *__restrict_
   }
 }
 
+// NC = 2 also moves the first iteration's TH step from the producers to stage 1's wavefront
 template <int M, int FM, int BW, int PRIO = 0, int NC = 1>
 __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, float *__restrict__ ring,
                                                float *__restrict__ cring,
@@ -2208,9 +2220,9 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
       lds_barrier();   // the producers' first step (row r0)
       for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
         progress_prio<PRIO>(h, thirds);
-        wi_s1_step<FM, PX>(S, cring, hring, A, C, a, Bf, r, L, lane, rowb);
-        wi_s1_step<FM, PX>(S, cring, hring, B, A, a, Bf, r + 1, L, lane, rowb);
-        wi_s1_step<FM, PX>(S, cring, hring, C, B, a, Bf, r + 2, L, lane, rowb);
+        wi_s1_step<FM, PX, false>(S, cring, hring, A, C, a, Bf, r, L, lane, rowb);
+        wi_s1_step<FM, PX, false>(S, cring, hring, B, A, a, Bf, r + 1, L, lane, rowb);
+        wi_s1_step<FM, PX, false>(S, cring, hring, C, B, a, Bf, r + 2, L, lane, rowb);
       }
       lds_barrier();
       lds_barrier();
@@ -2341,9 +2353,10 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     warp_flow_load(B, wa, nb, rowb, r0 + 1, P.xcb);
     for (int h = 0, g = r0; h <= thirds; ++h, g += 3) {
       progress_prio<PRIO>(h, thirds);
-      wi_prod_step<M, FM, BW>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
-      wi_prod_step<M, FM, BW>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
-      wi_prod_step<M, FM, BW>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
+      constexpr bool THP = NC == 1;
+      wi_prod_step<M, FM, BW, THP>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM, BW, THP>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM, BW, THP>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
     }
   }
 }

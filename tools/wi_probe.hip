@@ -35,7 +35,10 @@ using namespace tvl1k;
 #ifndef WI_M
 #define WI_M 6
 #endif
-constexpr int M = WI_M, BW = WI_BW;
+#ifndef WI_NC
+#define WI_NC 2
+#endif
+constexpr int M = WI_M, BW = WI_BW, NC = WI_NC, NWV = NC + BW / 64;   // waves per block
 
 #ifdef WI_WPE
 #define WI_ATTR __attribute__((amdgpu_waves_per_eu(WI_WPE)))
@@ -43,19 +46,20 @@ constexpr int M = WI_M, BW = WI_BW;
 #define WI_ATTR
 #endif
 template <int FM, int PRIO>
-__global__ __launch_bounds__(64 + BW) WI_ATTR void k_probe(WarpIterArgs w, unsigned long long *ts) {
+__global__ __launch_bounds__(64 * NC + BW) WI_ATTR void k_probe(WarpIterArgs w, unsigned long long *ts) {
   __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, BW>()];
   __shared__ float cring[2 * 5 * BW];
+  __shared__ float hring[NC == 2 ? 2 * kWiH * BW : 1];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves) return;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-  warp_iter_body<M, FM, BW, PRIO>(w, wid, ring, cring);
+  warp_iter_body<M, FM, BW, PRIO, NC>(w, wid, ring, cring, hring);
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long c1 = __builtin_amdgcn_s_memtime();
 #ifdef WI_BARRIER
   if ((threadIdx.x & 63) == 0)
-    __hip_atomic_fetch_add(tvl1_probe_bar + 3 * (size_t)gridDim.x + 3 * blockIdx.x + (threadIdx.x >> 6),
+    __hip_atomic_fetch_add(tvl1_probe_bar + NWV * (size_t)gridDim.x + NWV * blockIdx.x + (threadIdx.x >> 6),
                            c1 - c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
   (void)c0;
@@ -65,7 +69,7 @@ __global__ __launch_bounds__(64 + BW) WI_ATTR void k_probe(WarpIterArgs w, unsig
   const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
   const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    unsigned long long *o = ts + 4 * (3 * (size_t)blockIdx.x + wv);
+    unsigned long long *o = ts + 4 * (NWV * (size_t)blockIdx.x + wv);
     o[0] = t0;
     o[1] = t1;
     o[2] = hw;
@@ -154,7 +158,7 @@ int main(int argc, char **argv) {
   if (mode >= 2) a.P = 0;
 
   int per_cu = 0, cus = 0;
-  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_probe<0, 0>, 64 + BW, 0));
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_probe<0, 0>, 64 * NC + BW, 0));
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int slots = per_cu * cus;
   w.ra.bands = (W + BW - 5) / (BW - 4);
@@ -165,9 +169,9 @@ int main(int argc, char **argv) {
          w.ra.seg_rows, w.ra.waves, slots, per_cu);
   if (w.ra.waves > maxblk) return 1;
   unsigned long long *ts;
-  CK(hipMalloc(&ts, (size_t)w.ra.waves * 3 * 4 * sizeof(unsigned long long)));
+  CK(hipMalloc(&ts, (size_t)w.ra.waves * NWV * 4 * sizeof(unsigned long long)));
   unsigned long long *bar;
-  const size_t nbar = (size_t)w.ra.waves * 3 * 2;
+  const size_t nbar = (size_t)w.ra.waves * NWV * 2;
   CK(hipMalloc(&bar, nbar * 8));
 #ifdef WI_BARRIER
   CK(hipMemcpyToSymbol(HIP_SYMBOL(tvl1_probe_bar), &bar, sizeof(bar)));
@@ -182,11 +186,11 @@ int main(int argc, char **argv) {
       CK(hipEventRecord(e0));
       CK(hipMemset(bar, 0, nbar * 8));
       if (probe && prio)
-        hipLaunchKernelGGL((k_probe<0, 1>), dim3(w.ra.waves), dim3(64 + BW), 0, 0, w, ts);
+        hipLaunchKernelGGL((k_probe<0, 1>), dim3(w.ra.waves), dim3(64 * NC + BW), 0, 0, w, ts);
       else if (probe)
-        hipLaunchKernelGGL((k_probe<0, 0>), dim3(w.ra.waves), dim3(64 + BW), 0, 0, w, ts);
+        hipLaunchKernelGGL((k_probe<0, 0>), dim3(w.ra.waves), dim3(64 * NC + BW), 0, 0, w, ts);
       else
-        hipLaunchKernelGGL((k_warp_iter<M, 0, BW, 1>), dim3(w.ra.waves), dim3(64 + BW), 0, 0, w);
+        hipLaunchKernelGGL((k_warp_iter<M, 0, BW, 1, NC>), dim3(w.ra.waves), dim3(64 * NC + BW), 0, 0, w);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
@@ -200,13 +204,13 @@ int main(int argc, char **argv) {
   run(false);
   for (prio = 0; prio < 2; ++prio) {
   run(true);
-  std::vector<unsigned long long> t((size_t)w.ra.waves * 12);
+  std::vector<unsigned long long> t((size_t)w.ra.waves * 4 * NWV);
   CK(hipMemcpy(t.data(), ts, t.size() * 8, hipMemcpyDeviceToHost));
   int rate_khz = 0;
   CK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
   const double us = 1e3 / rate_khz;
   unsigned long long t0 = ~0ull, t1 = 0;
-  for (int i = 0; i < w.ra.waves * 3; ++i) {
+  for (int i = 0; i < w.ra.waves * NWV; ++i) {
     t0 = std::min(t0, t[4 * i]);
     t1 = std::max(t1, t[4 * i + 1]);
   }
@@ -214,9 +218,11 @@ int main(int argc, char **argv) {
   std::vector<double> st, en, life;
   std::vector<double> xe(8, 0.0), xn(8, 0.0);
   for (int bl = 0; bl < w.ra.waves; ++bl) {
-    const unsigned long long *o = &t[12 * bl];
+    const unsigned long long *o = &t[4 * NWV * bl];
     st.push_back((o[0] - t0) * us);
-    en.push_back((std::max({o[1], o[5], o[9]}) - t0) * us);
+    unsigned long long e = 0;
+    for (int v = 0; v < NWV; ++v) e = std::max(e, o[4 * v + 1]);
+    en.push_back((e - t0) * us);
     life.push_back((o[1] - o[0]) * us);
     const int x = (int)(o[3] & 7);
     xe[x] += en.back();
@@ -243,12 +249,12 @@ int main(int argc, char **argv) {
     const int cu = (hw >> 8) & 15, sh = (hw >> 12) & 1, se = (hw >> 13) & 7;
     return (((int)(o[3] & 7) * 8 + se) * 2 + sh) * 16 + cu;
   };
-  for (int bl = 0; bl < w.ra.waves; ++bl) cnt[cu_key(&t[12 * bl])]++;
+  for (int bl = 0; bl < w.ra.waves; ++bl) cnt[cu_key(&t[4 * NWV * bl])]++;
   std::vector<double> eb(8, 0.0), nb(8, 0.0);
   int used = 0;
   for (int c : cnt) used += c > 0;
   for (int bl = 0; bl < w.ra.waves; ++bl) {
-    const int c = std::min(cnt[cu_key(&t[12 * bl])], 7);
+    const int c = std::min(cnt[cu_key(&t[4 * NWV * bl])], 7);
     eb[c] += en[bl];
     nb[c] += 1;
   }
@@ -259,11 +265,11 @@ int main(int argc, char **argv) {
   auto simd_key = [&](const unsigned long long *o) { return cu_key(o) * 4 + (int)((o[2] >> 4) & 3); };
   std::vector<int> scons(8 * 64 * 16 * 4, 0), sprod(8 * 64 * 16 * 4, 0);
   for (int bl = 0; bl < w.ra.waves; ++bl)
-    for (int v = 0; v < 3; ++v) (v == 0 ? scons : sprod)[simd_key(&t[12 * bl + 4 * v])]++;
+    for (int v = 0; v < NWV; ++v) (v < NC ? scons : sprod)[simd_key(&t[4 * NWV * bl + 4 * v])]++;
   {
     double acc[8][8] = {}, n[8][8] = {};
     for (int bl = 0; bl < w.ra.waves; ++bl) {
-      const int k = simd_key(&t[12 * bl]);
+      const int k = simd_key(&t[4 * NWV * bl]);
       const int c = std::min(scons[k], 7), pr = std::min(sprod[k], 7);
       acc[c][pr] += life[bl];
       n[c][pr] += 1;
@@ -275,8 +281,8 @@ int main(int argc, char **argv) {
     double accm[8] = {}, nm[8] = {};
     for (int bl = 0; bl < w.ra.waves; ++bl) {
       int mx = 0;
-      for (int v = 0; v < 3; ++v) {
-        const int k = simd_key(&t[12 * bl + 4 * v]);
+      for (int v = 0; v < NWV; ++v) {
+        const int k = simd_key(&t[4 * NWV * bl + 4 * v]);
         mx = std::max(mx, 2 * scons[k] + sprod[k]);
       }
       mx = std::min(mx, 7);
@@ -306,27 +312,28 @@ int main(int argc, char **argv) {
   }
   // simd placement of the three waves of each block
   std::vector<int> sim(4, 0);
-  for (int i = 0; i < w.ra.waves * 3; ++i) sim[(t[4 * i + 2] >> 4) & 3]++;
+  for (int i = 0; i < w.ra.waves * NWV; ++i) sim[(t[4 * i + 2] >> 4) & 3]++;
   printf("waves per simd id: %d %d %d %d\n", sim[0], sim[1], sim[2], sim[3]);
 #ifdef WI_BARRIER
   {  // barrier wait share per role (shader cycles, last repetition)
     std::vector<unsigned long long> hb(nbar);
     CK(hipMemcpy(hb.data(), bar, nbar * 8, hipMemcpyDeviceToHost));
-    double bw[3] = {}, lf[3] = {};
+    double bw[NWV] = {}, lf[NWV] = {};
     for (int bl = 0; bl < w.ra.waves; ++bl)
-      for (int v = 0; v < 3; ++v) {
-        bw[v] += hb[3 * bl + v];
-        lf[v] += hb[3 * (size_t)w.ra.waves + 3 * bl + v];
+      for (int v = 0; v < NWV; ++v) {
+        bw[v] += hb[NWV * bl + v];
+        lf[v] += hb[NWV * (size_t)w.ra.waves + NWV * bl + v];
       }
-    printf("barrier share of wave life: consumer %.3f, producer0 %.3f, producer1 %.3f\n",
-           bw[0] / lf[0], bw[1] / lf[1], bw[2] / lf[2]);
+    printf("barrier share of wave life (waves 0..%d, consumers first):", NWV - 1);
+    for (int v = 0; v < NWV; ++v) printf(" %.3f", bw[v] / lf[v]);
+    printf("\n");
   }
 #endif
   {  // life by dispatch ordinal on the CU (blocks of one CU in blockIdx order)
     std::vector<int> seen(8 * 64 * 16, 0);
     double acc[8] = {}, n[8] = {};
     for (int bl = 0; bl < w.ra.waves; ++bl) {
-      const int o = std::min(seen[cu_key(&t[12 * bl])]++, 7);
+      const int o = std::min(seen[cu_key(&t[4 * NWV * bl])]++, 7);
       acc[o] += life[bl];
       n[o] += 1;
     }
