@@ -3,7 +3,9 @@
 counters (per-dispatch sums / averages).  FETCH_SIZE is doubled per
 MI355X_MICROARCH.md (gfx950 reports 1/2 of the bytes of wide coalesced streams);
 WRITE_SIZE is taken as is.  Both are in KB in rocprofv3's derived counters.
-Usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [kernel-substring ...]
+Usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [kernel-substring ...] [--batch]
+  --batch: the batched kernels of tvl1_calc_batch (kb_iterate_roll + kb_warp_iter as the
+           iteration class, kb_warp_ring as the warp class; tools/pmc_strips.sh)
 """
 import csv
 import glob
@@ -20,7 +22,9 @@ def short(name):
 def main():
     d = sys.argv[1]
     args = [a for a in sys.argv[2:] if not a.startswith("--") and not a.endswith(".json")]
-    want = args or ["k_iterate", "k_warp"]
+    batch = "--batch" in sys.argv
+    pre = "kb_" if batch else "k_"
+    want = args or [pre + "iterate", pre + "warp"]
     rows = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv"))))
     dur = defaultdict(list)
     for r in rows:
@@ -66,10 +70,10 @@ def main():
     # (k_iterate_roll + k_iterate_tb of the hybrid) and every warpBackward
     classes = {}
     # (k_warp_iter, warpBackward fused with a warp's first pass, is an iteration pass)
-    for cls, prefix in (("iterate", "k_iterate"), ("warp", "k_warp")):
-        ks = [k for k in out if k.startswith(prefix) or (cls == "iterate" and k.startswith("k_warp_iter"))]
+    for cls, prefix in (("iterate", pre + "iterate"), ("warp", pre + "warp")):
+        ks = [k for k in out if k.startswith(prefix) or (cls == "iterate" and k.startswith(pre + "warp_iter"))]
         if cls == "warp":
-            ks = [k for k in ks if not k.startswith("k_warp_iter")]
+            ks = [k for k in ks if not k.startswith(pre + "warp_iter")]
         if not ks:
             continue
         n = sum(out[k]["dispatches"] for k in ks)
@@ -100,8 +104,10 @@ def main():
                    "iterate_kernels": it["kernels"], "dispatches": it["dispatches"],
                    "warp_hbm_bytes_per_launch": classes.get("warp", {}).get("hbm_bytes_per_dispatch"),
                    "source": d, "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
-                   "separate passes, average over every iteration-pass dispatch of one pair "
-                   "alone (tools/pmc_single.sh); valu_frac from the SQ_INSTS_VALU pass"},
+                   "separate passes, average over every iteration-pass dispatch of " +
+                   ("one strip batch at a time (tools/pmc_strips.sh)" if batch else
+                    "one pair alone (tools/pmc_single.sh)") +
+                   "; valu_frac from the SQ_INSTS_VALU pass"},
                   open(path, "w"), indent=1)
 
 
