@@ -142,7 +142,10 @@ static size_t prof_begin(tvl1_ctx *c, hipStream_t st) {
   if (c->ev_used + 2 > c->ev_pool.size()) {
     for (int i = 0; i < 64; ++i) {
       hipEvent_t e;
-      if (hipEventCreate(&e) != hipSuccess) break;
+      // timing-only events: no system-scope fence (cache writeback + invalidate) at each
+      // record, which slowed the kernel after it and inflated the per-launch times ~6 %
+      // against the rocprofv3 kernel trace (r3)
+      if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) break;
       c->ev_pool.push_back(e);
     }
   }
