@@ -91,6 +91,10 @@ struct tvl1_ctx {
                                  // levels of at least this many px (2 px below: more waves)
   int roll_slots[kRollMax + 1][2][5] = {};   // resident k_iterate_roll<G, K, PX> wavefronts
   int fill = 100;            // TVL1_FILL: % of the resident slots a single-pair streaming launch
+                             // is sized for while the solve is alone on its device, and
+  int fill_shared = 60;      // TVL1_FILL_SHARED: ... while other solves of this process share
+                             // the device (their blocks take the rest; DESIGN 9: 3 in flight
+                             // +1.8 % at 60 %, and a pair alone keeps its 100 % latency)
                              // is sized for (segment rows)
   long roll_long_min = 0;    // >= 3-iteration passes stream (k_iterate_roll) on levels of at
                              // least this many 56 x 32 tiles, else k_iterate_tb
@@ -116,6 +120,8 @@ struct tvl1_ctx {
   size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
   double *bpartials = nullptr;
   int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
+  int batch_fill = 1;                   // TVL1_BATCH_FILL=0: batched launches always sized
+                                        // for every resident slot
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
   size_t map_bytes = 0;
   char *align_scratch = nullptr;        // tvl1_find_alignment's pyramid, keys, descriptors
@@ -770,6 +776,13 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
   int64_t level_iters[TVL1_MAX_LEVELS] = {};
   int64_t checks = 0;
   int32_t spec_misses = 0;   // speculative launches that ran empty
+  // share of the resident slots a streaming launch is sized for: all of them for a solve
+  // alone on its device, fill_shared while other solves are in progress (their blocks fill
+  // the rest instead of waiting for this launch's last round).  Segmentation never changes
+  // a result (tests/test_gpu_parity.py TVL1_ROLL_SEG cases)
+  auto fill_now = [&]() {
+    return g_solving[c->device & 63].load(std::memory_order_relaxed) > 1 ? c->fill_shared : c->fill;
+  };
 
   // ---- launch helpers
   // The streaming kernels (k_iterate_roll, k_warp_ring, k_warp_iter) take 32-bit buffer
@@ -820,7 +833,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
       wa.P = P;
       wa.bands = (lw + 63) / 64;
       wa.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                    : roll_segment(wa.bands, lh, 6, c->warp_ring_slots * c->fill / 100);
+                                    : roll_segment(wa.bands, lh, 6, c->warp_ring_slots * fill_now() / 100);
       wa.waves = wa.bands * ((lh + wa.seg_rows - 1) / wa.seg_rows);
 #define WARP_RING(FM) \
   hipLaunchKernelGGL((k_warp_ring<6, 2, FM>), dim3(wa.waves), dim3(128), 0, st, wa);
@@ -924,7 +937,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           constexpr int M = 6, BW = 128;
           w.ra.bands = (lw + BW - 5) / (BW - 4);
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                          : roll_segment(w.ra.bands, lh, 2 + M, c->witer_slots * c->fill / 100);
+                                          : roll_segment(w.ra.bands, lh, 2 + M, c->witer_slots * fill_now() / 100);
           w.ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           w.ra.waves = w.ra.bands * segs;
@@ -964,7 +977,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           const int out_w = 64 * px - 2 * halo;
           ra.bands = (lw + out_w - 1) / out_w;
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px] * c->fill / 100);
+                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px] * fill_now() / 100);
           ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           ra.waves = ra.bands * segs;
@@ -1432,6 +1445,13 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
     if (r != TVL1_OK) return r;
   }
   const size_t ps = c->bps;
+  const SolveCount active(c->device);
+  // the single-pair rule for the launch sizes (solve(): fill_now); TVL1_BATCH_FILL=0 sizes
+  // every batched launch for all resident slots
+  auto fill_now = [&]() {
+    return c->batch_fill && g_solving[c->device & 63].load(std::memory_order_relaxed) > 1
+               ? c->fill_shared : c->fill;
+  };
   BatchSel all{};
   all.n = n;
   for (int b = 0; b < n; ++b) all.idx[b] = (uint8_t)b;
@@ -1517,7 +1537,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         wi.w.ra.b = batch_bufs;
         wi.w.ra.it = it;
         wi.w.ra.bands = (lw + 123) / 124;
-        wi.w.ra.seg_rows = roll_segment(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots);
+        wi.w.ra.seg_rows = roll_segment(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots * fill_now() / 100);
         wi.w.ra.waves = wi.w.ra.bands * ((lh + wi.w.ra.seg_rows - 1) / wi.w.ra.seg_rows);
         if (wi.w.ra.waves > c->bnblk)
           return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", wi.w.ra.waves, c->bnblk);
@@ -1654,7 +1674,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           // segments sized so the batch's wavefronts fill whole rounds of resident slots
           br.ra.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
                                            : roll_segment(br.ra.bands * sel.n, lh, K,
-                                                          c->roll_slots[K][0][2]);
+                                                          c->roll_slots[K][0][2] * fill_now() / 100);
           br.ra.waves = br.ra.bands * ((lh + br.ra.seg_rows - 1) / br.ra.seg_rows);
           blocks = br.ra.waves;
           if (blocks > c->bnblk)
@@ -2103,10 +2123,12 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_SPEC_TRACE")) c->spec_trace = atoi(m);
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
   if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_BATCH_FILL")) c->batch_fill = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
   if (const char *m = getenv("TVL1_FILL")) c->fill = std::max(10, atoi(m));
+  if (const char *m = getenv("TVL1_FILL_SHARED")) c->fill_shared = std::max(10, atoi(m));
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void **)&c->pinned, sizeof(double) * (8 + kBatchMax),
