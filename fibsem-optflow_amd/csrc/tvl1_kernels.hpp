@@ -1449,6 +1449,143 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
   tb_iterate_store<G, RH, NG, PX, FM>(t, lds, r, Y, X, c4, rr);
 }
 
+// ---------------------------------------------------------------- K6+K8, tall blocked regions
+// k_iterate_tb4<FM>: one pass of K <= 4 iterations over a 64 x 64 region (4-px x halo, K-row
+// y halo: 56 x (64 - 2K) output px), 512 threads.  Each thread owns 2 px of 4 CONSECUTIVE
+// rows, so the y-neighbours inside its rows are registers and only the rows between two
+// threads go through LDS: the last row's p12 / p22 (estimateU's p at y-1 of the next
+// thread's first row) and the first row's u1 / u2 (the projection's u at y+1 of the
+// previous thread's last row) -- 16 KB, 2 barriers per iteration as in k_iterate_tb, but 8
+// px of work per thread between them.  Against k_iterate_tb's 64 x 32 regions the halo
+// recompute falls from 1.52x to 1.31x at K = 4 (1.41x to 1.26x at K = 3).  Same
+// estimate_u / dual_component arithmetic, so the same bits (the region-edge rows take their
+// own row as the neighbour, as k_iterate_tb's LDS clamp does; no stored cell depends on them).
+constexpr int kTb4Rows = 64, kTb4RowsPerThread = 4, kTb4Groups = kTb4Rows / kTb4RowsPerThread;
+// WPE: 0 = the compiler's register choice (165 VGPRs: one block of 8 waves per CU), 4 = four
+// waves per SIMD (two blocks per CU, 128 VGPRs with spills) -- TVL1_TB4=1 / 2
+template <int FM, int WPE = 0>
+__global__ __launch_bounds__(32 * kTb4Groups, WPE) void k_iterate_tb4(TBArgs t) {
+  constexpr int PX = 2, LPR = 32, NR = kTb4RowsPerThread, NGR = kTb4Groups;
+  constexpr int HALO = 4 / PX;   // lanes of the 4-px x halo
+  using V = float2;
+  __shared__ V lds[4][NGR][LPR];   // [p12 last, p22 last, u1 first, u2 first][group][lane]
+  const IterArgs &a = t.it;
+  if (gated_off(a.gate, a.gate_seq)) return;   // whole grid
+  const int tid = threadIdx.x;
+  const int c4 = tid % LPR;
+  const int q = tid / LPR;                     // row group: region rows NR q .. NR q + NR - 1
+  int bx, by;
+  tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
+  const int K = t.niter;
+  const int xr0 = bx * 56 - 4;
+  const int yr0 = by * t.out_h - K;
+  const int X = xr0 + PX * c4;
+  const int xa = imin(imax(X, 0), a.P - PX);
+  Row<false, PX> r[NR];
+  int Y[NR];
+  bool out_ok[NR];
+#pragma unroll
+  for (int g = 0; g < NR; ++g) {
+    const int row = NR * q + g;
+    Y[g] = yr0 + row;
+    const int ya = imin(imax(Y[g], 0), a.H - 1);
+    load_row<false, PX>(r[g], a, (size_t)ya * a.P + xa);
+    out_ok[g] = c4 >= HALO && c4 < LPR - HALO && row >= K && row < kTb4Rows - K && Y[g] >= 0 &&
+                Y[g] < a.H && X < a.W;
+  }
+  double acc = 0.0;
+  for (int it = 0; it < K; ++it) {
+    const bool last = it == K - 1;
+    // ---- estimateU (p^{n-1} at y-1: the row above in registers, or the previous group's
+    // last row from LDS; u^{n-1} -> u^n in place)
+    lds[0][q][c4] = pack(r[NR - 1].p12);
+    lds[1][q][c4] = pack(r[NR - 1].p22);
+    __syncthreads();
+    float up12[PX], up22[PX], zero3[PX];
+    zerov<PX>(zero3);
+    if (q > 0) {
+      unpack(up12, lds[0][q - 1][c4]);
+      unpack(up22, lds[1][q - 1][c4]);
+    } else {   // region row 0: its own row (k_iterate_tb's clamp)
+#pragma unroll
+      for (int k = 0; k < PX; ++k) up12[k] = r[0].p12[k], up22[k] = r[0].p22[k];
+    }
+    // every row's estimateU reads p of the row above, which no row's estimateU changes
+#pragma unroll
+    for (int g = 0; g < NR; ++g) {
+      float n1[PX], n2[PX], n3[PX];
+      if (g == 0)
+        estimate_u<false, PX, FM>(r[0], up12, up22, zero3, X, Y[0], a, n1, n2, n3);
+      else
+        estimate_u<false, PX, FM>(r[g], r[g - 1].p12, r[g - 1].p22, zero3, X, Y[g], a, n1, n2, n3);
+      if (last && a.calc_err && out_ok[g]) {
+#pragma unroll
+        for (int k = 0; k < PX; ++k)
+          if (X + k < a.W) acc += (double)residual_px<FM>(r[g].u1[k] - n1[k], r[g].u2[k] - n2[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < PX; ++k) {
+        r[g].u1[k] = n1[k];
+        r[g].u2[k] = n2[k];
+      }
+    }
+    // ---- estimateDualVariables (u^n at y+1: the row below, or the next group's first row)
+    lds[2][q][c4] = pack(r[0].u1);
+    lds[3][q][c4] = pack(r[0].u2);
+    __syncthreads();
+    float d1[PX], d2[PX];
+    if (q < NGR - 1) {
+      unpack(d1, lds[2][q + 1][c4]);
+      unpack(d2, lds[3][q + 1][c4]);
+    } else {   // region bottom row: its own row
+#pragma unroll
+      for (int k = 0; k < PX; ++k) d1[k] = r[NR - 1].u1[k], d2[k] = r[NR - 1].u2[k];
+    }
+#pragma unroll
+    for (int g = 0; g < NR; ++g) {
+      const bool has_down = Y[g] + 1 < a.H;
+      float q11[PX], q12[PX], q21[PX], q22[PX];
+      if (g < NR - 1) {
+        dual_component<PX, false, FM>(r[g].u1, r[g + 1].u1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12);
+        dual_component<PX, false, FM>(r[g].u2, r[g + 1].u2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22);
+      } else {
+        dual_component<PX, false, FM>(r[g].u1, d1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12);
+        dual_component<PX, false, FM>(r[g].u2, d2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22);
+      }
+#pragma unroll
+      for (int k = 0; k < PX; ++k) {
+        r[g].p11[k] = q11[k]; r[g].p12[k] = q12[k];
+        r[g].p21[k] = q21[k]; r[g].p22[k] = q22[k];
+      }
+    }
+    // the next iteration's first barrier orders these LDS reads before the rewrite
+  }
+#pragma unroll
+  for (int g = 0; g < NR; ++g) {
+    if (out_ok[g]) {
+      const size_t off = (size_t)Y[g] * a.P + X;
+      stv<PX>(a.u1d, off, r[g].u1);
+      stv<PX>(a.u2d, off, r[g].u2);
+      stv<PX>(a.p11d, off, r[g].p11);
+      stv<PX>(a.p12d, off, r[g].p12);
+      stv<PX>(a.p21d, off, r[g].p21);
+      stv<PX>(a.p22d, off, r[g].p22);
+    }
+  }
+  if (a.calc_err) {
+    __shared__ double red[32 * NGR / kWave];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sum = 0.0;
+      for (int i = 0; i < 32 * NGR / kWave; ++i) sum += red[i];
+      a.partials[blockIdx.x] = sum;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- K6+K8 wavefront pipeline
 // k_iterate_roll<G, K, PX>: K consecutive primal-dual iterations in ONE streaming pass.
 // One wavefront owns a column band of 64*PX px (PX adjacent px per lane) of one row
