@@ -1031,19 +1031,24 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           t.it = a;
           t.niter = k;
           t.tiles_x = (lw + 55) / 56;
-          t.out_h = kTb4Rows - 2 * k;
+          const int nr = c->tb4 >= 3 ? 3 : 4;   // rows per thread
+          t.out_h = kTb4Groups * nr - 2 * k;
           blocks = t.tiles_x * ((lh + t.out_h - 1) / t.out_h);
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
                            c->partials_cap);
-#define TB4_M(FM)                                                                       \
-  if (c->tb4 == 2)                                                                     \
-    hipLaunchKernelGGL((k_iterate_tb4<FM, 4>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t); \
-  else                                                                                 \
-    hipLaunchKernelGGL((k_iterate_tb4<FM, 0>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t);
+#define TB4_M(FM)                                                                            \
+  if (c->tb4 == 2)                                                                          \
+    hipLaunchKernelGGL((k_iterate_tb4<FM, 4, 4>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t); \
+  else if (c->tb4 == 3)                                                                     \
+    hipLaunchKernelGGL((k_iterate_tb4<FM, 3, 4>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t); \
+  else if (c->tb4 == 4)                                                                     \
+    hipLaunchKernelGGL((k_iterate_tb4<FM, 3, 0>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t); \
+  else                                                                                      \
+    hipLaunchKernelGGL((k_iterate_tb4<FM, 4, 0>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t);
           MATH_SWITCH(math, TB4_M)
 #undef TB4_M
-          hbm = (double)blocks * 64.0 * kTb4Rows * 4.0 * ld_planes + Nl * 4.0 * st_planes;
+          hbm = (double)blocks * 64.0 * (kTb4Groups * nr) * 4.0 * ld_planes + Nl * 4.0 * st_planes;
         } else {   // 64 x 32 regions, 2 px per lane
           TBArgs t;
           t.it = a;

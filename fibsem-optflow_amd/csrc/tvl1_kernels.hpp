@@ -1460,12 +1460,13 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
 // recompute falls from 1.52x to 1.31x at K = 4 (1.41x to 1.26x at K = 3).  Same
 // estimate_u / dual_component arithmetic, so the same bits (the region-edge rows take their
 // own row as the neighbour, as k_iterate_tb's LDS clamp does; no stored cell depends on them).
-constexpr int kTb4Rows = 64, kTb4RowsPerThread = 4, kTb4Groups = kTb4Rows / kTb4RowsPerThread;
-// WPE: 0 = the compiler's register choice (165 VGPRs: one block of 8 waves per CU), 4 = four
-// waves per SIMD (two blocks per CU, 128 VGPRs with spills) -- TVL1_TB4=1 / 2
-template <int FM, int WPE = 0>
+constexpr int kTb4Groups = 16;   // row groups (threads per column) of a region
+// NR rows per thread (region 16 NR rows).  WPE: 0 = the compiler's register choice (NR = 4:
+// 165 VGPRs, one block of 8 waves per CU), 4 = four waves per SIMD (two blocks per CU; NR =
+// 4 spills at 128 VGPRs)
+template <int FM, int NR = 4, int WPE = 0>
 __global__ __launch_bounds__(32 * kTb4Groups, WPE) void k_iterate_tb4(TBArgs t) {
-  constexpr int PX = 2, LPR = 32, NR = kTb4RowsPerThread, NGR = kTb4Groups;
+  constexpr int PX = 2, LPR = 32, NGR = kTb4Groups, kTb4Rows = NR * NGR;
   constexpr int HALO = 4 / PX;   // lanes of the 4-px x halo
   using V = float2;
   __shared__ V lds[4][NGR][LPR];   // [p12 last, p22 last, u1 first, u2 first][group][lane]

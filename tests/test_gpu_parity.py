@@ -112,7 +112,7 @@ MODES = ["", "TVL1_ROLL_LONG_MIN=0", "TVL1_ROLL_LONG_MIN=0,TVL1_ROLL_SEG=8", "TV
          "TVL1_FUSE=0,TVL1_ROLL_LONG_MIN=0", "TVL1_BUF_LIMIT=100000", "TVL1_BUF_LIMIT=0",
          "TVL1_POLL=0", "TVL1_POLL=0,TVL1_FUSE_MIN=0", "TVL1_SPEC=0", "TVL1_SPEC=0,TVL1_FUSE_MIN=0",
          "TVL1_FUSE_MIN=0,TVL1_WI_NC=1", "TVL1_FUSE_MIN=0,TVL1_WI_NC=1,TVL1_ROLL_SEG=8",
-         "TVL1_TB4=0", "TVL1_TB4=2", "TVL1_TB4=0,TVL1_BUF_LIMIT=0"]
+         "TVL1_TB4=0", "TVL1_TB4=2", "TVL1_TB4=3", "TVL1_TB4=0,TVL1_BUF_LIMIT=0"]
 # (TVL1_POLL=0: residuals read after an event instead of the poll; TVL1_SPEC=0: nothing
 # enqueued behind a check before the host reads it)
 KNOBS = ("TVL1_ROLL_SEG", "TVL1_ROLL_PX4_MIN", "TVL1_ROLL_LONG_MIN", "TVL1_FUSE", "TVL1_FUSE_MIN",
