@@ -103,7 +103,7 @@ struct tvl1_ctx {
                              // buffer-addressed kernels take (tests force the fallbacks)
   int fuse = 1;              // TVL1_FUSE=0: no k_warp_iter (warp + first pass as two kernels)
   int tb4 = 1;               // TVL1_TB4=0: blocked passes (gamma = 0) in 64 x 32 regions
-                             // (k_iterate_tb) instead of 64 x 64 (k_iterate_tb4)
+                             // (k_iterate_tb) instead of 64 x 48 (k_iterate_tb4)
   long fuse_min = 4000000;   // TVL1_FUSE_MIN: k_warp_iter on levels of >= this many px; smaller
                              // levels: k_warp_ring + the pass (as fast, and their warps mostly
                              // run past the first check).  4 M since the two-consumer form
@@ -1026,26 +1026,19 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
             rows += std::min(ye - 1 + k, lh - 1) - std::max(ys - k, 0) + 1;
           }
           hbm = (double)ra.bands * 64.0 * px * rows * 4.0 * ld_planes + Nl * 4.0 * st_planes;
-        } else if (c->tb4 && !gam) {   // 64 x 64 regions, 4 rows x 2 px per thread
+        } else if (c->tb4 && !gam) {   // 64 x 48 regions, 3 rows x 2 px per thread
           TBArgs t;
           t.it = a;
           t.niter = k;
           t.tiles_x = (lw + 55) / 56;
-          const int nr = c->tb4 >= 3 ? 3 : 4;   // rows per thread
+          constexpr int nr = kTb4RowsPerThread;
           t.out_h = kTb4Groups * nr - 2 * k;
           blocks = t.tiles_x * ((lh + t.out_h - 1) / t.out_h);
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
                            c->partials_cap);
-#define TB4_M(FM)                                                                            \
-  if (c->tb4 == 2)                                                                          \
-    hipLaunchKernelGGL((k_iterate_tb4<FM, 4, 4>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t); \
-  else if (c->tb4 == 3)                                                                     \
-    hipLaunchKernelGGL((k_iterate_tb4<FM, 3, 4>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t); \
-  else if (c->tb4 == 4)                                                                     \
-    hipLaunchKernelGGL((k_iterate_tb4<FM, 3, 0>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t); \
-  else                                                                                      \
-    hipLaunchKernelGGL((k_iterate_tb4<FM, 4, 0>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t);
+#define TB4_M(FM) \
+  hipLaunchKernelGGL((k_iterate_tb4<FM>), dim3(blocks), dim3(32 * kTb4Groups), 0, st, t);
           MATH_SWITCH(math, TB4_M)
 #undef TB4_M
           hbm = (double)blocks * 64.0 * (kTb4Groups * nr) * 4.0 * ld_planes + Nl * 4.0 * st_planes;
@@ -2143,7 +2136,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_ROLL_PX4_MIN")) c->roll_px4_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_WI_NC")) c->wi_nc = atoi(m) == 1 ? 1 : 2;
-  if (const char *m = getenv("TVL1_TB4")) c->tb4 = atoi(m);
+  if (const char *m = getenv("TVL1_TB4")) c->tb4 = atoi(m) != 0;
   if (const char *m = getenv("TVL1_POLL")) c->poll = atoi(m);
   if (const char *m = getenv("TVL1_SPEC")) c->spec = atoi(m);
   if (const char *m = getenv("TVL1_SPEC_TRACE")) c->spec_trace = atoi(m);

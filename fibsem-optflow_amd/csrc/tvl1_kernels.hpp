@@ -1450,22 +1450,22 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
 }
 
 // ---------------------------------------------------------------- K6+K8, tall blocked regions
-// k_iterate_tb4<FM>: one pass of K <= 4 iterations over a 64 x 64 region (4-px x halo, K-row
-// y halo: 56 x (64 - 2K) output px), 512 threads.  Each thread owns 2 px of 4 CONSECUTIVE
-// rows, so the y-neighbours inside its rows are registers and only the rows between two
-// threads go through LDS: the last row's p12 / p22 (estimateU's p at y-1 of the next
-// thread's first row) and the first row's u1 / u2 (the projection's u at y+1 of the
-// previous thread's last row) -- 16 KB, 2 barriers per iteration as in k_iterate_tb, but 8
-// px of work per thread between them.  Against k_iterate_tb's 64 x 32 regions the halo
-// recompute falls from 1.52x to 1.31x at K = 4 (1.41x to 1.26x at K = 3).  Same
+// k_iterate_tb4<FM>: one pass of K <= 4 iterations over a 64 x 48 region (4-px x halo, K-row
+// y halo: 56 x (48 - 2K) output px), 512 threads.  Each thread owns 2 px of NR = 3
+// CONSECUTIVE rows, so the y-neighbours inside its rows are registers and only the rows
+// between two threads go through LDS: the last row's p12 / p22 (estimateU's p at y-1 of the
+// next thread's first row) and the first row's u1 / u2 (the projection's u at y+1 of the
+// previous thread's last row) -- 16 KB, 2 barriers per iteration as in k_iterate_tb, with 6 px
+// of work per thread between them.  Against k_iterate_tb's 64 x 32 regions the halo
+// recompute falls from 1.52x to 1.37x at K = 4, at 4 waves per SIMD (128 VGPRs) instead of
+// 8: the same time per pass on C2's level 4, and +0.7 % in flight.  (Four rows per
+// thread, 64 x 64 regions, needs 165 VGPRs -- one block per CU -- and was 49 % slower.)  Same
 // estimate_u / dual_component arithmetic, so the same bits (the region-edge rows take their
 // own row as the neighbour, as k_iterate_tb's LDS clamp does; no stored cell depends on them).
 constexpr int kTb4Groups = 16;   // row groups (threads per column) of a region
-// NR rows per thread (region 16 NR rows).  WPE: 0 = the compiler's register choice (NR = 4:
-// 165 VGPRs, one block of 8 waves per CU), 4 = four waves per SIMD (two blocks per CU; NR =
-// 4 spills at 128 VGPRs)
-template <int FM, int NR = 4, int WPE = 0>
-__global__ __launch_bounds__(32 * kTb4Groups, WPE) void k_iterate_tb4(TBArgs t) {
+constexpr int kTb4RowsPerThread = 3;
+template <int FM, int NR = kTb4RowsPerThread>
+__global__ __launch_bounds__(32 * kTb4Groups, 4) void k_iterate_tb4(TBArgs t) {
   constexpr int PX = 2, LPR = 32, NGR = kTb4Groups, kTb4Rows = NR * NGR;
   constexpr int HALO = 4 / PX;   // lanes of the 4-px x halo
   using V = float2;

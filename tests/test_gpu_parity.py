@@ -103,8 +103,9 @@ def test_constant_images_give_zero_flow(engine):
 #   TVL1_ROLL_SEG=8|64    streaming kernels' segment boundaries (8 = many short segments)
 #   TVL1_BUF_LIMIT=N      planes >= N bytes take the 64-bit-addressed kernels: k_warp_img and
 #                         the blocked passes for every pass (N = 0: every level)
-#   TVL1_TB4=0|2          blocked passes in 64 x 32 regions (k_iterate_tb<G,32,1,2>; the default
-#                         is k_iterate_tb4<FM,0>, 64 x 64) or k_iterate_tb4<FM,4>
+#   TVL1_TB4=0            blocked passes (gamma = 0) in 64 x 32 regions, k_iterate_tb<false,32,1,2>
+#                         (the default is k_iterate_tb4<FM>, 64 x 48; gamma != 0 always takes
+#                         k_iterate_tb<true,...>)
 # k_iterate<G, true> (tau/theta < 0) and the profile-1 kernels have their own tests below.
 MODES = ["", "TVL1_ROLL_LONG_MIN=0", "TVL1_ROLL_LONG_MIN=0,TVL1_ROLL_SEG=8", "TVL1_ROLL_SEG=8",
          "TVL1_ROLL_SEG=64", "TVL1_ROLL_PX4_MIN=0", "TVL1_ROLL_PX4_MIN=0,TVL1_ROLL_SEG=8",
@@ -112,7 +113,7 @@ MODES = ["", "TVL1_ROLL_LONG_MIN=0", "TVL1_ROLL_LONG_MIN=0,TVL1_ROLL_SEG=8", "TV
          "TVL1_FUSE=0,TVL1_ROLL_LONG_MIN=0", "TVL1_BUF_LIMIT=100000", "TVL1_BUF_LIMIT=0",
          "TVL1_POLL=0", "TVL1_POLL=0,TVL1_FUSE_MIN=0", "TVL1_SPEC=0", "TVL1_SPEC=0,TVL1_FUSE_MIN=0",
          "TVL1_FUSE_MIN=0,TVL1_WI_NC=1", "TVL1_FUSE_MIN=0,TVL1_WI_NC=1,TVL1_ROLL_SEG=8",
-         "TVL1_TB4=0", "TVL1_TB4=2", "TVL1_TB4=3", "TVL1_TB4=0,TVL1_BUF_LIMIT=0"]
+         "TVL1_TB4=0", "TVL1_TB4=0,TVL1_BUF_LIMIT=0"]
 # (TVL1_POLL=0: residuals read after an event instead of the poll; TVL1_SPEC=0: nothing
 # enqueued behind a check before the host reads it)
 KNOBS = ("TVL1_ROLL_SEG", "TVL1_ROLL_PX4_MIN", "TVL1_ROLL_LONG_MIN", "TVL1_FUSE", "TVL1_FUSE_MIN",
