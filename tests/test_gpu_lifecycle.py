@@ -117,3 +117,47 @@ def test_batch_alternating_geometries_hold_one_arena(built):
     eng.close()
     # after round 0 the arena has its final size: no further device memory is taken
     assert min(free[1:]) >= free[0] - (8 << 20), free
+
+
+def test_concurrent_batches_bit_identical(built):
+    """Two tvl1_calc_batch calls at once on their own contexts and streams: each sizes its
+    streaming launches for the shared share of the resident slots (fill_shared) while the
+    other runs, and every pair still equals the oracle bit for bit."""
+    p = capi.make_params(nscales=5, warps=4)
+    dev = torch.device("cuda", 0)
+    jobs = []
+    for j in range(2):
+        n, w, h = 5, 260, 90
+        I0s = np.stack([synth.gen_pair(w, h, seed=140 + 10 * j + b)[0] for b in range(n)])
+        I1s = np.stack([synth.gen_pair(w, h, seed=140 + 10 * j + b)[1] for b in range(n)])
+        jobs.append(dict(eng=capi.Engine(p), I0s=I0s, I1s=I1s, n=n, w=w, h=h,
+                         d0=torch.from_numpy(I0s).to(dev), d1=torch.from_numpy(I1s).to(dev),
+                         du=torch.zeros((n, h, w), dtype=torch.float32, device=dev),
+                         dv=torch.zeros((n, h, w), dtype=torch.float32, device=dev)))
+    torch.cuda.synchronize()
+    errs = []
+
+    def run(jb):
+        try:
+            e, n, w, h = jb["eng"], jb["n"], jb["w"], jb["h"]
+            for _ in range(3):
+                jb["st"] = e.calc_batch_device(n, jb["d0"].data_ptr(), w, w * h, jb["d1"].data_ptr(),
+                                               w, w * h, w, h, jb["du"].data_ptr(), jb["dv"].data_ptr(),
+                                               4 * w, 4 * w * h, stream=e.stream, warp_iters=True)
+            torch.cuda.ExternalStream(e.stream, device=dev).synchronize()
+        except Exception as ex:
+            errs.append(ex)
+
+    ths = [threading.Thread(target=run, args=(jb,)) for jb in jobs]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    for jb in jobs:
+        u, v = jb["du"].cpu().numpy(), jb["dv"].cpu().numpy()
+        for b in range(jb["n"]):
+            ur, vr, _, wr = checker.oracle_calc(jb["I0s"][b], jb["I1s"][b], p)
+            np.testing.assert_array_equal(jb["st"][b]["warp_iters"], wr)
+            assert bits_equal(u[b], ur) and bits_equal(v[b], vr)
+        jb["eng"].close()

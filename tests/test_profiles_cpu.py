@@ -59,3 +59,57 @@ def test_bench_line_carries_the_contract_fields(bench):
         e = modes[m]["epe_vs_headline_px"]
         assert modes[m]["same_iterations"]
         assert e["mean"] <= 1e-3 and e["p99.9"] <= 2e-2 and e["max"] <= 0.5
+
+
+# ---- round 3: one box, one evidence set (tools/final_profile.sh -> profiles/r3/final/):
+# the default bench line, one C2 pair alone and one production strip batch alone
+FINAL = PROF / "r3" / "final"
+
+
+def _class_avg_us(stats_csv, prefixes):
+    calls = ns = 0.0
+    for r in csv.DictReader(open(stats_csv)):
+        name = r["Name"].split("(")[0].replace("void ", "").replace("tvl1k::", "")
+        if name.startswith(prefixes):
+            calls += int(r["Calls"])
+            ns += float(r["TotalDurationNs"])
+    return ns / calls / 1e3, calls
+
+
+@pytest.mark.skipif(not FINAL.exists(), reason="no r3 final evidence set")
+@pytest.mark.parametrize("which", ["pair", "strips"])
+def test_r3_roofline_reproduces_by_hand(which):
+    """The bench line's `roofline.frac` (live byte accounting / HIP-event launch time) by hand
+    from the same bytes over the rocprofv3 kernel-trace launch average, within 5 %, and the
+    accounted bytes against the PMC FETCH x 2 + WRITE bytes of the same class -- for the C2
+    pair and for the production-strip batch."""
+    line = json.loads((FINAL / "bench_c2.json").read_text().splitlines()[-1])
+    if which == "pair":
+        roof = line["roofline"]
+        traffic = json.loads((FINAL / "traffic.json").read_text())
+        avg_us, calls = _class_avg_us(FINAL / "kernel_stats_single_pair.csv", ITER)
+    else:
+        roof = line["production_strips"]["roofline"]
+        traffic = json.loads((FINAL / "traffic_strips.json").read_text())
+        avg_us, calls = _class_avg_us(FINAL / "kernel_stats_strip_batch.csv",
+                                      ("kb_iterate", "kb_warp_iter"))
+    assert calls > 0 and roof["unit"] == "GB/s" and roof["peak"] == 8000.0
+    # the timing: the same bytes over the kernel trace's launch average
+    by_hand = roof["bytes_per_launch"] / (avg_us * 1e-6) / 8e12
+    assert abs(roof["frac"] / by_hand - 1) < 0.05, (which, roof["frac"], by_hand)
+    # the bytes: the engine's accounting against the PMC bytes of the same launch class (the
+    # strip batch's tiny levels fetch ~6 % beyond the tiling's compulsory bytes, DESIGN 5)
+    pmc_frac = traffic["iterate_hbm_bytes_per_launch"] / (avg_us * 1e-6) / 8e12
+    assert abs(roof["bytes_per_launch"] / traffic["iterate_hbm_bytes_per_launch"] - 1) < 0.07
+    assert abs(roof["frac"] / pmc_frac - 1) < 0.10, (which, roof["frac"], pmc_frac)
+    assert 0 < traffic["iterate_valu_frac"] < 1
+    assert roof["model_bytes_over_peak"] > 1.0 > roof["frac"]
+
+
+@pytest.mark.skipif(not FINAL.exists(), reason="no r3 final evidence set")
+def test_r3_bench_line_fields():
+    d = json.loads((FINAL / "bench_c2.json").read_text().splitlines()[-1])
+    assert d["config"]["workload"].startswith("C2") and d["n_gpus"] == 1
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and "build" in cb
+    assert d["production_strips"]["roofline"]["launches"] > 0
