@@ -122,8 +122,6 @@ struct tvl1_ctx {
   size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
   double *bpartials = nullptr;
   int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
-  int batch_fill = 1;                   // TVL1_BATCH_FILL=0: batched launches always sized
-                                        // for every resident slot
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
   size_t map_bytes = 0;
   char *align_scratch = nullptr;        // tvl1_find_alignment's pyramid, keys, descriptors
@@ -1463,13 +1461,11 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
     if (r != TVL1_OK) return r;
   }
   const size_t ps = c->bps;
+  // counted as a solve in progress (single-pair solves speculate and size their launches
+  // by this count); the batched launches themselves are sized for every resident slot (the
+  // shared share measured neutral here: 2925 / 2901 against 2919 / 2928 strip solves/s,
+  // profiles/r3/ab_batch_fill.txt)
   const SolveCount active(c->device);
-  // the single-pair rule for the launch sizes (solve(): fill_now); TVL1_BATCH_FILL=0 sizes
-  // every batched launch for all resident slots
-  auto fill_now = [&]() {
-    return c->batch_fill && g_solving[c->device & 63].load(std::memory_order_relaxed) > 1
-               ? c->fill_shared : c->fill;
-  };
   BatchSel all{};
   all.n = n;
   for (int b = 0; b < n; ++b) all.idx[b] = (uint8_t)b;
@@ -1555,7 +1551,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         wi.w.ra.b = batch_bufs;
         wi.w.ra.it = it;
         wi.w.ra.bands = (lw + 123) / 124;
-        wi.w.ra.seg_rows = roll_segment(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots * fill_now() / 100);
+        wi.w.ra.seg_rows = roll_segment(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots);
         wi.w.ra.waves = wi.w.ra.bands * ((lh + wi.w.ra.seg_rows - 1) / wi.w.ra.seg_rows);
         if (wi.w.ra.waves > c->bnblk)
           return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", wi.w.ra.waves, c->bnblk);
@@ -1692,7 +1688,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           // segments sized so the batch's wavefronts fill whole rounds of resident slots
           br.ra.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
                                            : roll_segment(br.ra.bands * sel.n, lh, K,
-                                                          c->roll_slots[K][0][2] * fill_now() / 100);
+                                                          c->roll_slots[K][0][2]);
           br.ra.waves = br.ra.bands * ((lh + br.ra.seg_rows - 1) / br.ra.seg_rows);
           blocks = br.ra.waves;
           if (blocks > c->bnblk)
@@ -2142,7 +2138,6 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_SPEC_TRACE")) c->spec_trace = atoi(m);
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
   if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
-  if (const char *m = getenv("TVL1_BATCH_FILL")) c->batch_fill = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
