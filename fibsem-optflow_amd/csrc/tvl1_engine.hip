@@ -109,10 +109,6 @@ struct tvl1_ctx {
                              // run past the first check).  4 M since the two-consumer form
                              // (C2's 4.2 Mpx level 4: one pair alone -3.7 %, in flight +0.3 %)
   int witer_slots = 0;       // resident k_warp_iter<6, -, 128, 1, wi_nc> blocks per device
-  int witer_slots_narrow = 0;   // ... of the narrow form k_warp_iter<4, -, 128, 1, 2, 5>
-  int wi_narrow = 1;         // TVL1_WI_M=6: always the wide window (M = 6); default: the
-                             // narrow one (M = 4) until a px leaves it
-  unsigned *fb_dev = nullptr;   // device flag the narrow form sets (in the gate buffer)
   int wi_nc = 2;             // TVL1_WI_NC: k_warp_iter consumer wavefronts (2: one per
                              // iteration of the pass; 1: both on one wave)
   // batch arena (tvl1_calc_batch): per logical plane, kBatchMax pairs' copies
@@ -146,10 +142,6 @@ struct tvl1_ctx {
   };
   std::vector<Mark> marks;
 };
-
-// pinned host slots (doubles): 0 / 2 residuals by check parity, 1 the check sequence word,
-// kPinnedFallback (as u32) the narrow warp's fallback flag, 8.. the batch's residuals
-constexpr int kPinnedFallback = 4;
 
 static size_t prof_begin(tvl1_ctx *c, hipStream_t st) {
   if (!c->profiling) return 0;
@@ -507,11 +499,8 @@ static tvl1_status launch_check(tvl1_ctx *c, hipStream_t st, int nparts, const C
                                 unsigned long long *seq_out) {
   unsigned long long *seq_dev = (unsigned long long *)(c->pinned_dev + 1);
   const unsigned long long seq = ++c->check_seq;
-  CheckGate gf = g;   // the narrow warp's fallback flag rides along with every residual
-  gf.fb_dev = c->fb_dev;
-  gf.fb_host = reinterpret_cast<unsigned *>(c->pinned_dev + kPinnedFallback);
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, nparts,
-                     c->pinned_dev + ((seq & 1) ? 2 : 0), c->poll ? seq_dev : nullptr, seq, gf);
+                     c->pinned_dev + ((seq & 1) ? 2 : 0), c->poll ? seq_dev : nullptr, seq, g);
   HIP_TRY(c, hipGetLastError());
   if (!c->poll) HIP_TRY(c, hipEventRecord(c->ev_check[seq & 1], st));
   *seq_out = seq;
@@ -739,10 +728,6 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     c->ev_used = 0;
     c->marks.clear();
   }
-  if (c->wi_narrow) {   // every solve starts with the narrow warp window
-    *(volatile unsigned *)(c->pinned + kPinnedFallback) = 0u;
-    HIP_TRY(c, hipMemsetAsync(c->fb_dev, 0, sizeof(unsigned), st));
-  }
 
   // [A.1] convertTo + [A.2] pyramid, kernel step = float(1/scaleStep)
   size_t tk = prof_begin(c, st);
@@ -949,19 +934,10 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           // a level's first warp, else when the previous warp did not stop at its first
           // check (a wrong guess recomputes them with the warp kernel after the check)
           w.store_c = store_c ? 1 : 0;
-          // the narrow window (M = 4: 5 blocks per CU) until a launch of this solve reports a
-          // px whose taps left it (k_reduce copies the flag to host memory); from then on the
-          // wide one (M = 6).  Both give the same bits: an out-of-window px takes the
-          // global-memory gather, which is exact, only slower.
-          const bool narrow = c->wi_narrow && c->wi_nc == 2 &&
-                              !*(volatile unsigned *)(c->pinned + kPinnedFallback);
-          w.fallback = narrow ? c->fb_dev : nullptr;
-          constexpr int BW = 128;
-          const int M = narrow ? 4 : 6;
+          constexpr int M = 6, BW = 128;
           w.ra.bands = (lw + BW - 5) / (BW - 4);
-          const int wslots = narrow ? c->witer_slots_narrow : c->witer_slots;
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                          : roll_segment(w.ra.bands, lh, 2 + M, wslots * fill_now() / 100);
+                                          : roll_segment(w.ra.bands, lh, 2 + M, c->witer_slots * fill_now() / 100);
           w.ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           w.ra.waves = w.ra.bands * segs;
@@ -969,13 +945,11 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           if (blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d blocks > partials capacity %d", blocks,
                            c->partials_cap);
-#define WITER(FM)                                                                                \
-  if (narrow)                                                                                   \
-    hipLaunchKernelGGL((k_warp_iter<4, FM, BW, 1, 2, 5>), dim3(w.ra.waves), dim3(128 + BW), 0, st, w); \
-  else if (c->wi_nc == 2)                                                                       \
-    hipLaunchKernelGGL((k_warp_iter<6, FM, BW, 1, 2>), dim3(w.ra.waves), dim3(128 + BW), 0, st, w); \
-  else                                                                                          \
-    hipLaunchKernelGGL((k_warp_iter<6, FM, BW, 1, 1>), dim3(w.ra.waves), dim3(64 + BW), 0, st, w);
+#define WITER(FM)                                                                           \
+  if (c->wi_nc == 2)                                                                       \
+    hipLaunchKernelGGL((k_warp_iter<M, FM, BW, 1, 2>), dim3(w.ra.waves), dim3(128 + BW), 0, st, w); \
+  else                                                                                     \
+    hipLaunchKernelGGL((k_warp_iter<M, FM, BW, 1, 1>), dim3(w.ra.waves), dim3(64 + BW), 0, st, w);
           MATH_SWITCH(math, WITER)
 #undef WITER
           // compulsory: p, u, I0 and the I1 window (x 1 + 2M/BW) per band column and row;
@@ -2158,7 +2132,6 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_ROLL_PX4_MIN")) c->roll_px4_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_WI_NC")) c->wi_nc = atoi(m) == 1 ? 1 : 2;
-  if (const char *m = getenv("TVL1_WI_M")) c->wi_narrow = atoi(m) == 4;
   if (const char *m = getenv("TVL1_TB4")) c->tb4 = atoi(m) != 0;
   if (const char *m = getenv("TVL1_POLL")) c->poll = atoi(m);
   if (const char *m = getenv("TVL1_SPEC")) c->spec = atoi(m);
@@ -2186,7 +2159,6 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   // hipHostMalloc does not promise zeroed memory: a stale sequence word >= the first check's
   // would let the residual poll return before k_reduce wrote
   memset(c->pinned, 0, sizeof(double) * (8 + kBatchMax));
-  c->fb_dev = reinterpret_cast<unsigned *>(c->gate + 4);   // the zeroed gate buffer
   // resident wavefronts / blocks of the streaming kernels, for their segment sizing
   {
     auto blocks_of = [&](const void *fn, int threads) {
@@ -2201,7 +2173,6 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     ROLL_SLOTS(false, 1, 4) ROLL_SLOTS(false, 2, 4) ROLL_SLOTS(true, 1, 4) ROLL_SLOTS(true, 2, 4)
 #undef ROLL_SLOTS
     c->warp_ring_slots = blocks_of((const void *)k_warp_ring<6, 2>, 128);
-    c->witer_slots_narrow = blocks_of((const void *)k_warp_iter<4, 0, 128, 1, 2, 5>, 256);
     c->witer_slots = c->wi_nc == 2 ? blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 2>, 256)
                                    : blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 1>, 192);
     // >= 3-iteration passes stream when the level has at least 4 wavefronts' worth of 56 x 32

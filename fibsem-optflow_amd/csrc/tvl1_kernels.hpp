@@ -1968,8 +1968,6 @@ struct WarpIterArgs {
   RollArgs ra;           // pass geometry (bands of 124 output px) and planes
   const float *I0, *I1;  // level images
   int store_c;           // also store I1wx / I1wy / rho (ra.it.I1wx, ...) for later passes
-  unsigned *fallback;    // set to 1 when a px's taps left the LDS window (the narrow form
-                         // reports it, so the host widens the window: tvl1_engine.hip)
 };
 
 // window ring rows: 16 for the shipped margin M = 6 (a power of two: slot = row & 15);
@@ -2037,9 +2035,6 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
   const int fy = tap_floor(wy);
   float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
   const bool inwin = fx - 1 >= P.xw0 && fx + 2 < P.xw0 + WW && fy - 1 >= gy - M && fy + 2 <= gy + M;
-  if (w.fallback != nullptr) {   // kernel argument: a uniform branch
-    if (__ballot(!inwin) != 0 && lane == 0) *w.fallback = 1u;   // idempotent vector store
-  }
   if (inwin) {
     warp_gather_fn<FM>(
         [&](int cy, int cx) {
@@ -2504,10 +2499,8 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
   }
 }
 
-// WPE: minimum waves per SIMD (0: the compiler's choice).  The narrow form (M = 4, WPE = 5)
-// fits 5 blocks per CU: 29,632 B of LDS and <= 96 VGPRs.
-template <int M, int FM = 0, int BW = 128, int PRIO = 1, int NC = 1, int WPE = 0>
-__global__ __launch_bounds__(64 * NC + BW, WPE) void k_warp_iter(WarpIterArgs w) {
+template <int M, int FM = 0, int BW = 128, int PRIO = 1, int NC = 1>
+__global__ __launch_bounds__(64 * NC + BW) void k_warp_iter(WarpIterArgs w) {
   __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, BW>()];
   __shared__ float cring[2 * 5 * BW];
   __shared__ float hring[NC == 2 ? 2 * kWiH * BW : 1];
@@ -2532,8 +2525,6 @@ struct CheckGate {
   const unsigned long long *in;
   unsigned long long in_seq;
   unsigned long long *out;
-  const unsigned *fb_dev;   // k_warp_iter's window-fallback flag, copied to fb_host when set
-  unsigned *fb_host;
   double thr;         // eps^2 * W * H
   int n, iters, kmax, eps_pos;
   int pk, pcalc;
@@ -2574,7 +2565,6 @@ __global__ void k_reduce(const double *__restrict__ partials, int n, double *__r
   if (threadIdx.x == 0) {
     const double e = s[0];
     out[0] = e;
-    if (g.fb_dev && *(volatile const unsigned *)g.fb_dev) *(volatile unsigned *)g.fb_host = 1u;
     if (g.out) {
       const bool ends = !(e > g.thr && g.n < g.iters);
       bool ok = ends;

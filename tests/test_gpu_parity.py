@@ -96,10 +96,9 @@ def test_constant_images_give_zero_flow(engine):
 # k_iterate_tb<G,32,1,2>; the knobs (read at tvl1_create) reach the rest:
 #   TVL1_ROLL_LONG_MIN=0  >= 3-iteration passes stream too: k_iterate_roll<G,3|4,2>
 #   TVL1_ROLL_PX4_MIN=0   2-iteration passes at 4 px per lane: k_iterate_roll<G,1|2,4>
-#   TVL1_FUSE_MIN=0       warpBackward fused with each warp's first pass: k_warp_iter<4,-,128,1,2,5>
-#                         (two consumer wavefronts, one per iteration, narrow window) until a
-#                         px leaves the window, then <6,-,128,1,2> (TVL1_WI_M=6: always);
-#                         TVL1_WI_NC=1: <6,-,128,1,1>, both iterations on one wavefront
+#   TVL1_FUSE_MIN=0       warpBackward fused with each warp's first pass: k_warp_iter<6,-,128,1,2>
+#                         (two consumer wavefronts, one per iteration; TVL1_WI_NC=1: <..,1,1>,
+#                         both iterations on one wavefront)
 #   TVL1_FUSE=0           never fused (k_warp_ring + the pass, on every level)
 #   TVL1_ROLL_SEG=8|64    streaming kernels' segment boundaries (8 = many short segments)
 #   TVL1_BUF_LIMIT=N      planes >= N bytes take the 64-bit-addressed kernels: k_warp_img and
@@ -114,12 +113,11 @@ MODES = ["", "TVL1_ROLL_LONG_MIN=0", "TVL1_ROLL_LONG_MIN=0,TVL1_ROLL_SEG=8", "TV
          "TVL1_FUSE=0,TVL1_ROLL_LONG_MIN=0", "TVL1_BUF_LIMIT=100000", "TVL1_BUF_LIMIT=0",
          "TVL1_POLL=0", "TVL1_POLL=0,TVL1_FUSE_MIN=0", "TVL1_SPEC=0", "TVL1_SPEC=0,TVL1_FUSE_MIN=0",
          "TVL1_FUSE_MIN=0,TVL1_WI_NC=1", "TVL1_FUSE_MIN=0,TVL1_WI_NC=1,TVL1_ROLL_SEG=8",
-         "TVL1_TB4=0", "TVL1_TB4=0,TVL1_BUF_LIMIT=0", "TVL1_FUSE_MIN=0,TVL1_WI_M=6"]
+         "TVL1_TB4=0", "TVL1_TB4=0,TVL1_BUF_LIMIT=0"]
 # (TVL1_POLL=0: residuals read after an event instead of the poll; TVL1_SPEC=0: nothing
 # enqueued behind a check before the host reads it)
 KNOBS = ("TVL1_ROLL_SEG", "TVL1_ROLL_PX4_MIN", "TVL1_ROLL_LONG_MIN", "TVL1_FUSE", "TVL1_FUSE_MIN",
-         "TVL1_BUF_LIMIT", "TVL1_BATCH_FUSE", "TVL1_POLL", "TVL1_SPEC", "TVL1_WI_NC", "TVL1_TB4",
-         "TVL1_WI_M")
+         "TVL1_BUF_LIMIT", "TVL1_BATCH_FUSE", "TVL1_POLL", "TVL1_SPEC", "TVL1_WI_NC", "TVL1_TB4")
 CONFIG_CASES = [
     (250, 131, 21, dict(nscales=5, warps=5)),
     (97, 201, 22, dict(nscales=4, warps=3, gamma=0.1)),
