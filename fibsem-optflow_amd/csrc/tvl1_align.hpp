@@ -630,8 +630,10 @@ static bool find_homography(const std::vector<Pt> &a, const std::vector<Pt> &b, 
   }
   if (!lmeds && best_in < 4) return false;
   if (lmeds && best_med >= 1e300) return false;
-  // inliers of the best hypothesis, then a least-squares refit
-  const double lt2 = lmeds ? 2.5 * 2.5 * 1.4826 * 1.4826 * (1 + 5.0 / std::max(1, n - 4)) * best_med : t2;
+  // inliers of the best hypothesis, then a least-squares refit.  LMEDS: OpenCV's robust
+  // sigma from the median, floored at 0.001 px (LMeDSPointSetRegistrator::run), squared
+  const double sg = lmeds ? std::max(2.5 * 1.4826 * (1 + 5.0 / std::max(1, n - 4)) * std::sqrt(best_med), 0.001) : 0;
+  const double lt2 = lmeds ? sg * sg : t2;
   std::vector<Pt> ia, ib;
   for (int i = 0; i < n; ++i) {
     const bool in = reproj_err2(best, a[i], b[i]) <= lt2;

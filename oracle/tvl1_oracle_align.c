@@ -560,8 +560,10 @@ static int find_homography(const Pt *a, const Pt *b, int n, int method, double t
   free(e);
   if (!lmeds && best_in < 4) return 0;
   if (lmeds && best_med >= 1e300) return 0;
-  const double lt2 =
-      lmeds ? 2.5 * 2.5 * 1.4826 * 1.4826 * (1 + 5.0 / imax(1, n - 4)) * best_med : t2;
+  /* LMEDS: sigma = 2.5 * 1.4826 * (1 + 5 / (n - 4)) * sqrt(median), floored at 0.001 px */
+  double sg = lmeds ? 2.5 * 1.4826 * (1 + 5.0 / imax(1, n - 4)) * sqrt(best_med) : 0;
+  if (lmeds && sg < 0.001) sg = 0.001;
+  const double lt2 = lmeds ? sg * sg : t2;
   Pt *ia = (Pt *)malloc(sizeof(Pt) * n), *ib = (Pt *)malloc(sizeof(Pt) * n);
   size_t ni = 0;
   for (int i = 0; i < n; ++i) {

@@ -35,7 +35,13 @@ def test_exact_correspondences_give_the_homography(built, method):
     a = rng.uniform(0, 3000, (60, 2))
     b = project(H_TRUE, a)
     H, mask = capi.find_homography(a, b, method, 3.0)
-    assert mask.all()
+    if method == 4:
+        # LMEDS's mask is the best 4-point hypothesis's, at OpenCV's robust sigma floored at
+        # 0.001 px: with float32 corners (ulp 2.4e-4 at 3000) a few points of an exact set
+        # fall outside it; the refit model below still fits every point
+        assert mask.mean() >= 0.9
+    else:
+        assert mask.all()
     assert rms(H, a.astype(np.float32), b.astype(np.float32)) < 2e-3   # float32 inputs
     np.testing.assert_allclose(H, H_TRUE, rtol=2e-4, atol=2e-6)
 
