@@ -15,6 +15,16 @@
 
 namespace ofio {
 
+namespace {
+void *default_alloc(size_t n) { return ::operator new(n, std::nothrow); }
+void default_release(void *p, size_t) { ::operator delete(p); }
+HostAllocHooks g_hooks{default_alloc, default_release};
+}  // namespace
+
+void set_host_alloc(const HostAllocHooks &h) { g_hooks = h; }
+void *host_alloc(size_t bytes) { return g_hooks.alloc(bytes); }
+void host_release(void *p, size_t bytes) { g_hooks.release(p, bytes); }
+
 // The largest image a decoder accepts: the solver's limit (tvl1_calc: W * H <= 2^31).
 constexpr uint64_t kMaxPixels = (uint64_t)1 << 31;
 

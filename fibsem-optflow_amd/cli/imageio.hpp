@@ -12,15 +12,61 @@
 // FIB-SEM slices are 8-bit grayscale, for which decoding is exact.
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
+#include <new>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace ofio {
 
+// Host storage of images and flow fields.  By default operator new; the CLI installs a
+// page-locked pool (hipHostMalloc) so that decoded slices are uploaded by one DMA straight
+// from the buffer the decoder wrote, and flow fields download likewise (optflow.cpp:315-316
+// GpuMat::upload).  Install before any image is allocated; release() gets
+// back exactly the pointers alloc() returned.
+struct HostAllocHooks {
+  void *(*alloc)(size_t bytes);
+  void (*release)(void *p, size_t bytes);
+};
+void set_host_alloc(const HostAllocHooks &h);
+void *host_alloc(size_t bytes);
+void host_release(void *p, size_t bytes);
+
+template <class T>
+struct HostAlloc {
+  using value_type = T;
+  HostAlloc() = default;
+  template <class U>
+  HostAlloc(const HostAlloc<U> &) {}
+  T *allocate(size_t n) {
+    if (n > (size_t)-1 / sizeof(T)) throw std::bad_alloc();
+    void *p = host_alloc(n * sizeof(T));
+    if (!p) throw std::bad_alloc();
+    return static_cast<T *>(p);
+  }
+  void deallocate(T *p, size_t n) { host_release(p, n * sizeof(T)); }
+  // resize() default-initialises (no zero fill): every decoder writes each pixel it sizes
+  template <class U>
+  void construct(U *p) noexcept {
+    ::new (static_cast<void *>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+  }
+  template <class U>
+  bool operator==(const HostAlloc<U> &) const { return true; }
+  template <class U>
+  bool operator!=(const HostAlloc<U> &) const { return false; }
+};
+template <class T>
+using HostVec = std::vector<T, HostAlloc<T>>;
+
 struct Image8 {
   int width = 0, height = 0;
-  std::vector<uint8_t> data;  // row-major, pitch == width
+  HostVec<uint8_t> data;  // row-major, pitch == width
   uint8_t *row(int y) { return data.data() + (size_t)y * width; }
   const uint8_t *row(int y) const { return data.data() + (size_t)y * width; }
 };

@@ -24,9 +24,10 @@
 //     they are silently ignored there);
 //   * a malformed JSON file is an error (the reference ignores parse failure);
 //   * build-only keys: "devices" (list of GPU ordinals, pairs sharded over them),
-//     "inflight" (pairs in flight per GPU, default 2), "decode_threads" (slice decode-ahead
+//     "inflight" (pairs in flight per GPU, default 3), "decode_threads" (slice decode-ahead
 //     pool, default min(16, cores - 1)), "medianFiltering",
-//     "matches_file", "stats_json", "skip_existing".
+//     "matches_file", "stats_json", "skip_existing", "pinned_host" (page-locked slices and
+//     flows, default off).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -159,6 +160,115 @@ struct DeviceCtx {
 
 std::mutex g_io_mutex;
 
+// Page-locked host buffers for what crosses PCIe (the reference uploads
+// with GpuMat::upload, optflow.cpp:315-316): the decode pool writes each slice straight
+// into one, so its upload is a single DMA with no pageable staging copy, and full flow
+// fields download into them.  hipHostMalloc costs milliseconds per 25 MB slice, so a
+// released buffer returns to a free list (best fit, up to 4x the request) instead of
+// being unpinned; the list keeps at most kKeep bytes and the pool pins at most kMax, past
+// which buffers are pageable; buffers under kMin stay pageable.  Pinning runs outside the
+// pool's lock, so decode threads never wait on each other's hipHostMalloc.  A buffer is released only
+// after the stream that read or wrote it was synchronised (each pair's solve and downloads
+// end in a stream sync before the next pair replaces DeviceCtx::h0 / h1).
+class PinnedPool {
+ public:
+  static void *alloc(size_t n) { return pool().get(n); }
+  static void release(void *p, size_t n) { pool().put(p, n); }
+  static size_t pinned_bytes() {
+    std::lock_guard<std::mutex> lk(pool().m_);
+    return pool().pinned_;
+  }
+  // pins, free-list hits, pageable fallbacks and the time spent pinning (OPTFLOW_PINNED_TRACE)
+  static std::string summary() {
+    PinnedPool &q = pool();
+    std::lock_guard<std::mutex> lk(q.m_);
+    char b[200];
+    snprintf(b, sizeof b, "pinned pool: %zu MiB pinned, %ld pins (%.1f ms), %ld reuses, %ld pageable",
+             q.pinned_ >> 20, q.n_pin_, q.pin_ms_, q.n_hit_, q.n_page_);
+    return b;
+  }
+
+ private:
+  static constexpr size_t kMin = 256u << 10, kKeep = 2ull << 30, kMax = 16ull << 30;
+  static PinnedPool &pool() {
+    static PinnedPool *p = new PinnedPool;   // never destroyed: buffers may outlive main's locals
+    return *p;
+  }
+  void *get(size_t n) {
+    if (n >= kMin && !off_) {
+      const size_t cap = (n + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+      std::vector<void *> drop;
+      {
+        std::lock_guard<std::mutex> lk(m_);
+        auto it = free_.lower_bound(cap);   // smallest kept buffer that holds n, up to 4x
+        if (it != free_.end() && it->first <= 4 * cap) {
+          void *p = it->second;
+          kept_ -= it->first;
+          live_[p] = it->first;
+          free_.erase(it);
+          ++n_hit_;
+          return p;
+        }
+        // make room under kMax from the free list before pinning more
+        while (pinned_ + cap > kMax && !free_.empty()) {
+          auto f = free_.begin();
+          drop.push_back(f->second);
+          pinned_ -= f->first;
+          kept_ -= f->first;
+          free_.erase(f);
+        }
+        if (pinned_ + cap <= kMax) pinned_ += cap;   // reserved; pinned outside the lock
+        else {
+          ++n_page_;
+          return ::operator new(n, std::nothrow);
+        }
+      }
+      for (void *q : drop) (void)hipHostFree(q);
+      void *p = nullptr;   // hipHostMalloc takes milliseconds: other threads go on meanwhile
+      const auto t0 = std::chrono::steady_clock::now();
+      if (hipHostMalloc(&p, cap, hipHostMallocPortable) == hipSuccess && p) {
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::lock_guard<std::mutex> lk(m_);
+        live_[p] = cap;
+        ++n_pin_;
+        pin_ms_ += ms;
+        return p;
+      }
+      std::lock_guard<std::mutex> lk(m_);
+      pinned_ -= cap;
+      off_ = true;   // no device / no pinnable memory: pageable from here on
+    }
+    return ::operator new(n, std::nothrow);
+  }
+  void put(void *p, size_t) {
+    if (!p) return;
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      auto it = live_.find(p);
+      if (it != live_.end()) {
+        const size_t cap = it->second;
+        live_.erase(it);
+        if (kept_ + cap <= kKeep) {
+          free_.emplace(cap, p);
+          kept_ += cap;
+        } else {
+          (void)hipHostFree(p);
+          pinned_ -= cap;
+        }
+        return;
+      }
+    }
+    ::operator delete(p);
+  }
+  std::mutex m_;
+  std::multimap<size_t, void *> free_;   // capacity -> buffer
+  std::map<void *, size_t> live_;        // pinned buffers handed out -> capacity
+  size_t kept_ = 0, pinned_ = 0;
+  std::atomic<bool> off_{false};
+  long n_pin_ = 0, n_hit_ = 0, n_page_ = 0;
+  double pin_ms_ = 0;
+};
+
 bool ensure(DeviceCtx &dc, size_t img_bytes, size_t flow_bytes, bool &realloc, std::string &err) {
   realloc = false;
   if ((img_bytes > dc.cap_img || flow_bytes > dc.cap_flow) && dc.stream)
@@ -246,7 +356,7 @@ void emit_points(const std::vector<std::pair<int, int>> &pts, const std::vector<
   }
 }
 
-void random_points(const std::vector<float> &fx, const std::vector<float> &fy, int W, int H,
+void random_points(const float *fx, const float *fy, int W, int H,
                    Value &im, const Value &args, const Rect &r0, const Rect &r1,
                    const std::vector<uint8_t> &mask, bool features) {
   const bool debug = args.get("debug", false).asBool();
@@ -425,7 +535,7 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
     res.stats["solves"].append(sv);
     return random_points_sampled(dc, fp, W, H, f0, f1, r0, r1, im, args, features, err);
   }
-  std::vector<float> fx((size_t)W * H), fy((size_t)W * H);
+  ofio::HostVec<float> fx((size_t)W * H), fy((size_t)W * H);   // pinned (PinnedPool)
   if (hipMemcpyAsync(fx.data(), dc.du, fx.size() * 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
       hipMemcpyAsync(fy.data(), dc.dv, fy.size() * 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
       hipStreamSynchronize(dc.stream) != hipSuccess) {
@@ -458,7 +568,7 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
     for (int y = 0; y < H; ++y)
       for (int x = 0; x < W; ++x)
         mask[(size_t)y * W + x] = (f0.row(r0.y + y)[r0.x + x] > 1) | (f1.row(r1.y + y)[r1.x + x] > 1);
-    random_points(fx, fy, W, H, im, args, r0, r1, mask, features);
+    random_points(fx.data(), fy.data(), W, H, im, args, r0, r1, mask, features);
   }
   return true;
 }
@@ -750,6 +860,14 @@ static int from_file(Value &args, bool plan_only) {
   }
   const bool skip_existing = args.get("skip_existing", false).asBool();
 
+  // build-only "pinned_host" (env OPTFLOW_PINNED overrides): page-locked slices and flow
+  // fields (PinnedPool), installed before the first image is allocated.  Off by default:
+  // on 96-pair jobs it measured 2-5 % slower end to end -- each 25 MB buffer
+  // costs 10-20 ms to pin, a C2 job's decode-ahead window spans ~100 slices, and the
+  // pageable upload it replaces (~1 ms per pair) runs on a worker that is not the bound
+  bool pinned = args.get("pinned_host", false).asBool();
+  if (const char *e = getenv("OPTFLOW_PINNED")) pinned = atoi(e) != 0;
+  if (!plan_only && pinned) ofio::set_host_alloc({PinnedPool::alloc, PinnedPool::release});
   // build-only "decode_threads": host threads decoding slices ahead of the GPU
   const unsigned hc = std::max(2u, std::thread::hardware_concurrency());
   DecodePool pool(std::max(1, args.get("decode_threads", (int)std::min(16u, hc - 1)).asInt()));
@@ -1053,6 +1171,7 @@ static int from_file(Value &args, bool plan_only) {
       Value e = results[i].stats;
       e["index"] = (int64_t)i;
       e["ok"] = results[i].ok;
+      e["host_pinned_bytes"] = (int64_t)PinnedPool::pinned_bytes();   // process total at exit
       st.append(e);
     }
     FILE *f = fopen(args["stats_json"].asString().c_str(), "w");
@@ -1061,6 +1180,8 @@ static int from_file(Value &args, bool plan_only) {
       fclose(f);
     }
   }
+  if (const char *e = getenv("OPTFLOW_PINNED_TRACE"); e && atoi(e))
+    fprintf(stderr, "%s\n", PinnedPool::summary().c_str());
   return 0;  // like the reference: per-pair failures are reported, exit status 0
 }
 

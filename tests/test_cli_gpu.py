@@ -282,3 +282,51 @@ def test_prescale_generic_linear(tmp_path, pair, scale):
     (fy,) = tmp_path.glob("g_*_y.tiff")
     assert np.array_equal(tif(fx).view(np.uint32), u.view(np.uint32))
     assert np.array_equal(tif(fy).view(np.uint32), v.view(np.uint32))
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_pinned_uploads_match_pageable(tmp_path, built, devices):
+    """SURVEY 8(f) N2 pinned uploads: slices decode into page-locked pool buffers (uploaded by
+    one DMA each) and flow fields download into them; buffers are recycled across pairs and
+    workers.  Outputs are byte-identical to the pageable path (OPTFLOW_PINNED=0), and the
+    stats report pinned memory in use (none with OPTFLOW_PINNED=0).  Slices are > 256 KiB so
+    the pool pins them; 7 pairs with slice reuse recycle the buffers.  Off by default; on
+    with the build-only config key "pinned_host" or OPTFLOW_PINNED=1."""
+    import os
+    W, H = 640, 480
+    stack = synth.gen_stack(W, H, 8, seed=91)
+    for z in range(8):
+        Image.fromarray(stack[z]).save(tmp_path / f"s{z}.png")
+    imgs = [{"p": str(tmp_path / f"s{z}.png"), "q": str(tmp_path / f"s{z + 1}.png"),
+             "output_name": f"z{z}"} for z in range(7)]
+    outs, pinned = {}, {}
+    for tag, env_v in (("pinned", "1"), ("pageable", "0"), ("config", None)):
+        d = tmp_path / tag
+        d.mkdir()
+        cfg = {"output_dir": str(d), "scale": 1, "output_type": "flow", "nscales": 3,
+               "warps": 2, "devices": devices, "rois": {"custom": [0, 0, W, H]},
+               "stats_json": str(d / "stats.json"), "images": imgs}
+        if tag == "config":
+            cfg["pinned_host"] = True   # the config key; no env
+        p = tmp_path / f"{tag}.json"
+        p.write_text(json.dumps(cfg))
+        env = dict(os.environ)
+        env.pop("OPTFLOW_PINNED", None)
+        if env_v is not None:
+            env["OPTFLOW_PINNED"] = env_v
+        r = subprocess.run([str(OPTFLOW), str(p)], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0, r.stderr
+        st = json.loads((d / "stats.json").read_text())
+        assert all(e["ok"] for e in st)
+        pinned[tag] = st[0]["host_pinned_bytes"]
+        outs[tag] = {f.name: f.read_bytes() for f in sorted(d.glob("*.tiff"))}
+    assert len(outs["pinned"]) == 14 and outs["pinned"] == outs["pageable"] == outs["config"]
+    # two slices + two flow fields per worker at least, all recycled: bounded by the pool
+    assert pinned["pinned"] >= 2 * W * H and pinned["config"] >= 2 * W * H, pinned
+    assert pinned["pageable"] == 0, pinned
+    assert pinned["pinned"] <= len(devices) * 64 * (1 << 20), pinned
+    # the custom ROI reads the whole frame: equal to the oracle on one pair
+    u, v = oracle_post(stack[3], stack[4], capi.make_params(nscales=3, warps=2), 0)
+    assert np.array_equal(tif(tmp_path / "pinned" / "z3_1.00_x.tiff"), u)
+    assert np.array_equal(tif(tmp_path / "pinned" / "z3_1.00_y.tiff"), v)

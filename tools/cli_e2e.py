@@ -10,6 +10,8 @@ configurations, each with the decode-ahead pool and with one decode thread:
   * "production strips": scale 0.5, top/bottom 100-row ROIs, reference defaults
     (gen_cross_file_list.py's job shape).
 Output type random_points (the production output) keeps TIFF writes out of the timing.
+--ab-pinned instead runs each job with the decode pool twice with page-locked slices and
+flows and twice pageable (OPTFLOW_PINNED=1/0, alternating).
 Prints one JSON line per run."""
 import argparse
 import json
@@ -40,7 +42,7 @@ def make_stack(d: Path, Z: int, W: int, H: int):
     return paths
 
 
-def run(cfg, d: Path, name: str, skip: int = 4):
+def run(cfg, d: Path, name: str, skip: int = 4, env=None):
     """Wall time of the whole CLI process, and the steady rate: the CLI prints "p q" as it
     starts each pair, so pairs after the first `skip` starts over the time from that start to
     the process end leave out process start, device init and the first decodes."""
@@ -48,7 +50,7 @@ def run(cfg, d: Path, name: str, skip: int = 4):
     p.write_text(json.dumps(cfg))
     t0 = time.perf_counter()
     proc = subprocess.Popen([str(OPTFLOW), str(p)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                            text=True)
+                            text=True, env=env)
     starts = []
     for line in proc.stdout:
         if line.strip() and not line.startswith("{"):
@@ -58,6 +60,9 @@ def run(cfg, d: Path, name: str, skip: int = 4):
     t1 = time.perf_counter()
     if rc != 0:
         raise RuntimeError(err[-2000:])
+    for line in err.splitlines():
+        if line.startswith("pinned pool:"):
+            print(line, flush=True)
     steady = None
     if len(starts) > skip + 1:
         steady = (len(starts) - skip) / (t1 - starts[skip])
@@ -70,6 +75,7 @@ def main():
     ap.add_argument("--width", type=int, default=6144)
     ap.add_argument("--height", type=int, default=4096)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--ab-pinned", action="store_true")
     args = ap.parse_args()
     d = Path(args.out or tempfile.mkdtemp(prefix="cli_e2e_"))
     d.mkdir(parents=True, exist_ok=True)
@@ -87,6 +93,19 @@ def main():
                           "rois": {"custom": [0, 0, W, H]}},
         "production_strips": {"scale": 0.5, "rois": {"top": 100, "bottom": 100}},
     }
+    if args.ab_pinned:
+        for name, extra in jobs.items():
+            for rep, pinned in enumerate((1, 0, 1, 0)):
+                cfg = {"output_dir": str(d / name), "output_type": "random_points",
+                       "matches_file": str(d / name / "pm"), "images": pairs, **extra}
+                (d / name).mkdir(exist_ok=True)
+                env = dict(os.environ, OPTFLOW_PINNED=str(pinned), OPTFLOW_PINNED_TRACE="1")
+                dt, steady = run(cfg, d, f"{name}_pin{pinned}_{rep}", env=env)
+                n = len(pairs)
+                print(json.dumps({"job": name, "pinned": pinned, "pairs": n,
+                                  "wall_s": round(dt, 3), "pairs_per_s": round(n / dt, 2),
+                                  "steady_pairs_per_s": steady and round(steady, 2)}), flush=True)
+        return
     for name, extra in jobs.items():
         for threads in (None, 1):
             cfg = {"output_dir": str(d / name), "output_type": "random_points",
