@@ -108,10 +108,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--width", type=int, default=6144)
-    ap.add_argument("--height", type=int, default=4096)
-    ap.add_argument("--nscales", type=int, default=5)
-    ap.add_argument("--warps", type=int, default=30)
+    # defaults None: C2's 6144x4096 / 5 scales / 30 warps, or for --workload strips the
+    # production strip's 3072x100 / 10 scales / 5 warps
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--nscales", type=int, default=None)
+    ap.add_argument("--warps", type=int, default=None)
     ap.add_argument("--iterations", type=int, default=300)
     ap.add_argument("--epsilon", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -154,6 +156,10 @@ def parse():
                          "rank to DIR/pair_s<s>_z<z>.npz (tests/test_gpu_stack.py; not timed "
                          "for the bench line)")
     args = ap.parse_args()
+    geo = (3072, 100, 10, 5) if args.workload == "strips" else (6144, 4096, 5, 30)
+    for k, d in zip(("width", "height", "nscales", "warps"), geo):
+        if getattr(args, k) is None:
+            setattr(args, k, d)
     if args.inflight is None:   # pairs (or strip batches) in flight per GPU
         # pairs: 3 (+1.5 % over 2 on the C2 pair, 4 is slower); strip batches: 2
         args.inflight = 2 if args.workload == "strips" else 3
