@@ -904,11 +904,25 @@ __device__ __forceinline__ void load_row(Row<G, PX> &r, const IterArgs &a, size_
 // OpenCV `divergence` (tvl1flow.cu) at px k of this lane; pl = p1 at x-1, pu = p2 at y-1.
 // Branch-free: every form is evaluated with its own association and the right one
 // selected (the x == 0, y > 0 form associates differently from the interior one).
+// YZ (the rolling pipelines): the caller's p2u is already +0.0f on row 0 (they zero p above
+// the image when they produce it), so there is no row-0 select, and the column-0 form is
+// evaluated only in a branch taken by wavefronts that hold a column <= 0 (c0w, wave-uniform:
+// the first band; columns < 0 are halo lanes, never stored).  The empty asm keeps the
+// compiler from flattening that branch into a select the other bands would pay.
+template <bool YZ = false>
 __device__ __forceinline__ float divergence(float p1, float p1l, float p2, float p2u, int x,
-                                            int y) {
+                                            int y, bool c0w = true) {
   // interior (p1 - p1l) + (p2 - p2u) and row 0 (p1 - p1l) + p2 are one form with p2u := 0
   // at y = 0 (p2 - +0 == p2 exactly, signed zeros included); column 0 (p1 + p2) - p2u and
   // the corner p1 + p2 likewise
+  if (YZ) {
+    float d = (p1 - p1l) + (p2 - p2u);
+    if (c0w) {
+      asm volatile("" ::: "memory");
+      d = x <= 0 ? (p1 + p2) - p2u : d;
+    }
+    return d;
+  }
   const float p2u0 = y > 0 ? p2u : 0.0f;
   const float rest = (p1 - p1l) + (p2 - p2u0);
   const float col0 = (p1 + p2) - p2u0;
@@ -943,20 +957,24 @@ __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, floa
            : rhoc + (I1wxv * u1o + I1wyv * u2o + (G ? a.gamma * u3o : 0.0f));
   // TH operator, branch-free: the three candidate steps are computed with the
   // reference's exact expressions and the applicable one selected.
-  const bool lo = rho < -a.l_t * gradv;
-  const bool hi = rho > a.l_t * gradv;
+  // (-l_t)*g == -(l_t*g) exactly (round-to-nearest is sign-symmetric): one product serves
+  // both bounds, and each +-l_t*I1w* pair below likewise
+  const float ltg = a.l_t * gradv;
+  const bool lo = rho < -ltg;
+  const bool hi = rho > ltg;
   const bool mid = gradv > kFltEps;
   // only selected when gradv > FLT_EPSILON
   const float fi = approx(FM) ? -rho * __builtin_amdgcn_rcpf(gradv) : th_quot(rho, gradv, mid);
   float d1 = mid ? fi * I1wxv : 0.0f;
   float d2 = mid ? fi * I1wyv : 0.0f;
   float d3 = mid ? fi * a.gamma : 0.0f;
-  d1 = hi ? -a.l_t * I1wxv : d1;
-  d2 = hi ? -a.l_t * I1wyv : d2;
-  d3 = hi ? -a.l_t * a.gamma : d3;     // +-l_t*gamma
-  d1 = lo ? a.l_t * I1wxv : d1;
-  d2 = lo ? a.l_t * I1wyv : d2;
-  d3 = lo ? a.l_t * a.gamma : d3;
+  const float ltx = a.l_t * I1wxv, lty = a.l_t * I1wyv, ltz = a.l_t * a.gamma;
+  d1 = hi ? -ltx : d1;
+  d2 = hi ? -lty : d2;
+  d3 = hi ? -ltz : d3;     // +-l_t*gamma
+  d1 = lo ? ltx : d1;
+  d2 = lo ? lty : d2;
+  d3 = lo ? ltz : d3;
   v1 = u1o + d1;
   v2 = u2o + d2;
   v3 = G ? u3o + d3 : 0.0f;
@@ -964,18 +982,19 @@ __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, floa
 
 // estimateU's second half at one px: u^n = v + theta * div(p^{n-1}).  pl = p*1 at x-1,
 // pu = p*2 at y-1.
-template <bool G, int FM = 0>
+template <bool G, int FM = 0, bool YZ = false>
 __device__ __forceinline__ void u_from_v(float v1, float v2, float v3, float p11, float p11l,
                                          float p12, float p12u, float p21, float p21l,
                                          float p22, float p22u, float p31, float p31l,
                                          float p32, float p32u, int x, int y,
-                                         const IterArgs &a, float &n1, float &n2, float &n3) {
-  const float div1 = divergence(p11, p11l, p12, p12u, x, y);
-  const float div2 = divergence(p21, p21l, p22, p22u, x, y);
+                                         const IterArgs &a, float &n1, float &n2, float &n3,
+                                         bool c0w = true) {
+  const float div1 = divergence<YZ>(p11, p11l, p12, p12u, x, y, c0w);
+  const float div2 = divergence<YZ>(p21, p21l, p22, p22u, x, y, c0w);
   n1 = contracts(FM) ? fm_fma(a.theta, div1, v1) : v1 + a.theta * div1;
   n2 = contracts(FM) ? fm_fma(a.theta, div2, v2) : v2 + a.theta * div2;
   if (G) {
-    const float div3 = divergence(p31, p31l, p32, p32u, x, y);
+    const float div3 = divergence<YZ>(p31, p31l, p32, p32u, x, y, c0w);
     n3 = contracts(FM) ? fm_fma(a.theta, div3, v3) : v3 + a.theta * div3;
   }
 }
@@ -990,18 +1009,18 @@ __device__ __forceinline__ float residual_px(float d1, float d2) {
 // estimateU at one px (x, y): the TH step from the warp constants and u^{n-1}, then
 // u^n = v + theta * div(p^{n-1}).  Shared by every iteration kernel, so they all run
 // exactly this sequence of IEEE float operations.
-template <bool G, int FM = 0, bool CPUP = false>
+template <bool G, int FM = 0, bool CPUP = false, bool YZ = false>
 __device__ __forceinline__ void estimate_u_px(float I1wxv, float I1wyv, float rhoc, float u1o,
                                               float u2o, float u3o, float p11, float p11l,
                                               float p12, float p12u, float p21, float p21l,
                                               float p22, float p22u, float p31, float p31l,
                                               float p32, float p32u, int x, int y,
                                               const IterArgs &a, float &n1, float &n2,
-                                              float &n3) {
+                                              float &n3, bool c0w = true) {
   float v1, v2, v3;
   th_px<G, FM, CPUP>(I1wxv, I1wyv, rhoc, u1o, u2o, u3o, a, v1, v2, v3);
-  u_from_v<G, FM>(v1, v2, v3, p11, p11l, p12, p12u, p21, p21l, p22, p22u, p31, p31l, p32, p32u, x,
-              y, a, n1, n2, n3);
+  u_from_v<G, FM, YZ>(v1, v2, v3, p11, p11l, p12, p12u, p21, p21l, p22, p22u, p31, p31l, p32,
+                      p32u, x, y, a, n1, n2, n3, c0w);
 }
 
 // estimateU for the PX px of this lane on row y.  up* = p12/p22/p32 of row y-1.
@@ -1464,37 +1483,18 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
 // own row as the neighbour, as k_iterate_tb's LDS clamp does; no stored cell depends on them).
 constexpr int kTb4Groups = 16;   // row groups (threads per column) of a region
 constexpr int kTb4RowsPerThread = 3;
-template <int FM, int NR = kTb4RowsPerThread>
-__global__ __launch_bounds__(32 * kTb4Groups, 4) void k_iterate_tb4(TBArgs t) {
-  constexpr int PX = 2, LPR = 32, NGR = kTb4Groups, kTb4Rows = NR * NGR;
-  constexpr int HALO = 4 / PX;   // lanes of the 4-px x halo
-  using V = float2;
-  __shared__ V lds[4][NGR][LPR];   // [p12 last, p22 last, u1 first, u2 first][group][lane]
-  const IterArgs &a = t.it;
-  if (gated_off(a.gate, a.gate_seq)) return;   // whole grid
-  const int tid = threadIdx.x;
-  const int c4 = tid % LPR;
-  const int q = tid / LPR;                     // row group: region rows NR q .. NR q + NR - 1
-  int bx, by;
-  tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
-  const int K = t.niter;
-  const int xr0 = bx * 56 - 4;
-  const int yr0 = by * t.out_h - K;
-  const int X = xr0 + PX * c4;
-  const int xa = imin(imax(X, 0), a.P - PX);
-  Row<false, PX> r[NR];
-  int Y[NR];
-  bool out_ok[NR];
-#pragma unroll
-  for (int g = 0; g < NR; ++g) {
-    const int row = NR * q + g;
-    Y[g] = yr0 + row;
-    const int ya = imin(imax(Y[g], 0), a.H - 1);
-    load_row<false, PX>(r[g], a, (size_t)ya * a.P + xa);
-    out_ok[g] = c4 >= HALO && c4 < LPR - HALO && row >= K && row < kTb4Rows - K && Y[g] >= 0 &&
-                Y[g] < a.H && X < a.W;
-  }
-  double acc = 0.0;
+
+// The iterations of one k_iterate_tb4 region.  IN: the region lies inside the image with a
+// margin (x > 0, y > 0, x + 1 < W, y + 1 < H for every px), so the border forms are constant
+// and the divergence / projection selects fold away: the same operations as the general
+// path takes for such px, hence the same bits.  The edge regions (the outer ring of tiles)
+// take the general path.
+template <int FM, int NR, bool IN>
+__device__ __forceinline__ void tb4_iterations(Row<false, 2> (&r)[NR], const int (&Y)[NR],
+                                               const bool (&out_ok)[NR], float2 (&lds)[4][kTb4Groups][32],
+                                               const IterArgs &a, int K, int X, int q, int c4,
+                                               double &acc) {
+  constexpr int PX = 2, NGR = kTb4Groups;
   for (int it = 0; it < K; ++it) {
     const bool last = it == K - 1;
     // ---- estimateU (p^{n-1} at y-1: the row above in registers, or the previous group's
@@ -1516,9 +1516,10 @@ __global__ __launch_bounds__(32 * kTb4Groups, 4) void k_iterate_tb4(TBArgs t) {
     for (int g = 0; g < NR; ++g) {
       float n1[PX], n2[PX], n3[PX];
       if (g == 0)
-        estimate_u<false, PX, FM>(r[0], up12, up22, zero3, X, Y[0], a, n1, n2, n3);
+        estimate_u<false, PX, FM>(r[0], up12, up22, zero3, IN ? 1 : X, IN ? 1 : Y[0], a, n1, n2, n3);
       else
-        estimate_u<false, PX, FM>(r[g], r[g - 1].p12, r[g - 1].p22, zero3, X, Y[g], a, n1, n2, n3);
+        estimate_u<false, PX, FM>(r[g], r[g - 1].p12, r[g - 1].p22, zero3, IN ? 1 : X, IN ? 1 : Y[g], a,
+                                  n1, n2, n3);
       if (last && a.calc_err && out_ok[g]) {
 #pragma unroll
         for (int k = 0; k < PX; ++k)
@@ -1544,14 +1545,15 @@ __global__ __launch_bounds__(32 * kTb4Groups, 4) void k_iterate_tb4(TBArgs t) {
     }
 #pragma unroll
     for (int g = 0; g < NR; ++g) {
-      const bool has_down = Y[g] + 1 < a.H;
+      const bool has_down = IN || Y[g] + 1 < a.H;
+      const int xd = IN ? 0 : X, wd = IN ? 64 : a.W;   // IN: has_right holds for both px
       float q11[PX], q12[PX], q21[PX], q22[PX];
       if (g < NR - 1) {
-        dual_component<PX, false, FM>(r[g].u1, r[g + 1].u1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12);
-        dual_component<PX, false, FM>(r[g].u2, r[g + 1].u2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22);
+        dual_component<PX, false, FM>(r[g].u1, r[g + 1].u1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12);
+        dual_component<PX, false, FM>(r[g].u2, r[g + 1].u2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22);
       } else {
-        dual_component<PX, false, FM>(r[g].u1, d1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12);
-        dual_component<PX, false, FM>(r[g].u2, d2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22);
+        dual_component<PX, false, FM>(r[g].u1, d1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12);
+        dual_component<PX, false, FM>(r[g].u2, d2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22);
       }
 #pragma unroll
       for (int k = 0; k < PX; ++k) {
@@ -1561,6 +1563,34 @@ __global__ __launch_bounds__(32 * kTb4Groups, 4) void k_iterate_tb4(TBArgs t) {
     }
     // the next iteration's first barrier orders these LDS reads before the rewrite
   }
+}
+
+template <int FM, int NR, bool IN>
+__device__ __forceinline__ void tb4_body(const TBArgs &t, float2 (&lds)[4][kTb4Groups][32], int xr0,
+                                         int yr0) {
+  constexpr int PX = 2, LPR = 32, NGR = kTb4Groups, kTb4Rows = NR * NGR;
+  constexpr int HALO = 4 / PX;   // lanes of the 4-px x halo
+  const IterArgs &a = t.it;
+  const int tid = threadIdx.x;
+  const int c4 = tid % LPR;
+  const int q = tid / LPR;                     // row group: region rows NR q .. NR q + NR - 1
+  const int K = t.niter;
+  const int X = xr0 + PX * c4;
+  const int xa = imin(imax(X, 0), a.P - PX);
+  Row<false, PX> r[NR];
+  int Y[NR];
+  bool out_ok[NR];
+#pragma unroll
+  for (int g = 0; g < NR; ++g) {
+    const int row = NR * q + g;
+    Y[g] = yr0 + row;
+    const int ya = imin(imax(Y[g], 0), a.H - 1);
+    load_row<false, PX>(r[g], a, (size_t)ya * a.P + xa);
+    out_ok[g] = c4 >= HALO && c4 < LPR - HALO && row >= K && row < kTb4Rows - K && Y[g] >= 0 &&
+                Y[g] < a.H && X < a.W;
+  }
+  double acc = 0.0;
+  tb4_iterations<FM, NR, IN>(r, Y, out_ok, lds, a, K, X, q, c4, acc);
 #pragma unroll
   for (int g = 0; g < NR; ++g) {
     if (out_ok[g]) {
@@ -1585,6 +1615,21 @@ __global__ __launch_bounds__(32 * kTb4Groups, 4) void k_iterate_tb4(TBArgs t) {
       a.partials[blockIdx.x] = sum;
     }
   }
+}
+
+template <int FM, int NR = kTb4RowsPerThread>
+__global__ __launch_bounds__(32 * kTb4Groups, 4) void k_iterate_tb4(TBArgs t) {
+  __shared__ float2 lds[4][kTb4Groups][32];   // [p12 last, p22 last, u1 first, u2 first][group][lane]
+  if (gated_off(t.it.gate, t.it.gate_seq)) return;   // whole grid
+  int bx, by;
+  tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
+  const int xr0 = bx * 56 - 4;
+  const int yr0 = by * t.out_h - t.niter;
+  // wave-uniform: the whole region inside the image with a 1-px margin (tb4_iterations' IN)
+  if (xr0 >= 1 && yr0 >= 1 && xr0 + 64 < t.it.W && yr0 + NR * kTb4Groups < t.it.H)
+    tb4_body<FM, NR, true>(t, lds, xr0, yr0);
+  else
+    tb4_body<FM, NR, false>(t, lds, xr0, yr0);
 }
 
 // ---------------------------------------------------------------- K6+K8 wavefront pipeline
@@ -1695,6 +1740,7 @@ struct RollLane {
                      // (a second px at x = W lands in the row's pitch padding, which no
                      // in-image px ever reads)
   int ys, ye;        // output rows of the segment
+  bool c0;           // wave-uniform: some lane of the wave holds a column <= 0 (the first band)
 };
 
 // x neighbours of px j of the lane: left = px j-1 (previous lane's last px for j = 0),
@@ -1777,24 +1823,33 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
     for (int j = 0; j < PX; ++j) {
       float n1, n2, n3 = 0.0f;
       if (VIN && n == 1)
-        u_from_v<G, FM>(S.U1p[0][j], S.U2p[0][j], S.U3p[0][j], S.P11c[0][j],
+        u_from_v<G, FM, true>(S.U1p[0][j], S.U2p[0][j], S.U3p[0][j], S.P11c[0][j],
                     left_of<PX>(S.P11c[0], j), S.P12c[0][j], S.P12p[0][j], S.P21c[0][j],
                     left_of<PX>(S.P21c[0], j), S.P22c[0][j], S.P22p[0][j], S.P31c[0][j],
                     G ? left_of<PX>(S.P31c[0], j) : 0.0f, S.P32c[0][j], S.P32p[0][j], L.X + j,
-                    yU, a, n1, n2, n3);
+                    yU, a, n1, n2, n3, L.c0);
       else
-        estimate_u_px<G, FM>(S.CX[n - 1][j], S.CY[n - 1][j], S.CR[n - 1][j], S.U1p[n - 1][j],
+        estimate_u_px<G, FM, false, true>(S.CX[n - 1][j], S.CY[n - 1][j], S.CR[n - 1][j], S.U1p[n - 1][j],
                          S.U2p[n - 1][j], S.U3p[n - 1][j], S.P11c[n - 1][j],
                          left_of<PX>(S.P11c[n - 1], j), S.P12c[n - 1][j], S.P12p[n - 1][j],
                          S.P21c[n - 1][j], left_of<PX>(S.P21c[n - 1], j), S.P22c[n - 1][j],
                          S.P22p[n - 1][j], S.P31c[n - 1][j],
                          G ? left_of<PX>(S.P31c[n - 1], j) : 0.0f, S.P32c[n - 1][j],
-                         S.P32p[n - 1][j], L.X + j, yU, a, n1, n2, n3);
+                         S.P32p[n - 1][j], L.X + j, yU, a, n1, n2, n3, L.c0);
       if (n == K && a.calc_err) {
         const float e = residual_px<FM>(S.U1p[n - 1][j] - n1, S.U2p[n - 1][j] - n2);
         acc += stU && L.X + j < a.W ? (double)e : 0.0;
       }
       S.U1c[n][j] = n1; S.U2c[n][j] = n2; if (G) S.U3c[n][j] = n3;
+    }
+    // below the image: u^n(yU) := u^n(yU - 1), so the projection's y-difference at row H-1
+    // is exactly +0 (OpenCV's has_down form) with no per-px select; rows >= H are never
+    // stored (a wave-uniform branch, taken only while a segment drains past the bottom)
+    if (yU >= a.H) {
+#pragma unroll
+      for (int j = 0; j < PX; ++j) {
+        S.U1c[n][j] = S.U1p[n][j]; S.U2c[n][j] = S.U2p[n][j]; if (G) S.U3c[n][j] = S.U3p[n][j];
+      }
     }
     if (n == K) {
       const unsigned vo = stU ? (unsigned)yU * rowb + L.vst : kOOB;
@@ -1804,19 +1859,29 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
     }
 
     const int yD = r - n;        // estimateDualVariables row of stage n
-    const bool has_down = yD + 1 < a.H;
+    // has_down: rows below the image repeat row H-1 (above)
 #pragma unroll
     for (int j = 0; j < PX; ++j) {
       const bool has_right = L.X + j + 1 < a.W;
       dual_px<false, false, FM>(S.U1p[n][j], right_of<PX>(S.U1p[n], j), S.U1c[n][j], has_right,
-                                has_down, a.taut, S.P11p[n - 1][j], S.P12p[n - 1][j],
+                                true, a.taut, S.P11p[n - 1][j], S.P12p[n - 1][j],
                                 S.P11c[n][j], S.P12c[n][j]);
       dual_px<false, false, FM>(S.U2p[n][j], right_of<PX>(S.U2p[n], j), S.U2c[n][j], has_right,
-                                has_down, a.taut, S.P21p[n - 1][j], S.P22p[n - 1][j],
+                                true, a.taut, S.P21p[n - 1][j], S.P22p[n - 1][j],
                                 S.P21c[n][j], S.P22c[n][j]);
       if (G)
-        dual_px<false, false, FM>(S.U3p[n][j], right_of<PX>(S.U3p[n], j), S.U3c[n][j], has_right, has_down,
+        dual_px<false, false, FM>(S.U3p[n][j], right_of<PX>(S.U3p[n], j), S.U3c[n][j], has_right, true,
                 a.taut, S.P31p[n - 1][j], S.P32p[n - 1][j], S.P31c[n][j], S.P32c[n][j]);
+    }
+    // above the image: p^n(yD < 0) := +0, the p2u the next stage's divergence reads on row 0
+    // (divergence<YZ>; OpenCV's y == 0 form).  Only the first K steps of a segment that
+    // starts at row 0 take this wave-uniform branch
+    if (n < K && yD < 0) {
+#pragma unroll
+      for (int j = 0; j < PX; ++j) {
+        S.P11c[n][j] = S.P12c[n][j] = S.P21c[n][j] = S.P22c[n][j] = 0.0f;
+        if (G) S.P31c[n][j] = S.P32c[n][j] = 0.0f;
+      }
     }
     if (n == K) {
       const unsigned vo = L.out && yD >= L.ys && yD < L.ye ? (unsigned)yD * rowb + L.vst : kOOB;
@@ -1865,6 +1930,7 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   const unsigned rowb = 4u * (unsigned)a.P;                 // row pitch in bytes
   L.ys = seg * ra.seg_rows;
   L.ye = imin(L.ys + ra.seg_rows, a.H);
+  L.c0 = band * (BW - 2 * HALO) - HALO <= 0;   // lane 0's first px (wave-uniform)
   const int r0 = imax(L.ys - K, 0);
 
   RollPipe<G, K, PX> S;
@@ -2208,23 +2274,32 @@ __device__ __forceinline__ void wi_s1_step(WiS1<PX> &S, const float *__restrict_
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     float n1, n2, n3;
-    u_from_v<false, FM>(v1[j], v2[j], 0.0f, S.P11c[j], left_of<PX>(S.P11c, j), S.P12c[j],
-                        S.P12p[j], S.P21c[j], left_of<PX>(S.P21c, j), S.P22c[j], S.P22p[j], 0.0f,
-                        0.0f, 0.0f, 0.0f, L.X + j, yU, a, n1, n2, n3);
+    u_from_v<false, FM, true>(v1[j], v2[j], 0.0f, S.P11c[j], left_of<PX>(S.P11c, j), S.P12c[j],
+                              S.P12p[j], S.P21c[j], left_of<PX>(S.P21c, j), S.P22c[j], S.P22p[j],
+                              0.0f, 0.0f, 0.0f, 0.0f, L.X + j, yU, a, n1, n2, n3, L.c0);
     S.U1c[j] = n1; S.U2c[j] = n2;
   }
+  // the rolling pipeline's edge rules (roll_advance): u below the image repeats row H-1,
+  // p above it is +0 -- wave-uniform branches instead of per-px selects
+  if (yU >= a.H) {
+#pragma unroll
+    for (int j = 0; j < PX; ++j) { S.U1c[j] = S.U1p[j]; S.U2c[j] = S.U2p[j]; }
+  }
   const int yD = r - 1;
-  const bool has_down = yD + 1 < a.H;
   float q11[PX], q12[PX], q21[PX], q22[PX], t1[PX], t2[PX];
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     const bool has_right = L.X + j + 1 < a.W;
-    dual_px<false, false, FM>(S.U1p[j], right_of<PX>(S.U1p, j), S.U1c[j], has_right, has_down,
+    dual_px<false, false, FM>(S.U1p[j], right_of<PX>(S.U1p, j), S.U1c[j], has_right, true,
                               a.taut, S.P11p[j], S.P12p[j], q11[j], q12[j]);
-    dual_px<false, false, FM>(S.U2p[j], right_of<PX>(S.U2p, j), S.U2c[j], has_right, has_down,
+    dual_px<false, false, FM>(S.U2p[j], right_of<PX>(S.U2p, j), S.U2c[j], has_right, true,
                               a.taut, S.P21p[j], S.P22p[j], q21[j], q22[j]);
     float t3;
     th_px<false, FM>(wx[j], wy[j], rh[j], S.U1c[j], S.U2c[j], 0.0f, a, t1[j], t2[j], t3);
+  }
+  if (yD < 0) {
+#pragma unroll
+    for (int j = 0; j < PX; ++j) q11[j] = q12[j] = q21[j] = q22[j] = 0.0f;
   }
   float *h = hring + (r & 1) * (kWiH * BW) + PX * lane;
   lds_put<PX>(h, t1);
@@ -2267,9 +2342,9 @@ __device__ __forceinline__ void wi_s2_step(WiS2<PX> &S, const float *__restrict_
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     float n1, n2, n3;
-    u_from_v<false, FM>(S.V1p[j], S.V2p[j], 0.0f, S.Q11c[j], left_of<PX>(S.Q11c, j), S.Q12c[j],
-                        S.Q12p[j], S.Q21c[j], left_of<PX>(S.Q21c, j), S.Q22c[j], S.Q22p[j], 0.0f,
-                        0.0f, 0.0f, 0.0f, L.X + j, yU, a, n1, n2, n3);
+    u_from_v<false, FM, true>(S.V1p[j], S.V2p[j], 0.0f, S.Q11c[j], left_of<PX>(S.Q11c, j),
+                              S.Q12c[j], S.Q12p[j], S.Q21c[j], left_of<PX>(S.Q21c, j), S.Q22c[j],
+                              S.Q22p[j], 0.0f, 0.0f, 0.0f, 0.0f, L.X + j, yU, a, n1, n2, n3, L.c0);
     if (a.calc_err) {
       const float e = residual_px<FM>(S.W1p[j] - n1, S.W2p[j] - n2);
       acc += stU && L.X + j < a.W ? (double)e : 0.0;
@@ -2281,15 +2356,18 @@ __device__ __forceinline__ void wi_s2_step(WiS2<PX> &S, const float *__restrict_
     bstorev<PX>(B.ud, B.ub, vo, S.U1c);
     bstorev<PX>(B.ud, B.ub, vo, S.U2c, ps);
   }
+  if (yU >= a.H) {   // u below the image repeats row H-1 (wi_s1_step)
+#pragma unroll
+    for (int j = 0; j < PX; ++j) { S.U1c[j] = S.U1p[j]; S.U2c[j] = S.U2p[j]; }
+  }
   const int yD = r - 2;
-  const bool has_down = yD + 1 < a.H;
   float o11[PX], o12[PX], o21[PX], o22[PX];
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     const bool has_right = L.X + j + 1 < a.W;
-    dual_px<false, false, FM>(S.U1p[j], right_of<PX>(S.U1p, j), S.U1c[j], has_right, has_down,
+    dual_px<false, false, FM>(S.U1p[j], right_of<PX>(S.U1p, j), S.U1c[j], has_right, true,
                               a.taut, S.Q11p[j], S.Q12p[j], o11[j], o12[j]);
-    dual_px<false, false, FM>(S.U2p[j], right_of<PX>(S.U2p, j), S.U2c[j], has_right, has_down,
+    dual_px<false, false, FM>(S.U2p[j], right_of<PX>(S.U2p, j), S.U2c[j], has_right, true,
                               a.taut, S.Q21p[j], S.Q22p[j], o21[j], o22[j]);
   }
   {
@@ -2343,6 +2421,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     L.vst = 4u * (unsigned)imax(L.X, 0);
     L.ys = ys;
     L.ye = ye;
+    L.c0 = X0 <= 0;
     const RollBufs &Bf = ra.b;
     if (wv == 0) {
       WiS1<PX> S;
@@ -2397,6 +2476,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     L.vst = 4u * (unsigned)imax(L.X, 0);
     L.ys = ys;
     L.ye = ye;
+    L.c0 = X0 <= 0;
     RollPipe<false, K, PX> S;
 #pragma unroll
     for (int n = 0; n <= K; ++n)
