@@ -965,16 +965,14 @@ __device__ __forceinline__ void th_px(float I1wxv, float I1wyv, float rhoc, floa
   const bool mid = gradv > kFltEps;
   // only selected when gradv > FLT_EPSILON
   const float fi = approx(FM) ? -rho * __builtin_amdgcn_rcpf(gradv) : th_quot(rho, gradv, mid);
-  float d1 = mid ? fi * I1wxv : 0.0f;
-  float d2 = mid ? fi * I1wyv : 0.0f;
-  float d3 = mid ? fi * a.gamma : 0.0f;
-  const float ltx = a.l_t * I1wxv, lty = a.l_t * I1wyv, ltz = a.l_t * a.gamma;
-  d1 = hi ? -ltx : d1;
-  d2 = hi ? -lty : d2;
-  d3 = hi ? -ltz : d3;     // +-l_t*gamma
-  d1 = lo ? ltx : d1;
-  d2 = lo ? lty : d2;
-  d3 = lo ? ltz : d3;
+  // d = lo ? l_t*I : hi ? -l_t*I : mid ? fi*I : 0 for I = I1wx, I1wy (gamma): the factor is
+  // selected once and multiplied per component -- (-l_t)*I == -(l_t*I) exactly, and the
+  // "none" case stays a selected +0 (0*I would be -0 for I < 0)
+  const float f = lo ? a.l_t : hi ? -a.l_t : fi;
+  const bool any = lo || hi || mid;
+  const float d1 = any ? f * I1wxv : 0.0f;
+  const float d2 = any ? f * I1wyv : 0.0f;
+  const float d3 = any ? f * a.gamma : 0.0f;     // +-l_t*gamma
   v1 = u1o + d1;
   v2 = u2o + d2;
   v3 = G ? u3o + d3 : 0.0f;
@@ -1656,7 +1654,7 @@ constexpr int kRollMax = 4;
 constexpr int kRollAhead = 2;   // input rows loaded ahead of the row entering the pipeline
 // rows loaded ahead by k_iterate_roll<.., PX>: 16-byte loads (PX = 4) keep as many bytes in
 // flight one row ahead as 8-byte loads two rows ahead, with one ring row less
-template <int PX>
+template <int K, int PX>
 constexpr int roll_ahead() { return PX == 4 ? 1 : kRollAhead; }
 
 // The planes of a streaming pass as five buffer groups, one 4-SGPR descriptor each: the
@@ -1682,13 +1680,15 @@ struct RollArgs {
   int waves;      // bands * segments
 };
 
-// lane i <- lane i-1 (DPP wave_shr:1; lane 0 gets 0)
+// lane i <- lane i-1 (DPP wave_shr:1; lane 0 gets 0).  bound_ctrl: the lane with no source
+// is written 0 by the DPP move itself, so no "old" value has to be put in its destination
+// first (one v_mov per shift)
 __device__ __forceinline__ float from_left(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 // lane i <- lane i+1 (DPP wave_shl:1; lane 63 gets 0)
 __device__ __forceinline__ float from_right(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
 template <bool G, int PX>
@@ -1697,11 +1697,12 @@ struct RollIn {   // one input row at this lane's PX px
   float p11[PX], p12[PX], p21[PX], p22[PX], p31[PX], p32[PX];
 };
 
-// p is loaded unconditionally and zeroed by a select when p == 0 (first pass of a level):
-// a branch here would make the compiler's wait counts conservative for every row.
+// p is loaded unconditionally (a branch here would make the compiler's wait counts
+// conservative for every row); when p == 0 (first pass of a level) its column offset voffp is
+// kOOB, so the buffer loads return +0.0f with no per-px select.
 template <bool G, int PX>
 __device__ __forceinline__ void roll_load(RollIn<G, PX> &v, const RollBufs &B, unsigned soff,
-                                          unsigned voff) {
+                                          unsigned voff, unsigned voffp) {
   const unsigned ps = B.pstride;
   bload<PX>(v.wx, B.c, B.cb, voff, soff);
   bload<PX>(v.wy, B.c, B.cb, voff, soff + ps);
@@ -1709,13 +1710,13 @@ __device__ __forceinline__ void roll_load(RollIn<G, PX> &v, const RollBufs &B, u
   bload<PX>(v.u1, B.us, B.ub, voff, soff);
   bload<PX>(v.u2, B.us, B.ub, voff, soff + ps);
   if (G) bload<PX>(v.u3, B.us, B.ub, voff, soff + 2 * ps);
-  bload<PX>(v.p11, B.ps, B.pb, voff, soff);
-  bload<PX>(v.p12, B.ps, B.pb, voff, soff + ps);
-  bload<PX>(v.p21, B.ps, B.pb, voff, soff + 2 * ps);
-  bload<PX>(v.p22, B.ps, B.pb, voff, soff + 3 * ps);
+  bload<PX>(v.p11, B.ps, B.pb, voffp, soff);
+  bload<PX>(v.p12, B.ps, B.pb, voffp, soff + ps);
+  bload<PX>(v.p21, B.ps, B.pb, voffp, soff + 2 * ps);
+  bload<PX>(v.p22, B.ps, B.pb, voffp, soff + 3 * ps);
   if (G) {
-    bload<PX>(v.p31, B.ps, B.pb, voff, soff + 4 * ps);
-    bload<PX>(v.p32, B.ps, B.pb, voff, soff + 5 * ps);
+    bload<PX>(v.p31, B.ps, B.pb, voffp, soff + 4 * ps);
+    bload<PX>(v.p32, B.ps, B.pb, voffp, soff + 5 * ps);
   }
 }
 
@@ -1735,6 +1736,8 @@ struct RollPipe {
 struct RollLane {
   int X;             // first px of the lane
   unsigned vload;    // byte offset of the (clamped) load column
+  unsigned vloadp;   // the p loads' column offset: kOOB when p = 0 (the first pass of a level),
+                     // where out-of-range buffer loads return +0.0f
   unsigned vst;      // byte offset of the lane's store column (out lanes only)
   bool out;          // lane is in the band interior and its first px inside the image
                      // (a second px at x = W lands in the row's pitch padding, which no
@@ -1774,7 +1777,8 @@ __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G,
                                           RollIn<G, PX> &ahead, const IterArgs &a,
                                           const RollBufs &B, int r, const RollLane &L,
                                           unsigned rowb, double &acc) {
-  roll_load<G, PX>(ahead, B, (unsigned)imin(r + roll_ahead<PX>(), a.H - 1) * rowb, L.vload);
+  roll_load<G, PX>(ahead, B, (unsigned)imin(r + roll_ahead<K, PX>(), a.H - 1) * rowb, L.vload,
+                   L.vloadp);
   // keep the loads of row r + roll_ahead ahead of this step's stores: waiting for them
   // roll_ahead steps later then leaves the younger stores and loads in flight (vmcnt
   // counts in issue order)
@@ -1807,12 +1811,12 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
     for (int n = K - 1; n >= 1; --n) {
       S.CX[n][j] = S.CX[n - 1][j]; S.CY[n][j] = S.CY[n - 1][j]; S.CR[n][j] = S.CR[n - 1][j];
     }
-    const bool z = a.p_zero;
+    // (p = 0 on a level's first pass: the loads returned +0, RollLane::vloadp)
     S.CX[0][j] = in.wx[j]; S.CY[0][j] = in.wy[j]; S.CR[0][j] = in.rh[j];
     S.U1p[0][j] = in.u1[j]; S.U2p[0][j] = in.u2[j]; S.U3p[0][j] = G ? in.u3[j] : 0.0f;
-    S.P11c[0][j] = z ? 0.0f : in.p11[j]; S.P12c[0][j] = z ? 0.0f : in.p12[j];
-    S.P21c[0][j] = z ? 0.0f : in.p21[j]; S.P22c[0][j] = z ? 0.0f : in.p22[j];
-    S.P31c[0][j] = (z || !G) ? 0.0f : in.p31[j]; S.P32c[0][j] = (z || !G) ? 0.0f : in.p32[j];
+    S.P11c[0][j] = in.p11[j]; S.P12c[0][j] = in.p12[j];
+    S.P21c[0][j] = in.p21[j]; S.P22c[0][j] = in.p22[j];
+    S.P31c[0][j] = G ? in.p31[j] : 0.0f; S.P32c[0][j] = G ? in.p32[j] : 0.0f;
   }
 
 #pragma unroll
@@ -1925,6 +1929,7 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   // load column: clamped so all PX px lie in the row's pitch (px >= W are never used by
   // a px < W: the right clamp and the x = 0 divergence form select)
   L.vload = 4u * imin(imax(L.X, 0), a.P - PX);
+  L.vloadp = a.p_zero ? kOOB : L.vload;
   L.out = PX * lane >= HALO && PX * lane < BW - HALO && L.X < a.W;
   L.vst = 4u * (unsigned)imax(L.X, 0);
   const unsigned rowb = 4u * (unsigned)a.P;                 // row pitch in bytes
@@ -1969,9 +1974,9 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
     }
   };
   double acc = 0.0;
-  if constexpr (roll_ahead<PX>() == 1) {   // 2-row ring, steps unrolled by 2
+  if constexpr (roll_ahead<K, PX>() == 1) {   // 2-row ring, steps unrolled by 2
     RollIn<G, PX> A, Bx;
-    roll_load<G, PX>(A, B, (unsigned)r0 * rowb, L.vload);
+    roll_load<G, PX>(A, B, (unsigned)r0 * rowb, L.vload, L.vloadp);
     dummy_stores();
     const int halves = (L.ye + K - r0 + 1) / 2;
     for (int h = 0, r = r0; h < halves; ++h, r += 2) {
@@ -1979,11 +1984,11 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
       roll_step<G, K, PX, FM>(S, Bx, A, a, B, r + 1, L, rowb, acc);
     }
   } else {   // 3-row ring, steps unrolled by 3
-    static_assert(roll_ahead<PX>() == 2, "the step loop below is unrolled for a 3-row ring");
+    static_assert(roll_ahead<K, PX>() == 2, "the step loop below is unrolled for a 3-row ring");
     RollIn<G, PX> A, Bx, C;
-    roll_load<G, PX>(A, B, (unsigned)r0 * rowb, L.vload);
+    roll_load<G, PX>(A, B, (unsigned)r0 * rowb, L.vload, L.vloadp);
     dummy_stores();
-    roll_load<G, PX>(Bx, B, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
+    roll_load<G, PX>(Bx, B, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload, L.vloadp);
     dummy_stores();
     // steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K (rows >= H drain the pipeline)
     const int thirds = (L.ye + K - r0 + 2) / 3;
@@ -2164,7 +2169,7 @@ __device__ __forceinline__ void wi_cons_step(RollPipe<false, 2, PX> &S,
                                              WiP<PX> &ahead, const IterArgs &a,
                                              const RollBufs &B, int r, const RollLane &L,
                                              int lane, unsigned rowb, double &acc) {
-  wi_p_load(ahead, B, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vload);
+  wi_p_load(ahead, B, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vloadp);
   __builtin_amdgcn_sched_barrier(0);
   lds_barrier();   // C ring row r was written at the previous step
   constexpr int BW = 64 * PX;
@@ -2244,7 +2249,7 @@ __device__ __forceinline__ void wi_s1_step(WiS1<PX> &S, const float *__restrict_
                                            float *__restrict__ hring, const WiP<PX> &cur,
                                            WiP<PX> &ahead, const IterArgs &a, const RollBufs &B,
                                            int r, const RollLane &L, int lane, unsigned rowb) {
-  wi_p_load(ahead, B, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vload);
+  wi_p_load(ahead, B, (unsigned)imin(r + kRollAhead, a.H - 1) * rowb, L.vloadp);
   __builtin_amdgcn_sched_barrier(0);
   lds_barrier();   // C ring row r was written at the previous step; hand-off slot r & 1 read
   constexpr int BW = 64 * PX;
@@ -2262,13 +2267,12 @@ __device__ __forceinline__ void wi_s1_step(WiS1<PX> &S, const float *__restrict_
       th_px<false, FM>(wx[j], wy[j], rh[j], v1[j], v2[j], 0.0f, a, v1[j], v2[j], t3);
     }
   }
-  const bool z = a.p_zero;
 #pragma unroll
-  for (int j = 0; j < PX; ++j) {
+  for (int j = 0; j < PX; ++j) {   // (p = 0 on a level's first pass: RollLane::vloadp)
     S.U1p[j] = S.U1c[j]; S.U2p[j] = S.U2c[j];
     S.P11p[j] = S.P11c[j]; S.P12p[j] = S.P12c[j]; S.P21p[j] = S.P21c[j]; S.P22p[j] = S.P22c[j];
-    S.P11c[j] = z ? 0.0f : cur.p11[j]; S.P12c[j] = z ? 0.0f : cur.p12[j];
-    S.P21c[j] = z ? 0.0f : cur.p21[j]; S.P22c[j] = z ? 0.0f : cur.p22[j];
+    S.P11c[j] = cur.p11[j]; S.P12c[j] = cur.p12[j];
+    S.P21c[j] = cur.p21[j]; S.P22c[j] = cur.p22[j];
   }
   const int yU = r;
 #pragma unroll
@@ -2417,6 +2421,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     RollLane L;
     L.X = X0 + PX * lane;
     L.vload = 4u * imin(imax(L.X, 0), a.P - PX);
+    L.vloadp = a.p_zero ? kOOB : L.vload;
     L.out = PX * lane >= HALO && PX * lane < BW - HALO && L.X < a.W;
     L.vst = 4u * (unsigned)imax(L.X, 0);
     L.ys = ys;
@@ -2432,8 +2437,8 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
         S.P11p[j] = S.P12p[j] = S.P21p[j] = S.P22p[j] = 0.0f;
       }
       WiP<PX> A, B, C;
-      wi_p_load(A, Bf, (unsigned)r0 * rowb, L.vload);
-      wi_p_load(B, Bf, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
+      wi_p_load(A, Bf, (unsigned)r0 * rowb, L.vloadp);
+      wi_p_load(B, Bf, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vloadp);
       lds_barrier();   // the producers' first step (row r0)
       for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
         progress_prio<PRIO>(h, thirds);
@@ -2472,6 +2477,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     RollLane L;
     L.X = X0 + PX * lane;
     L.vload = 4u * imin(imax(L.X, 0), a.P - PX);
+    L.vloadp = a.p_zero ? kOOB : L.vload;
     L.out = PX * lane >= HALO && PX * lane < BW - HALO && L.X < a.W;
     L.vst = 4u * (unsigned)imax(L.X, 0);
     L.ys = ys;
@@ -2505,9 +2511,9 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
       bstorev<PX>(Bf.pd, Bf.pb, kOOB, z, 3 * ps);
     };
     WiP<PX> A, B, C;
-    wi_p_load(A, Bf, (unsigned)r0 * rowb, L.vload);
+    wi_p_load(A, Bf, (unsigned)r0 * rowb, L.vloadp);
     dummy_stores();
-    wi_p_load(B, Bf, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vload);
+    wi_p_load(B, Bf, (unsigned)imin(r0 + 1, a.H - 1) * rowb, L.vloadp);
     dummy_stores();
     lds_barrier();   // the producers' first step (row r0)
     double acc = 0.0;
