@@ -1062,19 +1062,23 @@ __device__ __forceinline__ float sqrt_rn_core(float xs) {
   const float r = rm <= 0.0f ? sm : s;
   return rp > 0.0f ? sp : r;
 }
-// BR: lanes below 2^-96 (rare: both differences under 2^-48) take the scaled form in a
-// branch the wavefront skips when no lane needs it -- faster in the looped k_iterate_tb,
-// slower in the unrolled pipelines, which select instead.
+// x in (0, 2^-96) takes the scaled form (x*2^32, then *2^-16) in a branch the wavefront skips
+// when none of its lanes has such an x: both differences under 2^-48 yet not both zero, which
+// essentially never happens.  +0 (a locally constant u: every px of a first iteration on the
+// coarsest level) needs no scaling -- the core returns +0 exactly -- so it no longer sends the
+// wavefront into the scaled form, which made the branch slower than a select in the
+// unrolled pipelines (r2).  One unsigned compare finds (0, 2^-96): bits(x) - 1 wraps +0 (and
+// keeps NaN) above bits(2^-96) - 1.
 template <bool BR>
 __device__ __forceinline__ float sqrt_nn(float x) {
-  if (BR) {
-    float r = sqrt_rn_core(x);
-    if (x < 0x1p-96f) r = sqrt_rn_core(x * 0x1p32f) * 0x1p-16f;
-    return r;
+  (void)BR;
+  float r = sqrt_rn_core(x);
+  const bool tiny = __float_as_uint(x) - 1u < __float_as_uint(0x1p-96f) - 1u;
+  if (__ballot(tiny)) {
+    asm volatile("" ::: "memory");   // keep it a branch (see divergence)
+    r = tiny ? sqrt_rn_core(x * 0x1p32f) * 0x1p-16f : r;
   }
-  const bool small = x < 0x1p-96f;
-  const float r = sqrt_rn_core(small ? x * 0x1p32f : x);
-  return small ? r * 0x1p-16f : r;
+  return r;
 }
 
 template <bool BR = false>
