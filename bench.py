@@ -323,6 +323,15 @@ def run_stack(args, rank, world, local_rank, dist):
     threads = [threading.Thread(target=worker, args=(j,)) for j in range(F)]
     for t in threads:
         t.start()
+    # a progress line on stderr every 30 s (a full C4/C5 stack runs for minutes)
+    while True:
+        alive = [t for t in threads if t.is_alive()]
+        if not alive:
+            break
+        alive[0].join(timeout=30.0)
+        if alive[0].is_alive():
+            print(f"[rank {rank}] {sum(done)} pairs in {time.perf_counter() - t0:.0f} s",
+                  file=sys.stderr, flush=True)
     for t in threads:
         t.join()
     torch.cuda.synchronize(dev)
