@@ -37,7 +37,7 @@ struct BatchSel {            // the pairs a launch works on, passed by value
 __device__ __forceinline__ int bsel_bit(const BatchMask &m, int b) { return m.test(b); }
 
 // K1 convertTo for both frames of every pair: blockIdx.z = 2 * pair + frame.
-__global__ void kb_convert(const uint8_t *__restrict__ I0, size_t p0, size_t s0,
+TVL1_PLAIN __global__ void kb_convert(const uint8_t *__restrict__ I0, size_t p0, size_t s0,
                            const uint8_t *__restrict__ I1, size_t p1, size_t s1,
                            float *__restrict__ d0, float *__restrict__ d1, int W, int H, int P,
                            size_t ps) {
@@ -214,7 +214,7 @@ struct BatchMedian {
   int W, H, P, ksize;
   BatchSel sel;
 };
-__global__ void kb_median(BatchMedian w) {
+TVL1_PLAIN __global__ void kb_median(BatchMedian w) {
   const int x = blockIdx.x * 64 + threadIdx.x;
   const int y = blockIdx.y * 4 + threadIdx.y;
   if (x >= w.W || y >= w.H) return;
@@ -240,7 +240,7 @@ __global__ void kb_median(BatchMedian w) {
 }
 
 // K7 for the selected pairs: fixed-order sum of pair b's partials into out[b].
-__global__ void kb_reduce(const double *__restrict__ partials, int n, BatchSel sel,
+TVL1_PLAIN __global__ void kb_reduce(const double *__restrict__ partials, int n, BatchSel sel,
                           double *__restrict__ out) {
   __shared__ double s[kBlock];
   const int b = sel.idx[blockIdx.x];
@@ -286,7 +286,7 @@ struct BatchOut {
   size_t fpitch, fstride;
   BatchSel sel;
 };
-__global__ void kb_output(BatchOut w) {
+TVL1_PLAIN __global__ void kb_output(BatchOut w) {
   const int x = blockIdx.x * 64 + threadIdx.x;
   const int y = blockIdx.y * 4 + threadIdx.y;
   if (x >= w.W || y >= w.H) return;

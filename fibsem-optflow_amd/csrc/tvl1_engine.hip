@@ -25,6 +25,13 @@
 #include "tvl1_batch.hpp"
 #include "tvl1_align.hpp"
 
+// the iteration passes are compiled in tvl1_passes.hip (another instruction scheduler)
+namespace tvl1k {
+#define TVL1_PASS_INSTANCE(...) extern template __global__ void __VA_ARGS__;
+#include "tvl1_passes.inc"
+#undef TVL1_PASS_INSTANCE
+}  // namespace tvl1k
+
 using namespace tvl1k;
 
 namespace {

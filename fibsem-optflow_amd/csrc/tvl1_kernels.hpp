@@ -29,6 +29,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// The non-template kernels are defined once, in tvl1_engine.hip's translation unit.
+// tvl1_passes.hip includes these headers for its template instantiations only: there they
+// are declared as never-instantiated templates, so that unit emits no code for them.
+#ifdef TVL1_PASSES_TU
+#define TVL1_PLAIN template <int TVL1_PASSES_TU_UNUSED = 0>
+#else
+#define TVL1_PLAIN
+#endif
+
 namespace tvl1k {
 
 constexpr int kWave = 64;
@@ -142,7 +151,7 @@ __device__ __forceinline__ void bload(float (&d)[PX], const float *p, unsigned b
 
 // ---------------------------------------------------------------- K1 convert
 // GpuMat::convertTo(CV_32F, 1.0) for both frames (blockIdx.z selects the frame).
-__global__ void k_convert_u8(const uint8_t *__restrict__ s0, size_t sp0,
+TVL1_PLAIN __global__ void k_convert_u8(const uint8_t *__restrict__ s0, size_t sp0,
                              const uint8_t *__restrict__ s1, size_t sp1,
                              float *__restrict__ d0, float *__restrict__ d1, int W, int H,
                              int P) {
@@ -157,7 +166,7 @@ __global__ void k_convert_u8(const uint8_t *__restrict__ s0, size_t sp0,
 
 // [A.1] for CV_32FC1 inputs: convertTo(CV_32F, 255.0) = src * 255 + 0 (nvcc contracts it
 // to fma(255, src, 0): the same value, -0 becomes +0 either way).  Pitches in bytes.
-__global__ void k_convert_f32(const float *__restrict__ s0, size_t sp0,
+TVL1_PLAIN __global__ void k_convert_f32(const float *__restrict__ s0, size_t sp0,
                               const float *__restrict__ s1, size_t sp1,
                               float *__restrict__ d0, float *__restrict__ d1, int W, int H,
                               int P) {
@@ -241,7 +250,7 @@ __global__ void k_upsample(const float *__restrict__ s1, const float *__restrict
 
 // ---------------------------------------------------------------- K3 gradient
 // centeredGradient of I1, written interleaved (I1, I1x, I1y, 0) for the K5 gather.
-__global__ void k_gradient(const float *__restrict__ I, int W, int H, int P,
+TVL1_PLAIN __global__ void k_gradient(const float *__restrict__ I, int W, int H, int P,
                            float4 *__restrict__ G) {
   const int x = blockIdx.x * 64 + threadIdx.x;
   const int y = blockIdx.y * 4 + threadIdx.y;
@@ -261,7 +270,7 @@ __global__ void k_gradient(const float *__restrict__ I, int W, int H, int P,
 // float), x clamped to the edge columns (f := 0, the last column a single tap), the two
 // rows clamped but their weights kept; or the exact-2x INTER_AREA fast path.  Planes by
 // blockIdx.z (< nmul of them are then multiplied by mul: cv::multiply(u, 1/scaleStep)).
-__global__ void k_resize_hp(const float *__restrict__ s0, const float *__restrict__ s1,
+TVL1_PLAIN __global__ void k_resize_hp(const float *__restrict__ s0, const float *__restrict__ s1,
                             const float *__restrict__ s2, int sw, int sh, int sp,
                             float *__restrict__ d0, float *__restrict__ d1,
                             float *__restrict__ d2, int dw, int dh, int dp, double scale_x,
@@ -315,7 +324,7 @@ __device__ __forceinline__ int round_map(float v) {
   if (!(v > -2147483648.f && v < 2147483648.f)) return (int)0x80000000u;
   return (int)rintf(v);
 }
-__global__ void k_remap_cubic(const float *__restrict__ I0, const float4 *__restrict__ G,
+TVL1_PLAIN __global__ void k_remap_cubic(const float *__restrict__ I0, const float4 *__restrict__ G,
                               const float *__restrict__ u1, const float *__restrict__ u2,
                               int W, int H, int P, float *__restrict__ I1wx,
                               float *__restrict__ I1wy, float *__restrict__ rho) {
@@ -2640,7 +2649,7 @@ __host__ __device__ inline int sched_after(double prev, double thr, int n, int i
   return k;
 }
 
-__global__ void k_reduce(const double *__restrict__ partials, int n, double *__restrict__ out,
+TVL1_PLAIN __global__ void k_reduce(const double *__restrict__ partials, int n, double *__restrict__ out,
                          unsigned long long *seq_out, unsigned long long seq, CheckGate g) {
   if (gated_off(g.in, g.in_seq)) return;
   __shared__ double s[kBlock];
@@ -2675,7 +2684,7 @@ __global__ void k_reduce(const double *__restrict__ partials, int n, double *__r
 
 // ---------------------------------------------------------------- misc
 // Build-only median (cv::medianBlur CV_32F, ksize 3 or 5, BORDER_REPLICATE); blockIdx.z = component.
-__global__ void k_median(const float *__restrict__ s1, const float *__restrict__ s2, int W,
+TVL1_PLAIN __global__ void k_median(const float *__restrict__ s1, const float *__restrict__ s2, int W,
                          int H, int P, int ksize, float *__restrict__ d1,
                          float *__restrict__ d2) {
   const int x = blockIdx.x * 64 + threadIdx.x;
@@ -2702,7 +2711,7 @@ __global__ void k_median(const float *__restrict__ s1, const float *__restrict__
 }
 
 // Final flow (u1[0], u2[0]) -> caller's pitched planar outputs (A.4 + cuda::split).
-__global__ void k_output(const float *__restrict__ u1, const float *__restrict__ u2, int W,
+TVL1_PLAIN __global__ void k_output(const float *__restrict__ u1, const float *__restrict__ u2, int W,
                          int H, int P, float *__restrict__ ou, float *__restrict__ ov,
                          size_t opitch) {
   const int x = blockIdx.x * 64 + threadIdx.x;
@@ -2716,7 +2725,7 @@ __global__ void k_output(const float *__restrict__ u1, const float *__restrict__
 // features branch with output_type "flow" (mode 2: (flow + grid) warped by the
 // alignment, identity here, minus grid); then zero where I1 <= 1
 // (threshold THRESH_BINARY_INV + setTo(0, mask)).
-__global__ void k_postprocess(float *__restrict__ u, float *__restrict__ v, size_t fp,
+TVL1_PLAIN __global__ void k_postprocess(float *__restrict__ u, float *__restrict__ v, size_t fp,
                               const uint8_t *__restrict__ I1, size_t p1, int W, int H,
                               int mode) {
   const int x = blockIdx.x * 64 + threadIdx.x;
