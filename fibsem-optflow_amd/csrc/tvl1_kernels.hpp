@@ -1920,7 +1920,12 @@ constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
 
 // The pass of one wavefront (band / segment wid < ra.waves); k_iterate_roll and the
 // batched kb_iterate_roll differ only in how they find their planes and wid.
-template <bool G, int K, int PX, int FM>
+// PRIO: issue priority falling with the segment's progress (progress_prio), for
+// k_iterate_roll: a launch is one round of the resident slots, and at equal priority the
+// waves dispatched last on a SIMD would finish last (one C2 pair alone: <4,2> 317 -> 307 us,
+// <2,2> 52.2 -> 50.5 us per launch; in flight neutral; the batched passes keep 0, where it
+// measured -0.7 %: profiles/r3/ab_roll_prio.txt)
+template <bool G, int K, int PX, int FM, int PRIO = 0>
 __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   constexpr int HALO = roll_halo<K, PX>();
   constexpr int BW = 64 * PX;            // band width (px)
@@ -1993,6 +1998,7 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
     dummy_stores();
     const int halves = (L.ye + K - r0 + 1) / 2;
     for (int h = 0, r = r0; h < halves; ++h, r += 2) {
+      progress_prio<PRIO>(h, halves);
       roll_step<G, K, PX, FM>(S, A, Bx, a, B, r, L, rowb, acc);
       roll_step<G, K, PX, FM>(S, Bx, A, a, B, r + 1, L, rowb, acc);
     }
@@ -2006,6 +2012,7 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
     // steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K (rows >= H drain the pipeline)
     const int thirds = (L.ye + K - r0 + 2) / 3;
     for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
+      progress_prio<PRIO>(h, thirds);
       roll_step<G, K, PX, FM>(S, A, C, a, B, r, L, rowb, acc);
       roll_step<G, K, PX, FM>(S, Bx, A, a, B, r + 1, L, rowb, acc);
       roll_step<G, K, PX, FM>(S, C, Bx, a, B, r + 2, L, rowb, acc);
@@ -2024,7 +2031,7 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
   const int wid =
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
   if (wid >= ra.waves || gated_off(ra.it.gate, ra.it.gate_seq)) return;   // whole wavefronts
-  roll_body<G, K, PX, FM>(ra, wid);
+  roll_body<G, K, PX, FM, 1>(ra, wid);
 }
 
 // ---------------------------------------------------------------- K5 + first pass, two roles

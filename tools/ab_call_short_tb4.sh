@@ -1,4 +1,5 @@
-# r3 probe: 2-iteration passes on small levels in k_iterate_tb4 (TVL1_SHORT_TB4=1) vs k_iterate_roll<2,2>
+# r3 probe (record; the TVL1_SHORT_TB4 knob it sets was removed after this A/B, profiles/r3/ab_short_tb4.txt):
+# 2-iteration passes on small levels in k_iterate_tb4 vs k_iterate_roll<2,2>
 set -o pipefail
 mkdir -p gpurun_out
 TVL1_SHORT_TB4=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_batch.py -x -q --timeout 200 \
