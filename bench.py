@@ -522,16 +522,50 @@ def strips_line(args, rank, world, local_rank, dist):
             "api": "tvl1_calc_batch (DESIGN.md 4.6)"}
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) started plainly, without a launcher: start
+    `torch.distributed.run --nproc-per-node N bench.py <same args>` as a CHILD process (one
+    rank per GPU, as the reference runs one process per shard: gen_cross_file_list.py:26-27,
+    janelia_run.sh:3) and return its exit code.  Called before torch is imported, so this
+    process never touches the GPU (no exec from a GPU-initialised process).  Rank 0's JSON
+    line reaches our stdout through the inherited descriptor."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           str(ROOT / "bench.py"), *sys.argv[1:]]
+    if os.environ.get("BENCH_LAUNCH_DRYRUN") == "1":   # tests/test_bench_launch_cpu.py
+        print(json.dumps({"launch": cmd, "torch_imported": "torch" in sys.modules}), flush=True)
+        return 0
+    print(f"[bench] --gpus {n} without a launcher: starting {n} ranks via "
+          f"torch.distributed.run", file=sys.stderr, flush=True)
+    child = subprocess.Popen(cmd, cwd=str(ROOT))
+
+    def forward(sig, _frame):   # a driver's SIGTERM / Ctrl-C reaches the ranks too
+        child.send_signal(sig)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
+    return child.wait()
+
+
 def main():
     args = parse()
-    import numpy as np
-    import torch
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        # a line claiming N GPUs must come from N ranks (n_gpus is WORLD_SIZE)
+        sys.exit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE {world} "
+                 f"ranks")
+    import numpy as np
+    import torch
+
     dist = None
     # nccl (= RCCL) by default; BENCH_DIST_BACKEND=gloo rehearses the N > 1 path on fewer
     # GPUs than ranks (ranks share devices round-robin; the collectives here are only the

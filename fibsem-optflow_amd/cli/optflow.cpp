@@ -496,7 +496,26 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
   const size_t fp = (size_t)W * sizeof(float);
   tvl1_stats st;
   memset(&st, 0, sizeof st);
+  // per-warp executed iterations (level-major), reported in stats_json beside the totals
+  std::vector<int32_t> warp_iters((size_t)TVL1_MAX_LEVELS * std::max(1, prm.warps), -1);
+  st.warp_iterations = warp_iters.data();
+  st.warp_iterations_capacity = (int32_t)warp_iters.size();
   const auto t0 = std::chrono::steady_clock::now();
+  auto record = [&] {
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    Value sv;
+    sv["roi"][0] = r0.x;
+    sv["roi"][1] = r0.y;
+    sv["roi"][2] = W;
+    sv["roi"][3] = H;
+    sv["seconds"] = secs;
+    sv["levels"] = st.levels;
+    sv["iterations"] = (int64_t)st.iterations_total;
+    sv["checks"] = (int64_t)st.checks_total;
+    const size_t nw = std::min(warp_iters.size(), (size_t)std::max(0, st.levels) * std::max(1, prm.warps));
+    for (size_t k = 0; k < nw; ++k) sv["warp_iterations"][(int)k] = warp_iters[k];
+    res.stats["solves"].append(sv);
+  };
   tvl1_status s = tvl1_calc(dc.ctx, a, pitch, b, pitch1, W, H, dc.du, dc.dv, fp, &st, dc.stream);
   if (s != TVL1_OK) {
     err = tvl1_last_error(dc.ctx), dc.faulted = device_fault(s);
@@ -522,17 +541,7 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
       err = "solve failed", dc.faulted = true;
       return false;
     }
-    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    Value sv;
-    sv["roi"][0] = r0.x;
-    sv["roi"][1] = r0.y;
-    sv["roi"][2] = W;
-    sv["roi"][3] = H;
-    sv["seconds"] = secs;
-    sv["levels"] = st.levels;
-    sv["iterations"] = (int64_t)st.iterations_total;
-    sv["checks"] = (int64_t)st.checks_total;
-    res.stats["solves"].append(sv);
+    record();
     return random_points_sampled(dc, fp, W, H, f0, f1, r0, r1, im, args, features, err);
   }
   ofio::HostVec<float> fx((size_t)W * H), fy((size_t)W * H);   // pinned (PinnedPool)
@@ -542,17 +551,7 @@ bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1
     err = "flow download failed", dc.faulted = true;
     return false;
   }
-  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  Value sv;
-  sv["roi"][0] = r0.x;
-  sv["roi"][1] = r0.y;
-  sv["roi"][2] = W;
-  sv["roi"][3] = H;
-  sv["seconds"] = secs;
-  sv["levels"] = st.levels;
-  sv["iterations"] = (int64_t)st.iterations_total;
-  sv["checks"] = (int64_t)st.checks_total;
-  res.stats["solves"].append(sv);
+  record();
   if (otype == "map" || otype == "flow") {
     const std::string base = im["output"].asString() + im["output_suffix"].asString();
     std::string e;

@@ -1,0 +1,53 @@
+"""bench.py's launch contract on CPU (VERDICT r3 "next" item 2): a plain `bench.py --gpus N`
+(no launcher, WORLD_SIZE unset) starts N ranks itself -- `torch.distributed.run
+--nproc-per-node N` as a child process, before torch (or HIP) is imported, never an exec --
+and a launcher whose WORLD_SIZE disagrees with --gpus is an error, so a line can only claim
+n_gpus = N when N ranks ran.  The reference scales by one process per shard
+(/root/reference/support_scripts/gen_cross_file_list.py:26-27, singularity/janelia_run.sh:3).
+The GPU side (2 gloo ranks through the plain launch) is tests/test_gpu_stack.py."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def run(args, **env):
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    e.update(env)
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True,
+                          text=True, timeout=60, env=e, cwd=str(ROOT))
+
+
+def test_plain_multi_gpu_launch_spawns_ranks_before_torch():
+    r = run(["--gpus", "8", "--steps", "3", "--warmup", "1"], BENCH_LAUNCH_DRYRUN="1")
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["torch_imported"] is False
+    cmd = out["launch"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert int(cmd[cmd.index("--master-port") + 1]) > 0
+    # the same arguments reach every rank
+    i = cmd.index(str(ROOT / "bench.py"))
+    assert cmd[i + 1:] == ["--gpus", "8", "--steps", "3", "--warmup", "1"]
+
+
+def test_one_gpu_does_not_spawn():
+    # --gpus 1 runs in this process (no launcher needed): without a GPU it fails inside the
+    # bench, but never prints a launch line
+    r = run(["--gpus", "1", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+             "--no-strips-line", "--no-fast-math-line", "--width", "64", "--height", "48"],
+            BENCH_LAUNCH_DRYRUN="1")
+    assert '"launch"' not in r.stdout
+
+
+def test_launcher_world_size_must_match_gpus():
+    r = run(["--gpus", "8"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    assert r.returncode != 0
+    assert "WORLD_SIZE 2" in r.stderr
+    assert not r.stdout.strip()

@@ -50,6 +50,30 @@ def stack_run(tmp_path_factory, built):
     return d, json.loads(line)
 
 
+def test_plain_launch_runs_n_ranks(built, tmp_path):
+    """`bench.py --gpus 2` started plainly, as the driver's bench command is written (no
+    torch.distributed.run in front): bench.py starts the 2 ranks itself,
+    so the line says n_gpus 2 and every pair is solved exactly once across both ranks."""
+    z, strides = 10, (1, 4)
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--workload", "stack",
+           "--slices", str(z), "--width", "128", "--height", "96",
+           "--strides", ",".join(map(str, strides)), "--chunk", "2", "--inflight", "2",
+           "--nscales", "3", "--warps", "3", "--dump", str(tmp_path)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["process_group"] == "gloo"
+    want = {(s, k) for s in strides for k in range(z - s)}
+    assert out["config"]["pairs"] == len(want)
+    got = [tuple(int(t[1:]) for t in f.name.split("_")[1:3])
+           for f in tmp_path.glob("pair_s*_z*_r*.npz")]
+    assert sorted(got) == sorted(want)
+    assert {int(np.load(f)["rank"]) for f in tmp_path.glob("*.npz")} <= {0, 1}
+
+
 def expected_pairs():
     return {(s, z) for s in STRIDES for z in range(Z - s)}
 
