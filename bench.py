@@ -63,9 +63,10 @@ METRIC = "slice-pairs/sec (6k×4k, 5 scales, 30 warps) at 1/2/4/8 GPUs; % HBM ro
 
 
 PAIR_KERNEL = ("iteration passes: estimateU + estimateDualVariables + residual partials, <= 4 "
-               "iterations per HBM pass (k_iterate_roll wavefront pipeline / k_iterate_tb blocked "
-               "regions; on levels >= 5 Mpx each warp's first pass is k_warp_iter, warpBackward "
-               "fused in)")
+               "iterations per HBM pass (k_iterate_roll wavefront pipeline; long passes on levels "
+               "too small to fill the GPU with streaming segments in k_iterate_tb4's 64x48 "
+               "blocked regions; on levels >= 4 Mpx each warp's first pass is k_warp_iter, "
+               "warpBackward fused in)")
 STRIP_KERNEL = ("batched iteration passes of one tvl1_calc_batch call: kb_iterate_roll<K, 2> "
                 "(<= 4 iterations per HBM pass, a pair index per launch) and kb_warp_iter "
                 "(warpBackward fused with each warp's first pass)")

@@ -724,6 +724,17 @@ bool solve_rois(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1_in
   }
   bool realloc = false;
   if (!ensure(dc, img_bytes, std::max<size_t>(flow_bytes, 4), realloc, err)) return false;
+  // PinnedPool's invariant (cli/imageio.hpp): a host buffer goes back to the pool only after
+  // the stream that reads it was synchronised.  Every successful path below ends in a
+  // synchronising download; a failing one (an ROI outside the image, EINVAL / ESIZE, an
+  // alignment error) may leave the uploads of f0 / f1 queued, so it waits here.
+  struct SyncOnFailure {
+    DeviceCtx &dc;
+    bool ok = false;
+    ~SyncOnFailure() {
+      if (!ok && dc.stream) (void)hipStreamSynchronize(dc.stream);
+    }
+  } sync_guard{dc};
   if (realloc) f0_resident = f1_resident = false;
   // GpuMat::upload (optflow.cpp:315-316), skipped when the slice is already resident
   if (!f0_resident && hipMemcpyAsync(dc.d0, f0.data.data(), f0.data.size(), hipMemcpyHostToDevice, dc.stream) != hipSuccess) {
@@ -767,6 +778,7 @@ bool solve_rois(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1_in
     if (!solve_wrapper(dc, f0, *f1p, r0, r1, im, args, features, affine, res, err)) ok = false;
   }
   if (otype == "random_points") res.pms.push_back(move_pm(im));
+  sync_guard.ok = ok;
   return ok;
 }
 

@@ -85,6 +85,9 @@ struct tvl1_ctx {
   int poll = 1;                      // TVL1_POLL: wait for a residual by polling its
                                      // sequence number in host memory (0: event sync)
   hipEvent_t ev_order = nullptr;  // orders work on the caller's stream after a zero fill
+  hipEvent_t ev_switch = nullptr; // orders a call on a new stream after the previous stream
+  hipStream_t last_stream = nullptr;   // the stream the ctx's last call enqueued on
+  bool last_stream_valid = false;
   struct Retired {                // an arena outgrown while possibly in use (arena_alloc)
     char *p;
     std::vector<hipEvent_t> done;   // recorded on every stream the ctx has worked on
@@ -274,13 +277,17 @@ static int iterate_blocks(int W, int H) {
 
 // (Re)allocate one of the ctx's scratch arenas, zero-filled, for work on stream `use`.
 // The old allocation may still be read by work the ctx enqueued (tvl1_calc is
-// asynchronous), and hipFree would wait for every stream on the device -- every other
-// context's pair in flight.  So the old arena is retired, not freed: events recorded on the
-// ctx's streams mark its last use, and it is released once they are done (reap_retired; at
-// most kRetiredMax are held, older ones are waited for) or at tvl1_destroy.  Growth
-// therefore never drains the device.  The arenas are only ever grown: a smaller layout
-// re-lays the existing allocation (ensure_geometry, ensure_batch).  The work on `use` is
-// ordered after the zero fill by an event, not by a host wait.  (The stream-ordered
+// asynchronous).  It is retired, not freed at once: events recorded on the ctx's recent
+// streams (note_stream keeps the last 8) mark its last use, and reap_retired releases it
+// once they are done, or waits for the oldest when more than kRetiredMax are held, or at
+// tvl1_destroy.  What makes the release safe is hipFree itself: on ROCm it synchronises the
+// whole device before it frees, so a retired arena is never freed under a kernel that
+// still reads it, whatever stream that kernel is on.  The price is that a reap stalls every
+// other context's pairs in flight for that moment; it happens only when an arena was
+// outgrown (geometry growth, at most twice held), never in the steady state of a job whose
+// sizes repeat.  The arenas are only ever grown: a smaller layout re-lays the existing
+// allocation (ensure_geometry, ensure_batch), ordered across streams by order_streams.  The
+// work on `use` is ordered after the zero fill by an event, not by a host wait.  (The stream-ordered
 // allocator, hipMallocAsync / hipFreeAsync, would release in stream order too, but it
 // deadlocked against a concurrent hipStreamDestroy on this ROCm, so it is not used.)
 // Remember a stream the ctx enqueues work on, so a retired arena can be released once every
@@ -320,6 +327,22 @@ static void reap_retired(tvl1_ctx *c, bool wait) {
     else c->retired[keep++] = r;
   }
   c->retired.resize(keep);
+}
+
+// A ctx's arenas are reused (and re-laid in place) by every call, so a call on a stream
+// other than the previous call's must not start before that stream's work on them is done
+// (a batch re-laid for a new geometry on stream B while stream A's kb_output still
+// reads the old layout).  One event record + stream wait per switch of streams; a ctx that
+// stays on one stream pays nothing.  A stream the caller has destroyed since has nothing
+// left on it: its record fails and is ignored.
+static void order_streams(tvl1_ctx *c, hipStream_t st) {
+  if (c->last_stream_valid && c->last_stream != st) {
+    if (hipEventRecord(c->ev_switch, c->last_stream) == hipSuccess)
+      (void)hipStreamWaitEvent(st, c->ev_switch, 0);
+    (void)hipGetLastError();
+  }
+  c->last_stream = st;
+  c->last_stream_valid = true;
 }
 
 static tvl1_status arena_alloc(tvl1_ctx *c, char **arena, size_t *have, size_t bytes,
@@ -374,6 +397,7 @@ static tvl1_status arena_alloc(tvl1_ctx *c, char **arena, size_t *have, size_t b
 // Carve the arena for a geometry; grows (never shrinks) the device allocation.  The
 // calls's work goes to stream st.
 static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H, hipStream_t st) {
+  order_streams(c, st);
   note_stream(c, st);
   if (!c->retired.empty()) reap_retired(c, false);
   Geometry g;
@@ -2159,7 +2183,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
       hipEventCreateWithFlags(&c->ev_check[1], hipEventDisableTiming) != hipSuccess ||
       hipMalloc((void **)&c->gate, 256) != hipSuccess ||
       hipMemset(c->gate, 0, 256) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_switch, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return set_err(nullptr, TVL1_EHIP, "HIP initialisation failed on device %d", device);
   }
@@ -2361,6 +2386,7 @@ tvl1_status tvl1_find_alignment(tvl1_ctx *c, const uint8_t *frame1, size_t pitch
   }
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
+  order_streams(c, st);
   {
     const tvl1_status r = ensure_pattern(c);
     if (r != TVL1_OK) return r;
@@ -2455,6 +2481,7 @@ tvl1_status tvl1_orb_detect(tvl1_ctx *c, const uint8_t *frame, size_t pitch, int
   }
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
+  order_streams(c, st);
   {
     const tvl1_status r = ensure_pattern(c);
     if (r != TVL1_OK) return r;
@@ -2500,6 +2527,7 @@ tvl1_status tvl1_match_knn2(tvl1_ctx *c, const uint8_t *query, int32_t nq, const
   if (nq == 0) return TVL1_OK;
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
+  order_streams(c, st);
   const int nseg = std::max(1, std::min(kMatchSegs, (nt + 255) / 256));
   const int seg = (int)align_up((size_t)((std::max(nt, 1) + nseg - 1) / nseg), 64);
   // scratch: query and train descriptors, the per-segment top-2, the merged top-2
@@ -2551,6 +2579,7 @@ tvl1_status tvl1_postprocess_affine(tvl1_ctx *c, float *u, float *v, size_t fp, 
   if (W <= 0 || H <= 0) return set_err(c, TVL1_ESIZE, "bad size");
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
+  order_streams(c, st);
   const size_t need = 2 * (size_t)W * H * sizeof(float);
   if (need > c->map_bytes) {
     char *m = reinterpret_cast<char *>(c->map_scratch);
@@ -2632,6 +2661,7 @@ void tvl1_destroy(tvl1_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   if (c->gate) (void)hipFree(c->gate);
   if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+  if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
   delete c;
 }
 

@@ -161,3 +161,40 @@ def oracle_postprocess_affine(u: np.ndarray, v: np.ndarray, I1: np.ndarray, flow
                                C.c_size_t(4 * W), i1.ctypes.data_as(C.c_void_p), C.c_size_t(W), W,
                                H, int(flow_output), m.ctypes.data_as(C.c_void_p))
     return uu, vv
+
+
+# ---- stopping-rule robustness: the oracle's per-check
+# error / scaledEps trace and an alternative residual accumulation order
+def oracle_check_trace(I0: np.ndarray, I1: np.ndarray, params: TVL1Params | None = None,
+                       residual_mode: int = 0, cap: int = 1 << 16):
+    """oracle_calc with every check recorded: returns (u, v, stats, warp_iters, trace) where
+    trace is an (n, 4) array of (level, warp, n, error / scaledEps).  residual_mode 1 sums the
+    residual in float, rows reversed (orc_set_residual_mode)."""
+    lib = load_oracle()
+    buf = np.zeros((cap, 4), np.float64)
+    lib.orc_set_residual_mode(int(residual_mode))
+    lib.orc_set_check_trace(buf.ctypes.data_as(C.c_void_p), cap)
+    try:
+        u, v, st, wi = oracle_calc(I0, I1, params)
+        n = int(lib.orc_check_trace_count())
+    finally:
+        lib.orc_set_check_trace(None, 0)
+        lib.orc_set_residual_mode(0)
+    if n > cap:
+        raise RuntimeError(f"check trace overflow ({n} > {cap})")
+    return u, v, st, wi, buf[:n].copy()
+
+
+def check_margins(trace: np.ndarray, iterations: int) -> np.ndarray:
+    """Relative distance of each check's decision from the nearest threshold that could flip
+    the schedule.  After a check at iteration n with r = error / scaledEps the warp stops iff
+    r <= 1; otherwise prevError -= scaledEps per unchecked iteration, so the next check comes
+    at n + 2 iff r < 2, else at n + 4 iff r < 4, at n + 6 iff r < 6, ... (procOneScale's
+    rule).  The thresholds are therefore t in {1, 2, 4, 6, ...} (those reachable
+    before `iterations`), and a perturbation of the residual by a relative delta flips a
+    decision only if delta >= |r - t| / r for some t.  Returns that relative margin per check."""
+    out = np.empty(len(trace))
+    for i, (_, _, n, r) in enumerate(trace):
+        ts = [1.0] + [float(t) for t in range(2, max(2, iterations - int(n)) + 1, 2)]
+        out[i] = min(abs(r - t) for t in ts) / r
+    return out

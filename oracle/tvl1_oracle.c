@@ -254,6 +254,39 @@ static inline float divergence(const float *v1, const float *v2, int y, int x, i
   return v1[0] + v2[0];
 }
 
+/* Parity report only: how the residual is accumulated,
+ * and a trace of every check's error / scaledEps.  OpenCV 3.4.1's cuda::sum of the CV_32F
+ * diff buffer (procOneScale, behind /root/reference/src/optflow.cpp:518-519) reduces in an
+ * order this restatement cannot know [OCV], so the report measures how far each stopping
+ * decision sits from its threshold and reruns the schedule under a deliberately different
+ * accumulation.
+ *   mode 0 (default, the engine's): each row summed left to right in double, rows in order;
+ *   mode 1: each row summed left to right in float, the row sums added in float from the
+ *           last row to the first -- a lossy, differently ordered accumulation.
+ * Process-global, not thread-safe: test infrastructure. */
+static int g_resid_mode = 0;
+static double *g_trace = NULL;
+static int g_trace_cap = 0, g_trace_n = 0;
+
+void orc_set_residual_mode(int mode) { g_resid_mode = mode; }
+
+/* records of 4 doubles: level, warp, n, error / scaledEps; NULL turns the trace off */
+void orc_set_check_trace(double *buf, int cap_records) {
+  g_trace = buf;
+  g_trace_cap = buf ? cap_records : 0;
+  g_trace_n = 0;
+}
+
+int orc_check_trace_count(void) { return g_trace_n; }
+
+static void trace_check(int level, int warp, int n, double ratio) {
+  if (g_trace && g_trace_n < g_trace_cap) {
+    double *r = g_trace + 4 * (size_t)g_trace_n;
+    r[0] = level, r[1] = warp, r[2] = n, r[3] = ratio;
+  }
+  if (g_trace) ++g_trace_n;
+}
+
 /* [A.3] estimateU: TH thresholding + u = v + theta * div(p). */
 static double estimate_u(const float *I1wx, const float *I1wy, const float *grad,
                          const float *rho_c, const float *p11, const float *p12,
@@ -261,9 +294,12 @@ static double estimate_u(const float *I1wx, const float *I1wy, const float *grad
                          const float *p32, float *u1, float *u2, float *u3, int w, int h,
                          float l_t, float theta, float gamma, int calc_error, int fma_mode) {
   double *rows = calc_error ? (double *)calloc((size_t)h, sizeof(double)) : NULL;
+  const int fmode = calc_error && g_resid_mode == 1;
+  float *frows = fmode ? (float *)calloc((size_t)h, sizeof(float)) : NULL;
 #pragma omp parallel for schedule(static)
   for (int y = 0; y < h; ++y) {
     double rsum = 0.0;
+    float fsum = 0.0f;
     for (int x = 0; x < w; ++x) {
       const size_t i = IDX(x, y, w);
       const float I1wxv = I1wx[i];
@@ -308,15 +344,24 @@ static double estimate_u(const float *I1wx, const float *I1wy, const float *grad
       if (calc_error) {
         const float e1 = u1o - u1n, e2 = u2o - u2n;
         /* FMA: n1 + n2 -> fma(e1, e1, e2*e2) */
-        rsum += (double)(fma_mode ? fmaf(e1, e1, e2 * e2) : e1 * e1 + e2 * e2);
+        const float term = fma_mode ? fmaf(e1, e1, e2 * e2) : e1 * e1 + e2 * e2;
+        rsum += (double)term;
+        if (fmode) fsum += term;
       }
     }
     if (rows) rows[y] = rsum;
+    if (frows) frows[y] = fsum;
   }
   double total = 0.0;
   if (rows) {
     for (int y = 0; y < h; ++y) total += rows[y];
     free(rows);
+  }
+  if (frows) {
+    float ft = 0.0f;
+    for (int y = h - 1; y >= 0; --y) ft += frows[y];
+    free(frows);
+    total = (double)ft;
   }
   return total;
 }
@@ -555,6 +600,7 @@ static int calc_in(const tvl1_params *prm, const void *I0, size_t pitch0, const 
           error = e;
           prevError = error;
           ++checks;
+          trace_check(s, wp, n, error / scaledEps);
         } else {
           error = DBL_MAX;
           prevError -= scaledEps;

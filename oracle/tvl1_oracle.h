@@ -117,6 +117,11 @@ void orc_postprocess_affine(float *u, float *v, size_t flow_pitch, const uint8_t
                             size_t pitch1, int w, int h, int flow_output, const float affine[6]);
 
 /* number of OpenMP threads the oracle uses (1 when built without OpenMP) */
+/* parity report only: residual accumulation order and a per-check trace of
+ * error / scaledEps (records of 4 doubles: level, warp, n, ratio) */
+void orc_set_residual_mode(int mode);
+void orc_set_check_trace(double *buf, int cap_records);
+int orc_check_trace_count(void);
 int orc_num_threads(void);
 void orc_set_num_threads(int n);
 

@@ -120,9 +120,11 @@ def test_batch_alternating_geometries_hold_one_arena(built):
 
 
 def test_concurrent_batches_bit_identical(built):
-    """Two tvl1_calc_batch calls at once on their own contexts and streams: each sizes its
-    streaming launches for the shared share of the resident slots (fill_shared) while the
-    other runs, and every pair still equals the oracle bit for bit."""
+    """Two tvl1_calc_batch calls at once on their own contexts and streams: each counts as a
+    solve in progress on the device (single-pair solves running beside them size their
+    streaming launches for the shared share, fill_shared; the batched launches themselves
+    keep full-slot sizing, solve_batch_chunk), and every pair still equals the oracle bit for
+    bit."""
     p = capi.make_params(nscales=5, warps=4)
     dev = torch.device("cuda", 0)
     jobs = []
@@ -161,3 +163,37 @@ def test_concurrent_batches_bit_identical(built):
             np.testing.assert_array_equal(jb["st"][b]["warp_iters"], wr)
             assert bits_equal(u[b], ur) and bits_equal(v[b], vr)
         jb["eng"].close()
+
+
+def test_batch_relaid_across_streams_without_sync(built):
+    """one ctx runs tvl1_calc_batch on stream A, then, with no host sync, a smaller
+    geometry on stream B -- ensure_batch re-lays the same arena in place.  order_streams makes
+    B wait for A's last kernels (kb_output reads the old layout), so both batches equal the
+    oracle bit for bit."""
+    p = capi.make_params(nscales=4, warps=3)
+    dev = torch.device("cuda", 0)
+    eng = capi.Engine(p)
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    jobs = []
+    for (n, w, h, seed) in ((6, 300, 120, 300), (4, 200, 70, 310)):
+        I0s = np.stack([synth.gen_pair(w, h, seed=seed + b)[0] for b in range(n)])
+        I1s = np.stack([synth.gen_pair(w, h, seed=seed + b)[1] for b in range(n)])
+        jobs.append(dict(n=n, w=w, h=h, I0s=I0s, I1s=I1s, d0=torch.from_numpy(I0s).to(dev),
+                         d1=torch.from_numpy(I1s).to(dev),
+                         du=torch.zeros((n, h, w), dtype=torch.float32, device=dev),
+                         dv=torch.zeros((n, h, w), dtype=torch.float32, device=dev)))
+    torch.cuda.synchronize()
+    for jb, st in zip(jobs, (sa, sb)):
+        n, w, h = jb["n"], jb["w"], jb["h"]
+        jb["st"] = eng.calc_batch_device(n, jb["d0"].data_ptr(), w, w * h, jb["d1"].data_ptr(), w,
+                                         w * h, w, h, jb["du"].data_ptr(), jb["dv"].data_ptr(),
+                                         4 * w, 4 * w * h, stream=st.cuda_stream, warp_iters=True)
+    sb.synchronize()
+    sa.synchronize()
+    for jb in jobs:
+        u, v = jb["du"].cpu().numpy(), jb["dv"].cpu().numpy()
+        for b in range(jb["n"]):
+            ur, vr, _, wr = checker.oracle_calc(jb["I0s"][b], jb["I1s"][b], p)
+            np.testing.assert_array_equal(jb["st"][b]["warp_iters"], wr)
+            assert bits_equal(u[b], ur) and bits_equal(v[b], vr), (jb["w"], b)
+    eng.close()
