@@ -2,6 +2,9 @@
 #include "imageio.hpp"
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <cfloat>
@@ -700,16 +703,16 @@ bool read_gray8(const std::string &path, Image8 &img, std::string &err) {
 static inline int cv_round(double v) { return (int)std::lrint(v); }
 static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
 
-void resize_u8(const Image8 &src, double fx, double fy, Image8 &dst) {
-  const int sw = src.width, sh = src.height;
+// cv::resize on the CPU, output rows [dy0, dy1) only: `row(sy)` gives source row sy and is
+// asked only for the rows resize_src_rows() names.  Every output row depends on its own
+// source rows alone, so a band computed here is byte-identical to the same rows of the whole
+// resized image (read_gray8_bands relies on it).
+template <class RowF>
+static void resize_rows(RowF row, int sw, int sh, double fx, double fy, int dy0, int dy1,
+                        uint8_t *dst) {
   const int dw = cv_round(sw * fx), dh = cv_round(sh * fy);
-  Image8 out;
-  out.width = dw;
-  out.height = dh;
-  out.data.assign((size_t)dw * dh, 0);
   if (dw == sw && dh == sh) {
-    out.data = src.data;
-    dst = std::move(out);
+    for (int dy = dy0; dy < dy1; ++dy) memcpy(dst + (size_t)(dy - dy0) * dw, row(dy), dw);
     return;
   }
   const double scale_x = 1. / fx, scale_y = 1. / fy;
@@ -721,14 +724,17 @@ void resize_u8(const Image8 &src, double fx, double fy, Image8 &dst) {
     // of OpenCV's 8u kernel rounds (s + 2) >> 2, its scalar tail cvRound(s * 0.25f);
     // partial 2x2 cells at odd borders average the samples that exist.
     const int dwidth1 = sw / 2;
-    for (int dy = 0; dy < dh; ++dy) {
-      uint8_t *D = out.row(dy);
+    for (int dy = dy0; dy < dy1; ++dy) {
+      uint8_t *D = dst + (size_t)(dy - dy0) * dw;
       const int sy0 = dy * 2;
-      if (sy0 >= sh) continue;
+      if (sy0 >= sh) {
+        memset(D, 0, dw);
+        continue;
+      }
       const int w = sy0 + 2 <= sh ? dwidth1 : 0;
       int dx = 0;
-      const uint8_t *S0 = src.row(sy0);
-      const uint8_t *S1 = sy0 + 1 < sh ? src.row(sy0 + 1) : S0;
+      const uint8_t *S0 = row(sy0);
+      const uint8_t *S1 = sy0 + 1 < sh ? row(sy0 + 1) : S0;
       for (; dx + 8 <= w; dx += 8)
         for (int k = dx; k < dx + 8; ++k)
           D[k] = (uint8_t)((S0[2 * k] + S0[2 * k + 1] + S1[2 * k] + S1[2 * k + 1] + 2) >> 2);
@@ -741,19 +747,18 @@ void resize_u8(const Image8 &src, double fx, double fy, Image8 &dst) {
         const int sx0 = dx * 2;
         for (int sy = 0; sy < 2 && sy0 + sy < sh; ++sy)
           for (int sx = 0; sx < 2 && sx0 + sx < sw; ++sx) {
-            sum += src.row(sy0 + sy)[sx0 + sx];
+            sum += row(sy0 + sy)[sx0 + sx];
             ++count;
           }
         D[dx] = count ? sat_u8(cv_round((float)sum / count)) : 0;
       }
     }
-    dst = std::move(out);
     return;
   }
   // Generic INTER_LINEAR (resizeGeneric_ with 11-bit fixed-point coefficients).
   constexpr int BITS = 11, SCALE = 1 << BITS;
-  std::vector<int> xofs(dw), yofs(dh);
-  std::vector<short> ax(2 * dw), ay(2 * dh);
+  std::vector<int> xofs(dw);
+  std::vector<short> ax(2 * dw);
   for (int dx = 0; dx < dw; ++dx) {
     float f = (float)((dx + 0.5) * scale_x - 0.5);
     int sx = (int)std::floor(f);
@@ -768,7 +773,14 @@ void resize_u8(const Image8 &src, double fx, double fy, Image8 &dst) {
     ax[2 * dx] = (short)cv_round((1.f - f) * SCALE);
     ax[2 * dx + 1] = (short)(SCALE - ax[2 * dx]);
   }
-  for (int dy = 0; dy < dh; ++dy) {
+  std::vector<int> h0(dw), h1(dw);
+  auto hres = [&](const uint8_t *S, std::vector<int> &D) {
+    for (int dx = 0; dx < dw; ++dx) {
+      const int sx = xofs[dx];
+      D[dx] = sx + 1 < sw ? S[sx] * ax[2 * dx] + S[sx + 1] * ax[2 * dx + 1] : S[sx] * SCALE;
+    }
+  };
+  for (int dy = dy0; dy < dy1; ++dy) {
     float f = (float)((dy + 0.5) * scale_y - 0.5);
     int sy = (int)std::floor(f);
     f -= sy;
@@ -778,26 +790,286 @@ void resize_u8(const Image8 &src, double fx, double fy, Image8 &dst) {
     if (sy >= sh - 1) {
       f = 0, sy = sh - 1;
     }
-    yofs[dy] = sy;
-    ay[2 * dy] = (short)cv_round((1.f - f) * SCALE);
-    ay[2 * dy + 1] = (short)(SCALE - ay[2 * dy]);
-  }
-  std::vector<int> h0(dw), h1(dw);
-  auto hres = [&](const uint8_t *S, std::vector<int> &D) {
-    for (int dx = 0; dx < dw; ++dx) {
-      const int sx = xofs[dx];
-      D[dx] = sx + 1 < sw ? S[sx] * ax[2 * dx] + S[sx + 1] * ax[2 * dx + 1] : S[sx] * SCALE;
-    }
-  };
-  for (int dy = 0; dy < dh; ++dy) {
-    const int sy = yofs[dy];
-    hres(src.row(sy), h0);
-    hres(src.row(std::min(sy + 1, sh - 1)), h1);
-    uint8_t *D = out.row(dy);
+    const short ay0 = (short)cv_round((1.f - f) * SCALE), ay1 = (short)(SCALE - ay0);
+    hres(row(sy), h0);
+    hres(row(std::min(sy + 1, sh - 1)), h1);
+    uint8_t *D = dst + (size_t)(dy - dy0) * dw;
     for (int dx = 0; dx < dw; ++dx)
-      D[dx] = sat_u8((ay[2 * dy] * h0[dx] + ay[2 * dy + 1] * h1[dx] + (1 << (2 * BITS - 1))) >> (2 * BITS));
+      D[dx] = sat_u8((ay0 * h0[dx] + ay1 * h1[dx] + (1 << (2 * BITS - 1))) >> (2 * BITS));
   }
+}
+
+void resized_size(int sw, int sh, double fx, double fy, int &dw, int &dh) {
+  dw = cv_round(sw * fx);
+  dh = cv_round(sh * fy);
+}
+
+// The source rows [sy0, sy1) that output rows [dy0, dy1) of resize_rows read.
+void resize_src_rows(int sw, int sh, double fx, double fy, int dy0, int dy1, int &sy0, int &sy1) {
+  const int dw = cv_round(sw * fx), dh = cv_round(sh * fy);
+  sy0 = sh;
+  sy1 = 0;
+  if (dy1 <= dy0) {
+    sy0 = sy1 = 0;
+    return;
+  }
+  if (dw == sw && dh == sh) {
+    sy0 = dy0, sy1 = dy1;
+    return;
+  }
+  const double scale_x = 1. / fx, scale_y = 1. / fy;
+  const int iscale_x = cv_round(scale_x), iscale_y = cv_round(scale_y);
+  if (std::abs(scale_x - iscale_x) < DBL_EPSILON && std::abs(scale_y - iscale_y) < DBL_EPSILON &&
+      iscale_x == 2 && iscale_y == 2) {
+    sy0 = std::min(2 * dy0, sh);
+    sy1 = std::min(2 * dy1, sh);
+    if (sy1 <= sy0) sy0 = sy1 = 0;
+    return;
+  }
+  for (int dy : {dy0, dy1 - 1}) {   // sy is monotonic in dy
+    float f = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = (int)std::floor(f);
+    sy = std::max(0, std::min(sy, sh - 1));
+    sy0 = std::min(sy0, sy);
+    sy1 = std::max(sy1, std::min(sy + 1, sh - 1) + 1);
+  }
+}
+
+void resize_u8(const Image8 &src, double fx, double fy, Image8 &dst) {
+  Image8 out;
+  resized_size(src.width, src.height, fx, fy, out.width, out.height);
+  out.data.resize((size_t)out.width * out.height);
+  resize_rows([&](int sy) { return src.row(sy); }, src.width, src.height, fx, fy, 0, out.height,
+              out.data.data());
   dst = std::move(out);
+}
+
+// ------------------------------------------------------------------ row bands
+// Strip-organised 8-bit gray TIFF read for only some rows: the header, the IFD and the strip
+// tables by pread, then, for uncompressed strips, just the bytes of the rows asked for, and
+// for compressed strips just the strips that hold them.  Returns 0 on success, 1 if the file
+// is not such a TIFF (the caller decodes it whole), -1 on a read / format error.
+namespace {
+struct PFile {
+  int fd = -1;
+  uint64_t size = 0;
+  ~PFile() {
+    if (fd >= 0) close(fd);
+  }
+  bool read(uint64_t off, size_t n, void *dst) const {
+    if (off > size || n > size - off) return false;
+    uint8_t *d = (uint8_t *)dst;
+    while (n) {
+      const ssize_t r = pread(fd, d, n, (off_t)off);
+      if (r <= 0) return false;
+      d += r, off += (uint64_t)r, n -= (size_t)r;
+    }
+    return true;
+  }
+};
+}  // namespace
+
+static int tiff_rows(const std::string &path, int &W, int &H,
+                     const std::vector<std::pair<int, int>> &ranges,   // source rows [a, b)
+                     std::vector<std::vector<uint8_t>> &rows, std::string &err) {
+  PFile f;
+  f.fd = open(path.c_str(), O_RDONLY);
+  if (f.fd < 0) {
+    err = "cannot open " + path;
+    return -1;
+  }
+  struct stat st;
+  if (fstat(f.fd, &st) != 0) return 1;
+  f.size = (uint64_t)st.st_size;
+  uint8_t hdr[8];
+  if (!f.read(0, 8, hdr)) return 1;
+  const bool le = hdr[0] == 'I';
+  if (memcmp(hdr, "II*\0", 4) && memcmp(hdr, "MM\0*", 4)) return 1;
+  auto u16 = [&](const uint8_t *q) { return le ? (uint32_t)(q[0] | q[1] << 8) : (uint32_t)(q[0] << 8 | q[1]); };
+  auto u32 = [&](const uint8_t *q) {
+    return le ? (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24
+              : (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3];
+  };
+  const uint32_t ifd = u32(hdr + 4);
+  uint8_t c2[2];
+  if (!f.read(ifd, 2, c2)) return 1;
+  const uint32_t nent = u16(c2);
+  std::vector<uint8_t> ents((size_t)nent * 12);
+  if (!f.read((uint64_t)ifd + 2, ents.size(), ents.data())) return 1;
+  uint32_t w = 0, h = 0, bps = 8, comp = 1, photo = 1, spp = 1, rps = 0, planar = 1, pred = 1,
+           fmt = 1;
+  std::vector<uint32_t> offs, cnts;
+  auto values = [&](const uint8_t *e, std::vector<uint32_t> &v) {
+    const uint32_t type = u16(e + 2), cnt = u32(e + 4);
+    const size_t sz = type == 3 ? 2 : 4;
+    if ((uint64_t)cnt * sz > f.size) return false;
+    std::vector<uint8_t> raw((size_t)cnt * sz);
+    if (raw.size() <= 4) memcpy(raw.data(), e + 8, raw.size());
+    else if (!f.read(u32(e + 8), raw.size(), raw.data())) return false;
+    v.resize(cnt);
+    for (uint32_t i = 0; i < cnt; ++i) v[i] = sz == 2 ? u16(&raw[i * 2]) : u32(&raw[i * 4]);
+    return true;
+  };
+  for (uint32_t i = 0; i < nent; ++i) {
+    const uint8_t *e = &ents[(size_t)i * 12];
+    std::vector<uint32_t> v;
+    if (!values(e, v)) return 1;
+    const uint32_t v0 = v.empty() ? 0 : v[0];
+    switch (u16(e)) {
+      case 256: w = v0; break;
+      case 257: h = v0; break;
+      case 258: bps = v0; break;
+      case 259: comp = v0; break;
+      case 262: photo = v0; break;
+      case 273: offs = v; break;
+      case 277: spp = v0; break;
+      case 278: rps = v0; break;
+      case 279: cnts = v; break;
+      case 284: planar = v0; break;
+      case 317: pred = v0; break;
+      case 339: fmt = v0; break;
+      default: break;
+    }
+  }
+  // only the layout this reader covers: 8-bit gray strips, uncompressed / LZW / deflate
+  if (!w || !h || bps != 8 || spp != 1 || planar != 1 || fmt == 3 || offs.empty() ||
+      offs.size() != cnts.size() || (photo != 0 && photo != 1) ||
+      (comp != 1 && comp != 5 && comp != 8 && comp != 32946) || (uint64_t)w * h > kMaxPixels)
+    return 1;
+  if (!rps || rps > h) rps = h;
+  if ((uint64_t)offs.size() * rps < h) return 1;   // whole decode reports the missing rows
+  W = (int)w, H = (int)h;
+  rows.assign(h, {});
+  std::vector<uint8_t> strip;
+  long have_strip = -1;
+  for (const auto &rg : ranges) {
+    for (int y = rg.first; y < rg.second; ++y) {
+      if (y < 0 || y >= (int)h || !rows[y].empty()) continue;
+      const uint32_t s = (uint32_t)y / rps, r = (uint32_t)y % rps;
+      const uint32_t srows = std::min<uint32_t>(rps, h - s * rps);
+      std::vector<uint8_t> &o = rows[y];
+      o.resize(w);
+      if (comp == 1) {
+        // uncompressed: the row's bytes where they lie (a short strip reads as zeros, as the
+        // whole decode's padding does)
+        const uint64_t at = (uint64_t)r * w;
+        const uint64_t n = cnts[s] > at ? std::min<uint64_t>(w, cnts[s] - at) : 0;
+        memset(o.data(), 0, w);
+        if (n && !f.read((uint64_t)offs[s] + at, (size_t)n, o.data())) {
+          err = "TIFF: strip out of range";
+          return -1;
+        }
+      } else {
+        if (have_strip != (long)s) {
+          std::vector<uint8_t> src(cnts[s]);
+          if (!f.read(offs[s], src.size(), src.data())) {
+            err = "TIFF: strip out of range";
+            return -1;
+          }
+          const size_t expect = (size_t)srows * w;
+          strip.clear();
+          if (comp == 5) {
+            if (!lzw_decode(src.data(), src.size(), strip, expect)) {
+              err = "TIFF: corrupt LZW strip";
+              return -1;
+            }
+          } else {
+            strip.resize(expect);
+            uLongf dl = (uLongf)expect;
+            if (uncompress(strip.data(), &dl, src.data(), src.size()) != Z_OK) {
+              err = "TIFF: corrupt deflate strip";
+              return -1;
+            }
+          }
+          strip.resize(expect, 0);
+          if (pred == 2)
+            for (uint32_t k = 0; k < srows; ++k) {
+              uint8_t *q = strip.data() + (size_t)k * w;
+              for (uint32_t i = 1; i < w; ++i) q[i] = (uint8_t)(q[i] + q[i - 1]);
+            }
+          have_strip = (long)s;
+        }
+        memcpy(o.data(), strip.data() + (size_t)r * w, w);
+      }
+      if (photo == 0)
+        for (auto &b : o) b = (uint8_t)(255 - b);
+    }
+  }
+  return 0;
+}
+
+bool read_gray8_bands(const std::string &path, double scale,
+                      const std::function<std::vector<std::pair<int, int>>(int, int)> &bands_of,
+                      int &W, int &H, std::vector<Image8> &out, std::string &err, bool *partial) {
+  out.clear();
+  if (partial) *partial = false;
+  try {
+    // the source rows each band needs, for a source of sw x sh
+    auto plan = [&](int sw, int sh, std::vector<std::pair<int, int>> &bands,
+                    std::vector<std::pair<int, int>> &src) {
+      resized_size(sw, sh, scale, scale, W, H);
+      bands = bands_of(W, H);
+      src.clear();
+      for (auto &b : bands) {
+        if (b.first < 0 || b.second > H || b.first >= b.second) {
+          err = "row band [" + std::to_string(b.first) + ", " + std::to_string(b.second) +
+                ") outside the " + std::to_string(W) + "x" + std::to_string(H) + " image";
+          return false;
+        }
+        int a = 0, z = 0;
+        resize_src_rows(sw, sh, scale, scale, b.first, b.second, a, z);
+        src.emplace_back(a, z);
+      }
+      return true;
+    };
+    std::vector<std::pair<int, int>> bands, src;
+    {
+      // strip-organised TIFF: only the needed rows leave the file
+      int sw = 0, sh = 0;
+      std::vector<std::vector<uint8_t>> rows;
+      // the header first (sizes), then the rows: tiff_rows is called twice only for the
+      // sizes' sake when bands depend on them; one call with every row range would read
+      // the strips twice, so the plan is made from the header pass
+      std::string e2;
+      const int r = tiff_rows(path, sw, sh, {}, rows, e2);
+      if (r < 0) {
+        err = e2;
+        return false;
+      }
+      if (r == 0) {
+        if (!plan(sw, sh, bands, src)) return false;
+        if (tiff_rows(path, sw, sh, src, rows, err) != 0) return false;
+        for (size_t i = 0; i < bands.size(); ++i) {
+          Image8 im;
+          im.width = W;
+          im.height = bands[i].second - bands[i].first;
+          im.data.resize((size_t)im.width * im.height);
+          resize_rows([&](int sy) { return (const uint8_t *)rows[sy].data(); }, sw, sh, scale, scale,
+                      bands[i].first, bands[i].second, im.data.data());
+          out.push_back(std::move(im));
+        }
+        if (partial) *partial = true;
+        return true;
+      }
+    }
+    Image8 full;   // any other file: whole decode, then only the bands' rows are resized
+    if (!decode_any(path, full, err)) return false;
+    if (!plan(full.width, full.height, bands, src)) return false;
+    for (auto &b : bands) {
+      Image8 im;
+      im.width = W;
+      im.height = b.second - b.first;
+      im.data.resize((size_t)im.width * im.height);
+      resize_rows([&](int sy) { return full.row(sy); }, full.width, full.height, scale, scale,
+                  b.first, b.second, im.data.data());
+      out.push_back(std::move(im));
+    }
+    return true;
+  } catch (const std::exception &e) {
+    out.clear();
+    err = "cannot decode " + path + ": " + e.what();
+    return false;
+  }
 }
 
 // ------------------------------------------------------------------ TIFF write

@@ -14,6 +14,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <new>
 #include <string>
 #include <utility>
@@ -84,6 +85,22 @@ bool read_gray8(const std::string &path, Image8 &img, std::string &err);
 // INTER_AREA fast path (2x2 mean), other scales half-pixel-centre bilinear with
 // 11-bit fixed-point weights.
 void resize_u8(const Image8 &src, double fx, double fy, Image8 &dst);
+
+// Size of cv::resize's output (round half-even of src * f).
+void resized_size(int sw, int sh, double fx, double fy, int &dw, int &dh);
+// The source rows [sy0, sy1) that output rows [dy0, dy1) of resize_u8 read.
+void resize_src_rows(int sw, int sh, double fx, double fy, int dy0, int dy1, int &sy0, int &sy1);
+
+// Row bands of read_gray8 + resize_u8(scale) without decoding what they do not need (the
+// production strip jobs solve two ~100-row ROIs of each slice).  bands_of gets
+// the pre-scaled image size (W, H) and returns the bands [y0, y1) wanted; out[i] holds band
+// i, byte-identical to those rows of the whole decoded and resized image.  Strip-organised
+// 8-bit gray TIFF (uncompressed: only the rows' bytes; LZW / deflate: only their strips) is
+// read by pread; any other file is decoded whole first.  *partial says which happened.
+bool read_gray8_bands(const std::string &path, double scale,
+                      const std::function<std::vector<std::pair<int, int>>(int, int)> &bands_of,
+                      int &W, int &H, std::vector<Image8> &out, std::string &err,
+                      bool *partial = nullptr);
 
 // Single-channel float32 TIFF (uncompressed, SampleFormat=IEEE float).
 bool write_tiff_f32(const std::string &path, const float *data, int width, int height,

@@ -1219,6 +1219,41 @@ int main(int argc, const char *argv[]) {
       plan = true;
       continue;
     }
+    if (a == "--decode-bands") {   // tests: the ROI-limited read of strip jobs
+      // optflow --decode-bands <image> <out.tiff> <scale> <top> <bottom>: the top and bottom
+      // row bands of the pre-scaled slice (get_rois' top / bottom), stacked, as an 8-bit TIFF;
+      // stdout says whether only their rows were read
+      if (i + 5 >= argc) {
+        usage();
+        return 2;
+      }
+      const float sc = (float)atof(argv[i + 3]);
+      const int top = atoi(argv[i + 4]), bottom = atoi(argv[i + 5]);
+      int W = 0, H = 0;
+      bool partial = false;
+      std::vector<ofio::Image8> bands;
+      std::string err;
+      if (!ofio::read_gray8_bands(argv[i + 1], sc,
+                                  [&](int, int h) {
+                                    return std::vector<std::pair<int, int>>{{0, top}, {h - bottom, h}};
+                                  },
+                                  W, H, bands, err, &partial)) {
+        fprintf(stderr, "%s\n", err.c_str());
+        return 1;
+      }
+      ofio::Image8 out;
+      out.width = W;
+      out.height = bands[0].height + bands[1].height;
+      out.data.resize((size_t)W * out.height);
+      memcpy(out.data.data(), bands[0].data.data(), bands[0].data.size());
+      memcpy(out.data.data() + bands[0].data.size(), bands[1].data.data(), bands[1].data.size());
+      if (!ofio::write_tiff_u8(argv[i + 2], out, err)) {
+        fprintf(stderr, "%s\n", err.c_str());
+        return 1;
+      }
+      printf("%dx%d %s\n", W, H, partial ? "partial" : "whole");
+      return 0;
+    }
     if (a == "--decode") {
       if (i + 2 >= argc) {
         usage();

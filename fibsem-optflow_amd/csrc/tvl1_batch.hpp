@@ -78,7 +78,7 @@ struct BatchRing {
 };
 template <int M, int NW, int FM>
 __global__ __launch_bounds__(64 * NW) void kb_warp_ring(BatchRing br) {
-  __shared__ float ring[3 * warp_ring_rows<M, NW>() * (64 + 2 * M)];
+  __shared__ float ring[warp_ring_rows<M, NW>() * ring_pitch(64 + 2 * ring_mx<M>())];
   const int b = br.sel.idx[blockIdx.y];
   WarpRingArgs a = br.wa;
   const int us = bsel_bit(br.sel.ubit, b);
@@ -111,7 +111,7 @@ struct BatchWI {
 };
 template <int M, int FM, int NC = 2>
 __global__ __launch_bounds__(64 * NC + 128) void kb_warp_iter(BatchWI bw) {
-  __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, 128>()];
+  __shared__ float ring[wi_rows<M>() * ring_pitch(wi_ww<M, 128>())];
   __shared__ float cring[2 * 5 * 128];
   __shared__ float hring[NC == 2 ? 2 * kWiH * 128 : 1];
   const int b = bw.sel.idx[blockIdx.y];

@@ -132,6 +132,8 @@ struct tvl1_ctx {
   size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
   double *bpartials = nullptr;
   int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
+  char *gather_scratch = nullptr;       // tvl1_gather_flow's offsets and values
+  size_t gather_bytes = 0;
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
   size_t map_bytes = 0;
   char *align_scratch = nullptr;        // tvl1_find_alignment's pyramid, keys, descriptors
@@ -990,7 +992,8 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
             const int ys = sg * seg, ye = std::min(ys + seg, lh);
             rows += std::min(ye - 1 + 2, lh - 1) - std::max(ys - 2, 0) + 1;
           }
-          hbm = (double)w.ra.bands * BW * rows * 4.0 * ((p_zero ? 3 : 7) + (double)(BW + 2 * M) / BW) +
+          hbm = (double)w.ra.bands * BW * rows * 4.0 *
+                    ((p_zero ? 3 : 7) + (double)wi_ww<M, BW>() / BW) +
                 Nl * 4.0 * (6.0 + (w.store_c ? 3.0 : 0.0));
           alg_extra = Nl * 40.0;   // 40 B/px per warp
         } else if (exact_div) {   // taut < 0 or not finite: one iteration per launch, IEEE
@@ -1621,7 +1624,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           for (int b = 0; b < n; ++b) nz += pzero.test(b) ? 1 : 0;
           const double band_bytes = (double)wi.w.ra.bands * 128 * rows * 4.0;
           const double hbm = band_bytes * ((double)nz * 3 + (double)(n - nz) * 7 +
-                                           (double)n * (128 + 2 * 6) / 128) +
+                                           (double)n * wi_ww<6, 128>() / 128) +
                              (double)n * Nl * 4.0 * 9.0;
           prof_end(c, st, tkw, 0, (double)n * Nl * (64.0 * 2 + 40.0), hbm);
         }
@@ -2622,6 +2625,58 @@ tvl1_status tvl1_calc_host(tvl1_ctx *c, const uint8_t *I0, size_t pitch0, const 
   return TVL1_OK;
 }
 
+tvl1_status tvl1_postprocess_batch(tvl1_ctx *c, int32_t n, float *u, float *v, size_t fpitch,
+                                   size_t fstride, const uint8_t *I1, size_t pitch1,
+                                   size_t stride1, int32_t W, int32_t H, int32_t mode,
+                                   void *stream) {
+  if (n < 0) return set_err(c, TVL1_EINVAL, "n must be >= 0");
+  if (n == 0) return c ? TVL1_OK : set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  tvl1_status s = check_call(c, I1, pitch1, I1, pitch1, W, H, u, v, fpitch);
+  if (s != TVL1_OK) return s;
+  if (mode < 0 || mode > 2)
+    return set_err(c, TVL1_EINVAL, "mode must be 0 (flow), 1 (map) or 2 (map - grid)");
+  if (n > 1 && (fstride < fpitch * (size_t)H || fstride % 4 || stride1 < pitch1 * (size_t)(H - 1) + W))
+    return set_err(c, TVL1_EINVAL, "pair strides overlap the pairs");
+  if (n > 65535) return set_err(c, TVL1_EINVAL, "at most 65535 pairs per call");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(k_postprocess_batch, grid2(W, H, n), kBlk2, 0, (hipStream_t)stream, u, v,
+                     fpitch, fstride, I1, pitch1, stride1, W, H, mode);
+  HIP_TRY(c, hipGetLastError());
+  return TVL1_OK;
+}
+
+tvl1_status tvl1_gather_flow(tvl1_ctx *c, const float *u, const float *v, const int64_t *offsets,
+                             int32_t n, float *out_u, float *out_v, void *stream) {
+  if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
+  if (n < 0 || (n > 0 && (!u || !v || !offsets || !out_u || !out_v)))
+    return set_err(c, TVL1_EINVAL, "bad argument");
+  if (n == 0) return TVL1_OK;
+  for (int32_t i = 0; i < n; ++i)
+    if (offsets[i] < 0) return set_err(c, TVL1_EINVAL, "negative offset at %d", i);
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  order_streams(c, st);
+  const size_t need = align_up((size_t)n * sizeof(int64_t), 256) + (size_t)n * sizeof(float2);
+  if (need > c->gather_bytes) {
+    const tvl1_status r = arena_alloc(c, &c->gather_scratch, &c->gather_bytes,
+                                      std::max<size_t>(need, 64 << 10), st);
+    if (r != TVL1_OK) return r;
+  }
+  int64_t *doff = reinterpret_cast<int64_t *>(c->gather_scratch);
+  float2 *dout = reinterpret_cast<float2 *>(c->gather_scratch + align_up((size_t)n * sizeof(int64_t), 256));
+  std::vector<float2> host((size_t)n);
+  HIP_TRY(c, hipMemcpyAsync(doff, offsets, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_gather_flow, dim3((n + 255) / 256), dim3(256), 0, st, u, v, doff, n, dout);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipMemcpyAsync(host.data(), dout, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  for (int32_t i = 0; i < n; ++i) {
+    out_u[i] = host[i].x;
+    out_v[i] = host[i].y;
+  }
+  return TVL1_OK;
+}
+
 tvl1_status tvl1_postprocess(tvl1_ctx *c, float *u, float *v, size_t fpitch, const uint8_t *I1,
                              size_t pitch1, int32_t W, int32_t H, int32_t mode, void *stream) {
   tvl1_status s = check_call(c, I1, pitch1, I1, pitch1, W, H, u, v, fpitch);
@@ -2653,6 +2708,7 @@ void tvl1_destroy(tvl1_ctx *c) {
   if (c->barena) (void)hipFree(c->barena);
   if (c->align_scratch) (void)hipFree(c->align_scratch);
   if (c->map_scratch) (void)hipFree(c->map_scratch);
+  if (c->gather_scratch) (void)hipFree(c->gather_scratch);
   for (auto &r : c->retired) free_retired(r);
   if (c->align_pat) (void)hipFree(c->align_pat);
   if (c->pinned) (void)hipHostFree(c->pinned);

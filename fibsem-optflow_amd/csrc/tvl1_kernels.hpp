@@ -498,6 +498,22 @@ constexpr int kWarpAhead = 2;
 template <int M, int NW>
 constexpr int warp_ring_rows() { return 2 * NW + 2 * M <= 16 ? 16 : 32; }
 
+// Column margin and row pitch of the window rings (r4).  The gathers'
+// taps are ds_read_b32 / ds_read2_b32, banked (dword address mod 32) per 32-lane half.  A
+// half's lanes read consecutive window columns, but where the flow's y-component crosses an
+// integer inside the half its lanes read two ring rows: with the r3 row pitch 3WW = 420
+// (k_warp_iter) / 228 (k_warp_ring) dwords = 4 (mod 32), 4 lanes of one row landed on the
+// banks of 4 lanes of the other, a 2-way conflict on every tap read of that half (measured:
+// SQ_LDS_BANK_CONFLICT 16 % of SQ_LDS_IDX_ACTIVE in k_warp_iter; a model of C2's level 0
+// gives 26 % extra cycles on the gather).  A pitch = 0 (mod 32) maps a half's 32 consecutive
+// columns to 32 distinct banks whichever rows they read.  Rows keep the margin M (the ring
+// holds rows r-M .. r+M); columns take M - 1 (flow |u1| < 4 px inside the window instead of
+// 5; beyond it the same global-memory path as ever), which makes 3WW fit a multiple of 32
+// in less LDS than before: k_warp_iter 3 * 138 = 414 -> 416, k_warp_ring 3 * 74 = 222 -> 224.
+template <int M>
+constexpr int ring_mx() { return M == 6 ? 5 : M; }
+constexpr int ring_pitch(int ww) { return (3 * ww + 31) & ~31; }
+
 // warpBackward's rho_c = I1w - I1wx*u1 - I1wy*u2 - I0 (contracted: the two products
 // fused into the running difference, fma(-I1wy, u2, fma(-I1wx, u1, I1w)) - I0).
 template <int FM>
@@ -598,17 +614,18 @@ __device__ __forceinline__ void warp_flow_load(WarpRowI &v, const WarpRingArgs &
   bload<1>(t, a.I0, nb, xcb, so); v.i0 = t[0];
 }
 
-// Ring layout: [ring row][plane (I1, I1x, I1y)][WW]: one tap row's 12 values are within
-// 3 * WW < 256 dwords of one base, so they load with ds_read2_b32 immediate offsets.
+// Ring layout: [ring row][plane (I1, I1x, I1y)][WW], rows ring_pitch(WW) apart: one tap
+// row's 12 values are within 3 * WW < 256 dwords of one base, so they load with
+// ds_read2_b32 immediate offsets.
 template <int M, int NW>
 __device__ __forceinline__ void warp_ring_put(float *__restrict__ ring, const WarpRowI &v, int r,
                                               int lane) {
-  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>();
-  float *dst = ring + (r & (R - 1)) * (3 * WW);
+  constexpr int MX = ring_mx<M>(), WW = 64 + 2 * MX, R = warp_ring_rows<M, NW>();
+  float *dst = ring + (r & (R - 1)) * ring_pitch(WW);
   dst[lane] = v.c0;
   dst[WW + lane] = 0.5f * (v.r0 - v.l0);
   dst[2 * WW + lane] = 0.5f * (v.s0 - v.n0);
-  if (lane < 2 * M) {
+  if (lane < 2 * MX) {
     dst[64 + lane] = v.c1;
     dst[WW + 64 + lane] = 0.5f * (v.r1 - v.l1);
     dst[2 * WW + 64 + lane] = 0.5f * (v.s1 - v.n1);
@@ -621,7 +638,8 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
                                                int ye, int w, int lane, int x0,
                                                const unsigned (&xs)[2][3], unsigned xcb,
                                                unsigned nb, unsigned rowb) {
-  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>();
+  constexpr int MX = ring_mx<M>(), WW = 64 + 2 * MX, R = warp_ring_rows<M, NW>();
+  constexpr int PITCH = ring_pitch(WW);
   // loads for step + A: window row y0 + NW*A + M + w, flow row y0 + NW*A + w
   warp_ring_load(ahead, a, nb, rowb, y0 + NW * kWarpAhead + M + w, xs);
   warp_flow_load(ahead, a, nb, rowb, y0 + NW * kWarpAhead + w, xcb);
@@ -635,11 +653,11 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
   const int fx = tap_floor(wx);
   const int fy = tap_floor(wy);
   float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
-  const bool inwin = fx - 1 >= x0 - M && fx + 2 < x0 + 64 + M && fy - 1 >= y - M && fy + 2 <= y + M;
+  const bool inwin = fx - 1 >= x0 - MX && fx + 2 < x0 + 64 + MX && fy - 1 >= y - M && fy + 2 <= y + M;
   if (inwin) {
     warp_gather_fn<FM>(
         [&](int cy, int cx) {
-          const float *p = ring + (cy & (R - 1)) * (3 * WW) + (cx - (x0 - M));
+          const float *p = ring + (cy & (R - 1)) * PITCH + (cx - (x0 - MX));
           return Tap3{p[0], p[WW], p[2 * WW]};
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
@@ -667,11 +685,11 @@ __device__ __forceinline__ void warp_ring_step(float *__restrict__ ring, const W
 
 template <int M, int NW, int FM>
 __device__ __forceinline__ void warp_ring_body(const WarpRingArgs &a, int wid, float *__restrict__ ring) {
-  constexpr int WW = 64 + 2 * M, R = warp_ring_rows<M, NW>(), PL = R * WW;
+  constexpr int MX = ring_mx<M>(), WW = 64 + 2 * MX, R = warp_ring_rows<M, NW>();
   static_assert(3 * WW < 256, "one tap row within ds_read2_b32 offsets");
   static_assert(2 * NW + 2 * M <= R, "ring too small for the margin");
-  static_assert(2 * M <= 64, "second window slot per lane");
-  (void)PL;
+  static_assert(2 * MX <= 64, "second window slot per lane");
+  static_assert(ring_pitch(WW) % 32 == 0, "row pitch: no bank conflicts between ring rows");
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int band = wid % a.bands, seg = wid / a.bands;
@@ -680,8 +698,8 @@ __device__ __forceinline__ void warp_ring_body(const WarpRingArgs &a, int wid, f
   unsigned xs[2][3];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const int slot = k == 0 || lane < 2 * M ? lane + 64 * k : lane;
-    const int cc = imin(imax(x0 - M + slot, 0), a.W - 1);
+    const int slot = k == 0 || lane < 2 * MX ? lane + 64 * k : lane;
+    const int cc = imin(imax(x0 - MX + slot, 0), a.W - 1);
     xs[k][0] = 4u * cc;
     xs[k][1] = 4u * imax(cc - 1, 0);
     xs[k][2] = 4u * imin(cc + 1, a.W - 1);
@@ -720,7 +738,7 @@ __device__ __forceinline__ void warp_ring_body(const WarpRingArgs &a, int wid, f
 
 template <int M, int NW, int FM = 0>
 __global__ __launch_bounds__(64 * NW) void k_warp_ring(WarpRingArgs a) {
-  __shared__ float ring[3 * warp_ring_rows<M, NW>() * (64 + 2 * M)];
+  __shared__ float ring[warp_ring_rows<M, NW>() * ring_pitch(64 + 2 * ring_mx<M>())];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= a.waves) return;   // whole blocks
   warp_ring_body<M, NW, FM>(a, wid, ring);
@@ -2074,19 +2092,19 @@ __device__ __forceinline__ int wi_slot(int r) {
 // band width BW (px): 128 = 64 consumer lanes x 2 px + 2 producers (default), or 64 =
 // 64 lanes x 1 px + 1 producer (consumer and producer steps of similar length)
 template <int M, int BW>
-constexpr int wi_ww() { return BW + 2 * M; }
+constexpr int wi_ww() { return BW + 2 * ring_mx<M>(); }
 
 // window row r enters the ring: slot 64p + lane, and (producer 0, lanes < 2M) 128 + lane
 template <int M, int BW>
 __device__ __forceinline__ void wi_ring_put(float *__restrict__ ring, const WarpRowI &v, int r,
                                             int p, int lane) {
   constexpr int WW = wi_ww<M, BW>();
-  float *dst = ring + wi_slot<M>(r) * (3 * WW);
+  float *dst = ring + wi_slot<M>(r) * ring_pitch(WW);
   const int k0 = 64 * p + lane;
   dst[k0] = v.c0;
   dst[WW + k0] = 0.5f * (v.r0 - v.l0);
   dst[2 * WW + k0] = 0.5f * (v.s0 - v.n0);
-  if (p == 0 && lane < 2 * M) {
+  if (p == 0 && lane < 2 * ring_mx<M>()) {
     dst[BW + lane] = v.c1;
     dst[WW + BW + lane] = 0.5f * (v.r1 - v.l1);
     dst[2 * WW + BW + lane] = 0.5f * (v.s1 - v.n1);
@@ -2129,7 +2147,7 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
   if (inwin) {
     warp_gather_fn<FM>(
         [&](int cy, int cx) {
-          const float *q = ring + wi_slot<M>(cy) * (3 * WW) + (cx - P.xw0);
+          const float *q = ring + wi_slot<M>(cy) * ring_pitch(WW) + (cx - P.xw0);
           return Tap3{q[0], q[WW], q[2 * WW]};
         },
         wx, wy, fx, fy, sum, sumx, sumy, wsum);
@@ -2416,7 +2434,8 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
   constexpr int K = 2, PX = BW / 64, HALO = roll_halo<2, PX>(), WW = wi_ww<M, BW>();
   static_assert(BW == 64 || BW == 128, "one producer per 64 columns, PX = 1 or 2");
   static_assert(2 * M + 2 <= wi_rows<M>(), "window ring too small for the margin");
-  static_assert(2 * M <= 64, "second window slot per lane");
+  static_assert(2 * ring_mx<M>() <= 64, "second window slot per lane");
+  static_assert(ring_pitch(WW) % 32 == 0, "row pitch: no bank conflicts between ring rows");
   static_assert(kRollAhead == 2 && kWarpAhead == 2, "the step loops are unrolled by 3");
   static_assert(NC == 1 || NC == 2, "one consumer wave, or one per iteration");
   (void)WW;
@@ -2564,7 +2583,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     wa.H = a.H;
     wa.P = a.P;
     WiLane P;
-    P.xw0 = X0 - M;
+    P.xw0 = X0 - ring_mx<M>();
     P.ci = 64 * p + lane;
     const int px = X0 + P.ci;
     P.xc = imin(imax(px, 0), a.W - 1);
@@ -2575,7 +2594,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     unsigned xs[2][3];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const int slot = k == 1 && p == 0 && lane < 2 * M ? BW + lane : P.ci;
+      const int slot = k == 1 && p == 0 && lane < 2 * ring_mx<M>() ? BW + lane : P.ci;
       const int cc = imin(imax(P.xw0 + slot, 0), a.W - 1);
       xs[k][0] = 4u * cc;
       xs[k][1] = 4u * imax(cc - 1, 0);
@@ -2607,7 +2626,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
 
 template <int M, int FM = 0, int BW = 128, int PRIO = 1, int NC = 1>
 __global__ __launch_bounds__(64 * NC + BW) void k_warp_iter(WarpIterArgs w) {
-  __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, BW>()];
+  __shared__ float ring[wi_rows<M>() * ring_pitch(wi_ww<M, BW>())];
   __shared__ float cring[2 * 5 * BW];
   __shared__ float hring[NC == 2 ? 2 * kWiH * BW : 1];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
@@ -2755,6 +2774,45 @@ TVL1_PLAIN __global__ void k_postprocess(float *__restrict__ u, float *__restric
   }
   ur[x] = a;
   vr[x] = b;
+}
+
+// k_postprocess over n same-size pairs of a batch (tvl1_postprocess_batch): pair b =
+// blockIdx.z, its flow at u / v + b * fstride bytes and its frame1 at I1 + b * s1 bytes.
+TVL1_PLAIN __global__ void k_postprocess_batch(float *__restrict__ u, float *__restrict__ v,
+                                               size_t fp, size_t fstride,
+                                               const uint8_t *__restrict__ I1, size_t p1, size_t s1,
+                                               int W, int H, int mode) {
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x >= W || y >= H) return;
+  const size_t b = blockIdx.z;
+  float *ur = reinterpret_cast<float *>(reinterpret_cast<char *>(u) + b * fstride + (size_t)y * fp);
+  float *vr = reinterpret_cast<float *>(reinterpret_cast<char *>(v) + b * fstride + (size_t)y * fp);
+  float a = ur[x], c = vr[x];
+  if (mode >= 1) {
+    a = a + (float)x;
+    c = c + (float)y;
+  }
+  if (mode == 2) {
+    a = a - (float)x;
+    c = c - (float)y;
+  }
+  if (I1[b * s1 + (size_t)y * p1 + x] <= 1) {
+    a = 0.0f;
+    c = 0.0f;
+  }
+  ur[x] = a;
+  vr[x] = c;
+}
+
+// tvl1_gather_flow: out[i] = (u[off[i]], v[off[i]]) (element offsets), one lane per point.
+TVL1_PLAIN __global__ void k_gather_flow(const float *__restrict__ u, const float *__restrict__ v,
+                                         const int64_t *__restrict__ off, int n,
+                                         float2 *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t o = off[i];
+  out[i] = make_float2(u[o], v[o]);
 }
 
 }  // namespace tvl1k

@@ -18,7 +18,7 @@ REPO_ROOT = PKG_ROOT.parent
 ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
 
 TVL1_MAX_LEVELS = 32
-ABI_VERSION = 7          # TVL1_ABI_VERSION of include/tvl1.h
+ABI_VERSION = 8          # TVL1_ABI_VERSION of include/tvl1.h
 STATUS = {0: "TVL1_OK", 1: "TVL1_EINVAL", 2: "TVL1_ESIZE", 3: "TVL1_EHIP",
           4: "TVL1_ENOMEM", 5: "TVL1_ENODEV"}
 

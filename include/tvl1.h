@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TVL1_ABI_VERSION 7
+#define TVL1_ABI_VERSION 8
 #define TVL1_MAX_LEVELS 32
 
 typedef enum tvl1_status {
@@ -258,6 +258,22 @@ tvl1_status tvl1_calc_host(tvl1_ctx *ctx,
 tvl1_status tvl1_postprocess(tvl1_ctx *ctx, float *u, float *v, size_t flow_pitch,
                              const uint8_t *I1, size_t pitch1,
                              int32_t width, int32_t height, int32_t mode, void *stream);
+
+/* tvl1_postprocess on n same-size pairs of a batch in one launch (ABI 8; the CLI's batched
+ * strip jobs, solve_wrapper optflow.cpp:411-473 per ROI): pair b's flow at u / v +
+ * b*flow_pair_stride, its frame1 at I1 + b*pair_stride1 (bytes).  Device pointers, async. */
+tvl1_status tvl1_postprocess_batch(tvl1_ctx *ctx, int32_t n, float *u, float *v,
+                                   size_t flow_pitch, size_t flow_pair_stride,
+                                   const uint8_t *I1, size_t pitch1, size_t pair_stride1,
+                                   int32_t width, int32_t height, int32_t mode, void *stream);
+
+/* The flow values of a few chosen px (ABI 8): out_u[i] = u[offsets[i]], out_v[i] =
+ * v[offsets[i]], offsets in floats from the device pointers u / v (host array of n).  The
+ * point-match output draws npoints px per ROI (random_points, optflow.cpp:522-572) and needs
+ * only their flow, not the whole field.  Host outputs; synchronous on stream. */
+tvl1_status tvl1_gather_flow(tvl1_ctx *ctx, const float *u, const float *v,
+                             const int64_t *offsets, int32_t n, float *out_u, float *out_v,
+                             void *stream);
 
 /* The ctx's own non-blocking HIP stream (hipStream_t as void*): callers that keep
  * several pairs in flight on one device give each ctx its own stream this way. */

@@ -47,7 +47,7 @@ constexpr int M = WI_M, BW = WI_BW, NC = WI_NC, NWV = NC + BW / 64;   // waves p
 #endif
 template <int FM, int PRIO>
 __global__ __launch_bounds__(64 * NC + BW) WI_ATTR void k_probe(WarpIterArgs w, unsigned long long *ts) {
-  __shared__ float ring[wi_rows<M>() * 3 * wi_ww<M, BW>()];
+  __shared__ float ring[wi_rows<M>() * ring_pitch(wi_ww<M, BW>())];
   __shared__ float cring[2 * 5 * BW];
   __shared__ float hring[NC == 2 ? 2 * kWiH * BW : 1];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
