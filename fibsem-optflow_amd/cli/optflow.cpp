@@ -390,16 +390,23 @@ void random_points(const float *fx, const float *fy, int W, int H,
 // Drawn by a partial Fisher-Yates over the implicit list (row counts + a sparse swap map),
 // and only those px's flow values are read back: no 25 M-entry shuffle, no full download.
 // Debug runs keep the exact shuffle (random_points above) so their output is reproducible.
-bool random_points_sampled(DeviceCtx &dc, size_t fp, int W, int H, const ofio::Image8 &f0,
-                           const ofio::Image8 &f1, const Rect &r0, const Rect &r1, Value &im,
-                           const Value &args, bool features, std::string &err) {
-  const float scale = im.get("scale", args.get("scale", 0.5).asFloat()).asFloat();
-  const float inv_scale = 1. / scale;
-  const int npoints = im.get("npoints", args.get("npoints", 25).asInt()).asInt();
+// An engine status that leaves the device context in doubt (a HIP call failed, memory ran
+// out): the pair is retried on a rebuilt context.  TVL1_EINVAL / TVL1_ESIZE are input or
+// config errors (a bad medianFiltering, an ROI the solver rejects): reported like the
+// reference's input errors, without a context rebuild (ADVICE r2).
+static bool device_fault(tvl1_status s) {
+  return s == TVL1_EHIP || s == TVL1_ENOMEM || s == TVL1_ENODEV;
+}
+
+// The px the sampled random_points draws: npoints distinct px of the mask (frame0 > 1) |
+// (frame1 > 1) over a W x H ROI whose rows are row0(y) / row1(y); *total = the mask's size.
+template <class R0, class R1>
+std::vector<std::pair<int, int>> sample_points(R0 row0, R1 row1, int W, int H, int npoints,
+                                               uint64_t *total_out) {
   // mask = (frame0 > 1) | (frame1 > 1) on the ROIs (optflow.cpp:486-494), counted per row
   std::vector<uint64_t> prefix((size_t)H + 1, 0);
   for (int y = 0; y < H; ++y) {
-    const uint8_t *a = f0.row(r0.y + y) + r0.x, *b = f1.row(r1.y + y) + r1.x;
+    const uint8_t *a = row0(y), *b = row1(y);
     unsigned c = 0;
     for (int x = 0; x < W; ++x) c += (a[x] > 1) | (b[x] > 1);
     prefix[y + 1] = prefix[y] + c;
@@ -428,23 +435,36 @@ bool random_points_sampled(DeviceCtx &dc, size_t fp, int W, int H, const ofio::I
   for (uint64_t idx : pick) {
     const int y = (int)(std::upper_bound(prefix.begin(), prefix.end(), idx) - prefix.begin()) - 1;
     uint64_t left = idx - prefix[y];
-    const uint8_t *a = f0.row(r0.y + y) + r0.x, *b = f1.row(r1.y + y) + r1.x;
+    const uint8_t *a = row0(y), *b = row1(y);
     int x = 0;
     for (;; ++x)
       if (((a[x] > 1) | (b[x] > 1)) && left-- == 0) break;
     pts.emplace_back(x, y);
   }
+  *total_out = total;
+  return pts;
+}
+
+bool random_points_sampled(DeviceCtx &dc, size_t fp, int W, int H, const ofio::Image8 &f0,
+                           const ofio::Image8 &f1, const Rect &r0, const Rect &r1, Value &im,
+                           const Value &args, bool features, std::string &err) {
+  const float scale = im.get("scale", args.get("scale", 0.5).asFloat()).asFloat();
+  const float inv_scale = 1. / scale;
+  const int npoints = im.get("npoints", args.get("npoints", 25).asInt()).asInt();
+  uint64_t total = 0;
+  const std::vector<std::pair<int, int>> pts = sample_points(
+      [&](int y) { return f0.row(r0.y + y) + r0.x; }, [&](int y) { return f1.row(r1.y + y) + r1.x; },
+      W, H, npoints, &total);
   std::vector<float> vx(pts.size()), vy(pts.size());
-  for (size_t i = 0; i < pts.size(); ++i) {
-    const size_t off = (size_t)pts[i].second * fp + (size_t)pts[i].first * 4;
-    if (hipMemcpyAsync(&vx[i], (const char *)dc.du + off, 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
-        hipMemcpyAsync(&vy[i], (const char *)dc.dv + off, 4, hipMemcpyDeviceToHost, dc.stream) != hipSuccess) {
-      err = "flow read-back failed", dc.faulted = true;
-      return false;
-    }
-  }
-  if (hipStreamSynchronize(dc.stream) != hipSuccess) {
-    err = "flow read-back failed", dc.faulted = true;
+  std::vector<int64_t> off(pts.size());
+  for (size_t i = 0; i < pts.size(); ++i)
+    off[i] = (int64_t)(pts[i].second * (fp / 4) + pts[i].first);
+  // only the chosen px's flow crosses PCIe (tvl1_gather_flow: one upload, one gather, one
+  // download), synchronous
+  if (const tvl1_status s = tvl1_gather_flow(dc.ctx, dc.du, dc.dv, off.data(), (int32_t)off.size(),
+                                             vx.data(), vy.data(), dc.stream);
+      s != TVL1_OK) {
+    err = std::string("flow read-back failed: ") + tvl1_last_error(dc.ctx), dc.faulted = device_fault(s);
     return false;
   }
   emit_points(pts, vx, vy, total > 0, im, r0, r1, inv_scale, features);
@@ -471,13 +491,6 @@ struct PairResult {
   Value stats;
 };
 
-// An engine status that leaves the device context in doubt (a HIP call failed, memory ran
-// out): the pair is retried on a rebuilt context.  TVL1_EINVAL / TVL1_ESIZE are input or
-// config errors (a bad medianFiltering, an ROI the solver rejects): reported like the
-// reference's input errors, without a context rebuild (ADVICE r2).
-static bool device_fault(tvl1_status s) {
-  return s == TVL1_EHIP || s == TVL1_ENOMEM || s == TVL1_ENODEV;
-}
 
 // solve_wrapper (optflow.cpp:395-496) for one ROI.
 bool solve_wrapper(DeviceCtx &dc, const ofio::Image8 &f0, const ofio::Image8 &f1, const Rect &r0,
@@ -795,6 +808,10 @@ struct Loaded {
   bool ok = false;
   ofio::Image8 img;
   std::string err;
+  // load_bands: the pre-scaled slice's size and the row bands asked for
+  int W = 0, H = 0;
+  std::vector<ofio::Image8> bands;
+  bool partial = false;   // only the bands' source rows were read
 };
 using LoadFuture = std::shared_future<std::shared_ptr<Loaded>>;
 
@@ -820,6 +837,32 @@ class DecodePool {
       if (scale != 1) ofio::resize_u8(img, scale, scale, r->img);
       else r->img = std::move(img);
       r->ok = true;
+      return r;
+    });
+    LoadFuture f = task->get_future().share();
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      q_.emplace_back([task] { (*task)(); });
+    }
+    cv_.notify_one();
+    return f;
+  }
+  // imread + resize(scale) of only the rows of get_rois' top / bottom ROIs (SURVEY 3.2's
+  // production strips): bands in `keys` order, top = [0, top), bottom = [H - bottom, H) of
+  // the pre-scaled slice (ofio::read_gray8_bands: strip-organised TIFF reads just those rows)
+  LoadFuture load_bands(const std::string &path, float scale, std::vector<std::string> keys,
+                        int top, int bottom) {
+    auto task = std::make_shared<std::packaged_task<std::shared_ptr<Loaded>()>>([=] {
+      auto r = std::make_shared<Loaded>();
+      r->ok = ofio::read_gray8_bands(
+          path, scale,
+          [&](int, int h) {
+            std::vector<std::pair<int, int>> b;
+            for (const auto &k : keys) b.push_back(k == "top" ? std::make_pair(0, top)
+                                                              : std::make_pair(h - bottom, h));
+            return b;
+          },
+          r->W, r->H, r->bands, r->err, &r->partial);
       return r;
     });
     LoadFuture f = task->get_future().share();
@@ -883,7 +926,10 @@ static int from_file(Value &args, bool plan_only) {
   const unsigned hc = std::max(2u, std::thread::hardware_concurrency());
   DecodePool pool(std::max(1, args.get("decode_threads", (int)std::min(16u, hc - 1)).asInt()));
   std::atomic<size_t> next{0};
-  const size_t chunk = std::max<size_t>(1, std::min<size_t>(16, n / std::max<size_t>(1, devices.size() * 4)));
+  // the pairs the per-pair workers solve (all of them unless strip batching takes some)
+  std::vector<size_t> todo;
+  size_t m = 0;
+  size_t chunk = 1;
   std::atomic<int> hard_error{0};
 
   auto worker = [&](int device) {
@@ -910,7 +956,8 @@ static int from_file(Value &args, bool plan_only) {
       return path + "|" + b;
     };
     auto queue_chunk = [&](size_t start) {
-      for (size_t i = start; i < std::min(n, start + chunk); ++i) {
+      for (size_t k = start; k < std::min(m, start + chunk); ++k) {
+        const size_t i = todo[k];
         const float sc = scale_of(i);
         for (const char *side : {"p", "q"}) {
           const std::string path = images[i][side].asString(), k = key_of(path, sc);
@@ -919,13 +966,14 @@ static int from_file(Value &args, bool plan_only) {
       }
     };
     size_t next_start = next.fetch_add(chunk);
-    if (next_start < n) queue_chunk(next_start);
+    if (next_start < m) queue_chunk(next_start);
     for (;;) {
       const size_t start = next_start;
-      if (start >= n) break;
+      if (start >= m) break;
       next_start = next.fetch_add(chunk);
-      if (next_start < n) queue_chunk(next_start);
-      for (size_t i = start; i < std::min(n, start + chunk); ++i) {
+      if (next_start < m) queue_chunk(next_start);
+      for (size_t kk = start; kk < std::min(m, start + chunk); ++kk) {
+        const size_t i = todo[kk];
         Value im = images[i];
         const std::string p = im["p"].asString(), q = im["q"].asString();
         const float scale = scale_of(i);
@@ -956,14 +1004,18 @@ static int from_file(Value &args, bool plan_only) {
         // last pair of the two queued chunks that names it, whether or not it was decoded
         // for nothing because the slice was already resident
         auto needed_later = [&](const std::string &k) {
-          for (size_t j = i + 1; j < std::min(n, start + chunk); ++j)
+          for (size_t jj = kk + 1; jj < std::min(m, start + chunk); ++jj) {
+            const size_t j = todo[jj];
             if (key_of(images[j]["p"].asString(), scale_of(j)) == k ||
                 key_of(images[j]["q"].asString(), scale_of(j)) == k)
               return true;
-          for (size_t j = next_start; j < std::min(n, next_start + chunk); ++j)
+          }
+          for (size_t jj = next_start; jj < std::min(m, next_start + chunk); ++jj) {
+            const size_t j = todo[jj];
             if (key_of(images[j]["p"].asString(), scale_of(j)) == k ||
                 key_of(images[j]["q"].asString(), scale_of(j)) == k)
               return true;
+          }
           return false;
         };
         auto retire = [&](const std::string &k) {
@@ -1109,6 +1161,331 @@ static int from_file(Value &args, bool plan_only) {
     close_device(dc);
   };
 
+  // ---- batched strip jobs.  The production shape (SURVEY 3.2,
+  // gen_cross_file_list.py:75-99: global top / bottom ROIs at scale 0.5, per-image keys only
+  // p, q, the ids and output_name) is two ~100-row strips per pair: one tvl1_calc per strip
+  // is ~400 launches of a few microseconds, so the GPU idles on dispatch.  Here a worker
+  // takes a chunk of such pairs, reads only the strips' rows of each slice (read_gray8_bands),
+  // and solves each ROI key's strips of the whole chunk in one tvl1_calc_batch (every strip's
+  // flow and iteration counts identical to its own tvl1_calc), then writes each pair's
+  // outputs as solve_wrapper would (optflow.cpp:395-496).  Pairs that turn out not to fit
+  // (frames of different sizes, an ROI outside the slice, an unreadable file) are solved by
+  // the per-pair path afterwards, which reports them exactly as before.
+  std::vector<std::string> roi_keys;   // sorted, like solve_rois' std::map (optflow.cpp:339)
+  int roi_top = 0, roi_bottom = 0;
+  std::vector<char> deferred(n, 0);
+  std::vector<size_t> batched;         // pairs for the batch workers, in order
+  std::atomic<size_t> bnext{0};
+  size_t bchunk = 0;
+  auto batch_worker = [&](int device) {
+    DeviceCtx dc;
+    std::string err;
+    if (!open_device(dc, device, err)) {
+      std::lock_guard<std::mutex> lk(g_io_mutex);
+      fprintf(stderr, "Error: cannot use GPU %d: %s\n", device, err.c_str());
+      close_device(dc);
+      hard_error = 1;
+      return;
+    }
+    const float scale = args.get("scale", 0.5).asFloat();
+    char sbuf[32];
+    snprintf(sbuf, sizeof sbuf, "%0.2f", scale);
+    const tvl1_params prm = generate_TV_args(Value(), args);
+    const std::string otype = output_type_of(Value(), args);
+    const int mode = otype == "map" ? 1 : 0;   // no features on this path
+    // device buffers (grown): the chunk's packed frames and flows of one ROI key
+    uint8_t *dP = nullptr, *dQ = nullptr;
+    float *dU = nullptr, *dV = nullptr;
+    size_t cap_px = 0;
+    uint8_t *hP = nullptr, *hQ = nullptr;   // page-locked packing buffers (reused)
+    size_t cap_h = 0;
+    auto release = [&] {
+      for (void *q : {(void *)dP, (void *)dQ, (void *)dU, (void *)dV})
+        if (q) (void)hipFree(q);
+      for (void *q : {(void *)hP, (void *)hQ})
+        if (q) (void)hipHostFree(q);
+      dP = dQ = nullptr, dU = dV = nullptr, hP = hQ = nullptr;
+      cap_px = cap_h = 0;
+    };
+    auto grow = [&](size_t px) {
+      if (px > cap_px) {
+        for (void *q : {(void *)dP, (void *)dQ, (void *)dU, (void *)dV})
+          if (q) (void)hipFree(q);
+        dP = dQ = nullptr, dU = dV = nullptr, cap_px = 0;
+        if (hipMalloc((void **)&dP, px) != hipSuccess || hipMalloc((void **)&dQ, px) != hipSuccess ||
+            hipMalloc((void **)&dU, 4 * px) != hipSuccess || hipMalloc((void **)&dV, 4 * px) != hipSuccess)
+          return false;
+        cap_px = px;
+      }
+      if (px > cap_h) {
+        for (void *q : {(void *)hP, (void *)hQ})
+          if (q) (void)hipHostFree(q);
+        hP = hQ = nullptr, cap_h = 0;
+        if (hipHostMalloc((void **)&hP, px, hipHostMallocPortable) != hipSuccess ||
+            hipHostMalloc((void **)&hQ, px, hipHostMallocPortable) != hipSuccess)
+          return false;
+        cap_h = px;
+      }
+      return true;
+    };
+    std::map<std::string, LoadFuture> pending;   // path -> its bands (this chunk + the next)
+    auto queue_chunk = [&](size_t start) {
+      for (size_t k = start; k < std::min(batched.size(), start + bchunk); ++k)
+        for (const char *side : {"p", "q"}) {
+          const std::string path = images[batched[k]][side].asString();
+          if (!pending.count(path))
+            pending.emplace(path, pool.load_bands(path, scale, roi_keys, roi_top, roi_bottom));
+        }
+    };
+    size_t next_start = bnext.fetch_add(bchunk);
+    if (next_start < batched.size()) queue_chunk(next_start);
+    for (;;) {
+      const size_t start = next_start;
+      if (start >= batched.size()) break;
+      next_start = bnext.fetch_add(bchunk);
+      if (next_start < batched.size()) queue_chunk(next_start);
+      const size_t end = std::min(batched.size(), start + bchunk);
+      // the chunk's pairs whose two slices decoded to equal sizes, with their bands
+      struct Item {
+        size_t i;
+        Value im;
+        std::shared_ptr<Loaded> p, q;
+      };
+      std::vector<Item> items;
+      for (size_t k = start; k < end; ++k) {
+        const size_t i = batched[k];
+        Item it{i, images[i], nullptr, nullptr};
+        const std::string p = it.im["p"].asString(), q = it.im["q"].asString();
+        it.im["scale"] = it.im.get("scale", (double)scale).asDouble();
+        it.im["output"] = it.im.get("output", args["output_dir"].asString() + "/" +
+                                                  it.im["output_name"].asString() + "_" + sbuf);
+        it.p = pending.at(p).get();
+        it.q = pending.at(q).get();
+        if (!it.p->ok || !it.q->ok || it.p->W != it.q->W || it.p->H != it.q->H) {
+          deferred[i] = 1;   // the per-pair path reports or aligns it as the reference does
+          continue;
+        }
+        {
+          std::lock_guard<std::mutex> lk(g_io_mutex);
+          printf("%s %s\n", p.c_str(), q.c_str());
+          fflush(stdout);
+        }
+        if (skip_existing && otype != "random_points") {
+          bool all = true;
+          for (auto &key : roi_keys) {
+            const std::string base = it.im["output"].asString() + "_" + key;
+            all = all && file_exists(base + "_x.tiff") && file_exists(base + "_y.tiff");
+          }
+          if (all) {
+            results[i].done = results[i].ok = true;
+            continue;
+          }
+        }
+        items.push_back(std::move(it));
+      }
+      // slices no later pair of this or the next chunk names leave the map
+      {
+        std::map<std::string, LoadFuture> keep;
+        for (size_t k = next_start; k < std::min(batched.size(), next_start + bchunk); ++k)
+          for (const char *side : {"p", "q"}) {
+            const std::string path = images[batched[k]][side].asString();
+            auto f = pending.find(path);
+            if (f != pending.end()) keep.emplace(path, f->second);
+          }
+        pending.swap(keep);
+      }
+      const int nb = (int)items.size();
+      if (nb == 0) continue;
+      bool inject = false;
+      for (auto &it : items) inject = inject || inject_fault(it.i);
+      // one attempt, and after a device error one more on a rebuilt context
+      for (int attempt = 0; attempt < 2; ++attempt) {
+        std::string e;
+        bool ok = true;
+        std::vector<std::vector<Value>> solves(nb);
+        // debug random_points: the flows of every key, drawn pair by pair afterwards so the
+        // unseeded generator is consumed in the per-pair path's order (pair, then key)
+        std::vector<std::vector<float>> dbg_fx(roi_keys.size()), dbg_fy(roi_keys.size());
+        auto fail = [&](const std::string &what, tvl1_status st) {
+          e = what + (dc.ctx ? std::string(": ") + tvl1_last_error(dc.ctx) : std::string());
+          dc.faulted = device_fault(st) || st == TVL1_OK;
+          ok = false;
+        };
+        if (attempt == 0 && inject) fail("injected device fault", TVL1_EHIP);
+        if (ok && tvl1_set_params(dc.ctx, &prm) != TVL1_OK) fail("tvl1_set_params", TVL1_EINVAL);
+        for (size_t kk = 0; ok && kk < roi_keys.size(); ++kk) {
+          const std::string &key = roi_keys[kk];
+          const int W = items[0].p->W, h = items[0].p->bands[kk].height;
+          const int y0 = key == "top" ? 0 : items[0].p->H - h;
+          const size_t px = (size_t)W * h;
+          bool same = true;   // one geometry per launch: every pair's slices of one size
+          for (auto &it : items) same = same && it.p->W == W && it.p->bands[kk].height == h && it.p->H == items[0].p->H;
+          if (!same) {   // mixed slice sizes in one job: the per-pair path takes the chunk
+            for (auto &it : items) deferred[it.i] = 1;
+            items.clear();
+            break;
+          }
+          if (!grow(px * nb)) {
+            fail("hipMalloc failed for a strip batch", TVL1_ENOMEM);
+            break;
+          }
+          for (int b = 0; b < nb; ++b) {
+            memcpy(hP + px * b, items[b].p->bands[kk].data.data(), px);
+            memcpy(hQ + px * b, items[b].q->bands[kk].data.data(), px);
+          }
+          if (hipMemcpyAsync(dP, hP, px * nb, hipMemcpyHostToDevice, dc.stream) != hipSuccess ||
+              hipMemcpyAsync(dQ, hQ, px * nb, hipMemcpyHostToDevice, dc.stream) != hipSuccess) {
+            fail("upload failed", TVL1_EHIP);
+            break;
+          }
+          std::vector<tvl1_stats> st(nb);
+          std::vector<int32_t> wi((size_t)nb * TVL1_MAX_LEVELS * std::max(1, prm.warps), -1);
+          for (int b = 0; b < nb; ++b) {
+            memset(&st[b], 0, sizeof st[b]);
+            st[b].warp_iterations = wi.data() + (size_t)b * TVL1_MAX_LEVELS * std::max(1, prm.warps);
+            st[b].warp_iterations_capacity = TVL1_MAX_LEVELS * std::max(1, prm.warps);
+          }
+          const auto t0 = std::chrono::steady_clock::now();
+          tvl1_status sc = tvl1_calc_batch(dc.ctx, nb, dP, W, px, dQ, W, px, W, h, dU, dV, 4 * (size_t)W,
+                                           4 * px, st.data(), dc.stream);
+          if (sc == TVL1_OK)
+            sc = tvl1_postprocess_batch(dc.ctx, nb, dU, dV, 4 * (size_t)W, 4 * px, dQ, W, px, W, h,
+                                        mode, dc.stream);
+          if (sc != TVL1_OK) {
+            fail("strip batch", sc);
+            break;
+          }
+          const bool sampled = otype == "random_points" && !debug;
+          std::vector<float> fx, fy;   // whole flows (TIFF outputs, debug point matches)
+          std::vector<std::vector<std::pair<int, int>>> pts(nb);
+          std::vector<uint64_t> tot(nb, 0);
+          if (sampled) {
+            std::vector<int64_t> off;
+            for (int b = 0; b < nb; ++b) {
+              const ofio::Image8 &a = items[b].p->bands[kk], &c = items[b].q->bands[kk];
+              const int np = items[b].im.get("npoints", args.get("npoints", 25).asInt()).asInt();
+              pts[b] = sample_points([&](int y) { return a.row(y); }, [&](int y) { return c.row(y); },
+                                     W, h, np, &tot[b]);
+              for (auto &pt : pts[b]) off.push_back((int64_t)(px * b + (size_t)pt.second * W + pt.first));
+            }
+            fx.resize(off.size());
+            fy.resize(off.size());
+            sc = tvl1_gather_flow(dc.ctx, dU, dV, off.data(), (int32_t)off.size(), fx.data(),
+                                  fy.data(), dc.stream);
+            if (sc != TVL1_OK) {
+              fail("flow read-back", sc);
+              break;
+            }
+          } else {
+            fx.resize(px * nb);
+            fy.resize(px * nb);
+            if (hipMemcpyAsync(fx.data(), dU, 4 * px * nb, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
+                hipMemcpyAsync(fy.data(), dV, 4 * px * nb, hipMemcpyDeviceToHost, dc.stream) != hipSuccess ||
+                hipStreamSynchronize(dc.stream) != hipSuccess) {
+              fail("flow download failed", TVL1_EHIP);
+              break;
+            }
+          }
+          const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+          const Rect r{0, y0, W, h};
+          size_t o = 0;
+          for (int b = 0; b < nb && ok; ++b) {
+            Value &im = items[b].im;
+            Value sv;
+            sv["roi"][0] = 0;
+            sv["roi"][1] = y0;
+            sv["roi"][2] = W;
+            sv["roi"][3] = h;
+            sv["seconds"] = secs;
+            sv["batch"] = nb;
+            sv["levels"] = st[b].levels;
+            sv["iterations"] = (int64_t)st[b].iterations_total;
+            sv["checks"] = (int64_t)st[b].checks_total;
+            const size_t nw = std::min((size_t)st[b].warp_iterations_capacity,
+                                       (size_t)std::max(0, st[b].levels) * std::max(1, prm.warps));
+            for (size_t k = 0; k < nw; ++k) sv["warp_iterations"][(int)k] = st[b].warp_iterations[k];
+            sv["read_rows_only"] = items[b].p->partial && items[b].q->partial;
+            solves[b].push_back(sv);
+            if (sampled) {
+              std::vector<float> vx(fx.begin() + o, fx.begin() + o + pts[b].size()),
+                  vy(fy.begin() + o, fy.begin() + o + pts[b].size());
+              o += pts[b].size();
+              emit_points(pts[b], vx, vy, tot[b] > 0, im, r, r, 1.f / scale, false);
+            } else if (otype == "random_points") {   // debug: drawn below, pair by pair
+            } else {
+              const std::string base = im["output"].asString() + "_" + key;
+              std::string we;
+              if (!ofio::write_tiff_f32(base + "_x.tiff", fx.data() + px * b, W, h, 4 * (size_t)W, we) ||
+                  !ofio::write_tiff_f32(base + "_y.tiff", fy.data() + px * b, W, h, 4 * (size_t)W, we)) {
+                e = we, ok = false;   // an output error, not a device fault
+                dc.faulted = false;
+              }
+            }
+          }
+          if (otype == "random_points" && !sampled) {
+            dbg_fx[kk].swap(fx);
+            dbg_fy[kk].swap(fy);
+          }
+        }
+        if (items.empty()) break;   // handed to the per-pair path
+        if (ok && otype == "random_points" && debug) {   // the exact shuffle (random_points)
+          for (int b = 0; b < nb; ++b)
+            for (size_t kk = 0; kk < roi_keys.size(); ++kk) {
+              const ofio::Image8 &a = items[b].p->bands[kk], &c = items[b].q->bands[kk];
+              const int W = a.width, h = a.height;
+              const size_t px = (size_t)W * h;
+              const Rect r{0, roi_keys[kk] == "top" ? 0 : items[b].p->H - h, W, h};
+              std::vector<uint8_t> mask(px);
+              for (size_t k = 0; k < px; ++k) mask[k] = (a.data[k] > 1) | (c.data[k] > 1);
+              random_points(dbg_fx[kk].data() + px * b, dbg_fy[kk].data() + px * b, W, h,
+                            items[b].im, args, r, r, mask, false);
+            }
+        }
+        if (ok) {
+          for (int b = 0; b < nb; ++b) {
+            const size_t i = items[b].i;
+            for (auto &sv : solves[b]) results[i].stats["solves"].append(sv);
+            if (otype == "random_points") results[i].pms.push_back(move_pm(items[b].im));
+            results[i].ok = results[i].done = true;
+          }
+          break;
+        }
+        if (attempt == 0 && dc.faulted) {
+          {
+            std::lock_guard<std::mutex> lk(g_io_mutex);
+            fprintf(stderr, "Warning: strip batch of %d pairs (%zu..): %s; retrying on a fresh device context\n",
+                    nb, items[0].i, e.c_str());
+          }
+          for (auto &it : items) {   // the retry starts from the decoded bands again
+            it.im = images[it.i];
+            it.im["scale"] = it.im.get("scale", (double)scale).asDouble();
+            it.im["output"] = it.im.get("output", args["output_dir"].asString() + "/" +
+                                                      it.im["output_name"].asString() + "_" + sbuf);
+          }
+          release();
+          close_device(dc);
+          std::string e2;
+          if (!open_device(dc, device, e2)) {
+            e = "device context could not be rebuilt: " + e2;
+          } else {
+            continue;
+          }
+        }
+        std::lock_guard<std::mutex> lk(g_io_mutex);
+        for (auto &it : items) {
+          results[it.i].done = true;
+          results[it.i].ok = false;
+          fprintf(stderr, "Error: pair %zu (%s %s): %s\n", it.i, it.im["p"].asString().c_str(),
+                  it.im["q"].asString().c_str(), e.c_str());
+        }
+        break;
+      }
+    }
+    if (dc.stream) (void)hipStreamSynchronize(dc.stream);
+    release();
+    close_device(dc);
+  };
+
   // build-only "inflight": pairs solved concurrently per GPU (one worker thread, ctx and
   // stream each) so one pair's residual read-backs overlap another pair's kernels.  Strip
   // jobs (every ROI "top" / "bottom", the production shape: two 100-row strips per pair)
@@ -1117,8 +1494,48 @@ static int from_file(Value &args, bool plan_only) {
   bool strip_job = args.isMember("rois") && args["rois"].isObject() && args["rois"].size() > 0;
   if (strip_job)
     for (auto &k : args["rois"].memberNames()) strip_job = strip_job && (k == "top" || k == "bottom");
+  // build-only "strip_batch": strip pairs per tvl1_calc_batch (default 256; 0 or 1 = one
+  // tvl1_calc per strip, the r3 path).  A pair is batched when the job's ROIs are all top /
+  // bottom and its own keys are only the production ones (gen_cross_file_list.py:47-54);
+  // features, per-image ROIs / scales / TV parameters go the per-pair way.
+  const int strip_batch = std::min(256, std::max(0, args.get("strip_batch", 256).asInt()));
+  const std::string gotype = output_type_of(Value(), args);
+  const bool batching = !plan_only && strip_job && strip_batch > 1 && !resolve_features(Value(), args) &&
+                        (gotype == "map" || gotype == "flow" || gotype == "random_points");
+  if (batching) {
+    roi_keys = args["rois"].memberNames();
+    roi_top = args["rois"].get("top", 300).asInt();
+    roi_bottom = args["rois"].get("bottom", 300).asInt();
+    static const char *kProd[] = {"p", "q", "pId", "qId", "pGroupId", "qGroupId", "output_name", "output"};
+    for (size_t i = 0; i < n; ++i) {
+      bool ok = images[i].isObject();
+      for (auto &k : images[i].memberNames())
+        ok = ok && std::find_if(std::begin(kProd), std::end(kProd), [&](const char *x) { return k == x; }) !=
+                       std::end(kProd);
+      (ok ? batched : todo).push_back(i);
+    }
+  } else {
+    for (size_t i = 0; i < n; ++i) todo.push_back(i);
+  }
+  if (!batched.empty()) {
+    // "inflight" batches per GPU (default 2: one batch's residual syncs overlap the other's
+    // kernels), chunks small enough that every worker gets one
+    const int binflight = std::max(1, args.get("inflight", 2).asInt());
+    const size_t workers = devices.size() * (size_t)binflight;
+    bchunk = std::max<size_t>(1, std::min<size_t>(strip_batch, (batched.size() + workers - 1) / workers));
+    std::vector<std::thread> th;
+    for (int f = 0; f < binflight; ++f)
+      for (int d : devices) th.emplace_back(batch_worker, d);
+    for (auto &t : th) t.join();
+    for (size_t i = 0; i < n; ++i)
+      if (deferred[i]) todo.push_back(i);
+    std::sort(todo.begin(), todo.end());
+  }
+  m = todo.size();
+  chunk = std::max<size_t>(1, std::min<size_t>(16, m / std::max<size_t>(1, devices.size() * 4)));
   const int inflight = std::max(1, args.get("inflight", strip_job ? 8 : 3).asInt());
-  if (plan_only || (devices.size() == 1 && inflight == 1)) {
+  if (m == 0) {
+  } else if (plan_only || (devices.size() == 1 && inflight == 1)) {
     worker(devices[0]);
   } else {
     std::vector<std::thread> th;

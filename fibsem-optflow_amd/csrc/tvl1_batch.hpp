@@ -32,6 +32,7 @@ struct BatchSel {            // the pairs a launch works on, passed by value
   uint8_t idx[kBatchMax];    // pair indices
   BatchMask ubit, pbit;      // per pair: current u set / p set (0 or 1)
   BatchMask cerr, pzero;     // per pair: the pass ends in a residual check / p == 0
+  BatchMask storec;          // kb_warp_iter: per pair, store the warp constants to HBM
 };
 
 __device__ __forceinline__ int bsel_bit(const BatchMask &m, int b) { return m.test(b); }
@@ -96,8 +97,10 @@ __global__ __launch_bounds__(64 * NW) void kb_warp_ring(BatchRing br) {
 
 // K5 + the warp's first pass (2 iterations ending in the first check) fused, as
 // k_warp_iter (warp_iter_body; NC consumer wavefronts), on each selected pair (blockIdx.y =
-// entry of sel).  The warp constants are always stored (pairs that continue read them in
-// later passes).
+// entry of sel).  The warp constants go to HBM only for the pairs in sel.storec -- those
+// predicted to need later passes (a level's first warp, or a pair whose previous warp ran
+// past its first check), as k_warp_iter's store_c; a pair that continues without them is
+// re-gathered by kb_warp_ring after the check.
 struct BatchWI {
   WarpIterArgs w;            // geometry and scalars; pointers set per pair
   const float *I0, *I1;      // level s images of pair 0 (pair stride ips)
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(64 * NC + 128) void kb_warp_iter(BatchWI bw) {
     a.partials = bw.partials + (size_t)b * bw.nblk;
     w.I0 = bw.I0 + b * bw.ips;
     w.I1 = bw.I1 + b * bw.ips;
-    w.store_c = 1;
+    w.store_c = bsel_bit(bw.sel.storec, b);
     RollBufs &B = w.ra.b;   // group geometry set by the host
     B.c = a.I1wx;
     B.us = a.u1s;
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(64 * NC + 128) void kb_warp_iter(BatchWI bw) {
   }
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves) return;
-  warp_iter_body<M, FM, 128, 0, NC>(w, wid, ring, cring, hring);
+  warp_iter_body<M, FM, 128, 0, NC, TVL1_WI_S2F && NC == 2>(w, wid, ring, cring, hring);
 }
 
 // K6+K8(+K7 partials): one pass of K iterations as a k_iterate_roll<false, K, PX> wavefront
@@ -239,12 +242,13 @@ TVL1_PLAIN __global__ void kb_median(BatchMedian w) {
   w.U[us ^ 1][c][b * w.ps + (size_t)y * w.P + x] = v[n / 2];
 }
 
-// K7 for the selected pairs: fixed-order sum of pair b's partials into out[b].
-TVL1_PLAIN __global__ void kb_reduce(const double *__restrict__ partials, int n, BatchSel sel,
-                          double *__restrict__ out) {
+// K7 for the selected pairs: fixed-order sum of pair b's n partials (at partials + b * stride)
+// into out[b].
+TVL1_PLAIN __global__ void kb_reduce(const double *__restrict__ partials, size_t stride, int n,
+                                     BatchSel sel, double *__restrict__ out) {
   __shared__ double s[kBlock];
   const int b = sel.idx[blockIdx.x];
-  const double *p = partials + (size_t)b * n;
+  const double *p = partials + (size_t)b * stride;
   double acc = 0.0;
   for (int i = threadIdx.x; i < n; i += kBlock) acc += p[i];
   s[threadIdx.x] = acc;

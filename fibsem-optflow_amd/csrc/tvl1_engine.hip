@@ -132,6 +132,10 @@ struct tvl1_ctx {
   size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
   double *bpartials = nullptr;
   int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
+  int batch_group = 1;                  // TVL1_BATCH_GROUP=0: r3's lock-step passes (the
+                                        // shortest pass any pair allows, for all)
+  int batch_store_pred = 1;             // TVL1_BATCH_STORE=1: kb_warp_iter always stores the
+                                        // warp constants (r3); default: only predicted pairs
   char *gather_scratch = nullptr;       // tvl1_gather_flow's offsets and values
   size_t gather_bytes = 0;
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
@@ -1535,10 +1539,14 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
   const float taut = (float)(prm.tau / prm.theta);
   const float upmul = (float)(1.0 / prm.scale_step);
   BatchMask ubit{}, pbit{};
-  std::vector<int64_t> level_iters((size_t)n * TVL1_MAX_LEVELS, 0), checks(n, 0);
+  std::vector<int64_t> level_iters((size_t)n * TVL1_MAX_LEVELS, 0), checks(n, 0), regathers(n, 0);
   std::vector<int> nit(n);
   std::vector<double> err(n), prev(n);
   std::vector<char> act(n);
+  // per pair: its previous warp on this level stopped at the first check, so this warp's
+  // fused pass is predicted to stop there too and its constants are not stored (k_warp_iter's
+  // store_c rule)
+  std::vector<char> stopped_first(n, 0);
   for (int s = L - 1; s >= 0; --s) {
     const int lw = g.ws[s], lh = g.hs[s], P = g.ps[s];
     const double scaledEps = prm.epsilon * prm.epsilon * (double)lw * (double)lh;
@@ -1604,6 +1612,12 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         wi.sel.ubit = ubit;
         wi.sel.pbit = pbit;
         wi.sel.pzero = pzero;
+        int nstore = 0;
+        for (int b = 0; b < n; ++b)
+          if (wp == 0 || !stopped_first[b] || !c->batch_store_pred) {
+            wi.sel.storec.set(b);
+            ++nstore;
+          }
         const size_t tkw = prof_begin(c, st);
 #define KB_WITER(FM)                                                                             \
   if (c->wi_nc == 2)                                                                            \
@@ -1625,11 +1639,11 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           const double band_bytes = (double)wi.w.ra.bands * 128 * rows * 4.0;
           const double hbm = band_bytes * ((double)nz * 3 + (double)(n - nz) * 7 +
                                            (double)n * wi_ww<6, 128>() / 128) +
-                             (double)n * Nl * 4.0 * 9.0;
+                             Nl * 4.0 * (6.0 * n + 3.0 * nstore);
           prof_end(c, st, tkw, 0, (double)n * Nl * (64.0 * 2 + 40.0), hbm);
         }
-        hipLaunchKernelGGL(kb_reduce, dim3(n), dim3(kBlock), 0, st, c->bpartials, wi.w.ra.waves,
-                           all, c->pinned_dev + 8);
+        hipLaunchKernelGGL(kb_reduce, dim3(n), dim3(kBlock), 0, st, c->bpartials,
+                           (size_t)wi.w.ra.waves, wi.w.ra.waves, all, c->pinned_dev + 8);
         HIP_TRY(c, hipEventRecord(c->ev_check[0], st));
       } else {   // k_warp_ring's streaming LDS-ring gather, per pair
         BatchRing br{};
@@ -1666,7 +1680,10 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
       if (fuse) {   // the fused first pass: n = 0 (no check), n = 1 (check)
         HIP_TRY(c, hipEventSynchronize(c->ev_check[0]));
         nact = 0;
+        BatchSel regather{};   // pairs that continue without stored constants
+        regather.ubit = ubit;  // u^0: the set the fused pass read
         for (int b = 0; b < n; ++b) {
+          const bool stored = wp == 0 || !stopped_first[b] || !c->batch_store_pred;
           nit[b] = 2;
           ubit.flip(b);
           pbit.flip(b);
@@ -1676,13 +1693,43 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           ++checks[b];
           act[b] = err[b] > scaledEps && nit[b] < prm.iterations;
           nact += act[b];
+          stopped_first[b] = !act[b];
+          if (act[b] && !stored) regather.idx[regather.n++] = (uint8_t)b;
         }
+        if (regather.n > 0) {   // a wrong guess: gather the constants (k_warp_ring's body)
+          BatchRing br{};
+          br.wa.W = lw;
+          br.wa.H = lh;
+          br.wa.P = P;
+          br.wa.bands = (lw + 63) / 64;
+          br.wa.seg_rows = roll_segment(br.wa.bands * regather.n, lh, 6, c->warp_ring_slots);
+          br.wa.waves = br.wa.bands * ((lh + br.wa.seg_rows - 1) / br.wa.seg_rows);
+          br.I0 = c->bI0s[s];
+          br.I1 = c->bI1s[s];
+          for (int k = 0; k < 2; ++k)
+            for (int j = 0; j < 2; ++j) br.U[k][j] = c->bU[k][j];
+          for (int j = 0; j < 3; ++j) br.C[j] = c->bC[j];
+          br.ips = c->bips[s];
+          br.ps = ps;
+          br.sel = regather;
+          const size_t tkr = prof_begin(c, st);
+#define KB_RING(FM) \
+  hipLaunchKernelGGL((kb_warp_ring<6, 2, FM>), dim3(br.wa.waves, regather.n), dim3(128), 0, st, br);
+          MATH_SWITCH(math, KB_RING)
+#undef KB_RING
+          prof_end(c, st, tkr, 1, (double)regather.n * lw * lh * 40.0,
+                   (double)regather.n * lw * lh * 28.0);
+          for (int j = 0; j < regather.n; ++j) ++regathers[regather.idx[j]];
+        }
+      } else {
+        for (int b = 0; b < n; ++b) stopped_first[b] = 0;
       }
       while (nact > 0) {
-        // each active pair's pass (the single-pair rule), the batch runs the shortest
-        int K = kTbMax;
+        // each active pair's pass (the single-pair rule): k iterations up to and including
+        // its next check, at most kTbMax
         std::vector<int> kb(n, 0);
         std::vector<char> ends(n, 0);
+        int kmin = kTbMax;
         for (int b = 0; b < n; ++b) {
           if (!act[b]) continue;
           int k = 0;
@@ -1697,102 +1744,121 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
             ps_ -= scaledEps;
           }
           kb[b] = k;
-          K = std::min(K, k);
+          kmin = std::min(kmin, k);
         }
-        BatchSel sel{};
-        BatchSel chk{};
-        for (int b = 0; b < n; ++b) {
-          if (!act[b]) continue;
-          sel.idx[sel.n++] = (uint8_t)b;
-          if (ends[b] && kb[b] == K) {
-            sel.cerr.set(b);
-            chk.idx[chk.n++] = (uint8_t)b;
+        // r4: pairs grouped by their pass length, one launch per group, so every pair runs
+        // its whole pass.  TVL1_BATCH_GROUP=0 keeps r3's lock step: one launch of
+        // the shortest pass any active pair allows, the others split theirs.
+        if (!c->batch_group)
+          for (int b = 0; b < n; ++b)
+            if (act[b] && kb[b] > kmin) {
+              kb[b] = kmin;
+              ends[b] = 0;
+            }
+        int ngroups = 0;
+        for (int K = 1; K <= kTbMax; ++K) {
+          BatchSel sel{};
+          BatchSel chk{};
+          for (int b = 0; b < n; ++b) {
+            if (!act[b] || kb[b] != K) continue;
+            sel.idx[sel.n++] = (uint8_t)b;
+            if (ends[b]) {
+              sel.cerr.set(b);
+              chk.idx[chk.n++] = (uint8_t)b;
+            }
           }
-        }
-        sel.ubit = ubit;
-        sel.pbit = pbit;
-        sel.pzero = pzero;
-        int blocks;   // residual partials per pair
-        {   // wavefront pipelines: 128-px bands down the whole level, one per wave
-          BatchRoll br{};
-          br.ra.b = batch_bufs;
-          br.ra.it = it;
-          const int halo = (K + 1) / 2 * 2;   // roll_halo<K, 2>
-          br.ra.bands = (lw + 128 - 2 * halo - 1) / (128 - 2 * halo);
-          // segments sized so the batch's wavefronts fill whole rounds of resident slots
-          br.ra.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                           : roll_segment(br.ra.bands * sel.n, lh, K,
-                                                          c->roll_slots[K][0][2]);
-          br.ra.waves = br.ra.bands * ((lh + br.ra.seg_rows - 1) / br.ra.seg_rows);
-          blocks = br.ra.waves;
-          if (blocks > c->bnblk)
-            return set_err(c, TVL1_EHIP, "internal: %d waves > batch partials %d", blocks, c->bnblk);
-          for (int k = 0; k < 2; ++k)
-            for (int j = 0; j < 2; ++j) br.U[k][j] = c->bU[k][j];
-          for (int k = 0; k < 2; ++k)
-            for (int j = 0; j < 4; ++j) br.Pp[k][j] = c->bP[k][j];
-          for (int j = 0; j < 3; ++j) br.C[j] = c->bC[j];
-          br.ps = ps;
-          br.partials = c->bpartials;
-          br.nblk = blocks;
-          br.sel = sel;
-          const dim3 grid((br.ra.waves + 3) / 4, sel.n);
-          const size_t tkp = prof_begin(c, st);
+          if (sel.n == 0) continue;
+          ++ngroups;
+          sel.ubit = ubit;
+          sel.pbit = pbit;
+          sel.pzero = pzero;
+          int blocks;   // residual partials per pair (pair stride c->bnblk)
+          {   // wavefront pipelines: 128-px bands down the whole level, one per wave
+            BatchRoll br{};
+            br.ra.b = batch_bufs;
+            br.ra.it = it;
+            const int halo = (K + 1) / 2 * 2;   // roll_halo<K, 2>
+            br.ra.bands = (lw + 128 - 2 * halo - 1) / (128 - 2 * halo);
+            // segments sized so the launch's wavefronts fill whole rounds of resident slots
+            br.ra.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
+                                             : roll_segment(br.ra.bands * sel.n, lh, K,
+                                                            c->roll_slots[K][0][2]);
+            br.ra.waves = br.ra.bands * ((lh + br.ra.seg_rows - 1) / br.ra.seg_rows);
+            blocks = br.ra.waves;
+            if (blocks > c->bnblk)
+              return set_err(c, TVL1_EHIP, "internal: %d waves > batch partials %d", blocks, c->bnblk);
+            for (int k = 0; k < 2; ++k)
+              for (int j = 0; j < 2; ++j) br.U[k][j] = c->bU[k][j];
+            for (int k = 0; k < 2; ++k)
+              for (int j = 0; j < 4; ++j) br.Pp[k][j] = c->bP[k][j];
+            for (int j = 0; j < 3; ++j) br.C[j] = c->bC[j];
+            br.ps = ps;
+            br.partials = c->bpartials;
+            br.nblk = c->bnblk;
+            br.sel = sel;
+            const dim3 grid((br.ra.waves + 3) / 4, sel.n);
+            const size_t tkp = prof_begin(c, st);
 #define KB_ROLL_M(FM) hipLaunchKernelGGL((kb_iterate_roll<KK, 2, FM>), grid, dim3(256), 0, st, br);
 #define KB_ROLL(K_)                 \
   {                                 \
     constexpr int KK = K_;          \
     MATH_SWITCH(math, KB_ROLL_M)    \
   }
-          switch (K) {
-            case 1: KB_ROLL(1) break;
-            case 2: KB_ROLL(2) break;
-            case 3: KB_ROLL(3) break;
-            default: KB_ROLL(4) break;
-          }
+            switch (K) {
+              case 1: KB_ROLL(1) break;
+              case 2: KB_ROLL(2) break;
+              case 3: KB_ROLL(3) break;
+              default: KB_ROLL(4) break;
+            }
 #undef KB_ROLL
 #undef KB_ROLL_M
-          if (tkp) {   // k_iterate_roll's accounting (PX = 2 bands) per pair of the launch
-            const int seg = br.ra.seg_rows, segs = (lh + seg - 1) / seg;
-            double rows = 0.0;
-            for (int sg = 0; sg < segs; ++sg) {
-              const int ys = sg * seg, ye = std::min(ys + seg, lh);
-              rows += std::min(ye - 1 + K, lh - 1) - std::max(ys - K, 0) + 1;
+            if (tkp) {   // k_iterate_roll's accounting (PX = 2 bands) per pair of the launch
+              const int seg = br.ra.seg_rows, segs = (lh + seg - 1) / seg;
+              double rows = 0.0;
+              for (int sg = 0; sg < segs; ++sg) {
+                const int ys = sg * seg, ye = std::min(ys + seg, lh);
+                rows += std::min(ye - 1 + K, lh - 1) - std::max(ys - K, 0) + 1;
+              }
+              const double Nl = (double)lw * lh;
+              int nz = 0;
+              for (int j = 0; j < sel.n; ++j) nz += pzero.test(sel.idx[j]) ? 1 : 0;
+              const double band_bytes = (double)br.ra.bands * 128 * rows * 4.0;
+              const double hbm = band_bytes * ((double)sel.n * 5 + (double)(sel.n - nz) * 4) +
+                                 (double)sel.n * Nl * 4.0 * 6.0;
+              prof_end(c, st, tkp, 0, (double)sel.n * Nl * 64.0 * K, hbm);
             }
-            const double Nl = (double)lw * lh;
-            int nz = 0;
-            for (int j = 0; j < sel.n; ++j) nz += pzero.test(sel.idx[j]) ? 1 : 0;
-            const double band_bytes = (double)br.ra.bands * 128 * rows * 4.0;
-            const double hbm = band_bytes * ((double)sel.n * 5 + (double)(sel.n - nz) * 4) +
-                               (double)sel.n * Nl * 4.0 * 6.0;
-            prof_end(c, st, tkp, 0, (double)sel.n * Nl * 64.0 * K, hbm);
           }
+          if (chk.n > 0)
+            hipLaunchKernelGGL(kb_reduce, dim3(chk.n), dim3(kBlock), 0, st, c->bpartials,
+                               (size_t)c->bnblk, blocks, chk, c->pinned_dev + 8);
         }
-        for (int j = 0; j < sel.n; ++j) {
-          const int b = sel.idx[j];
+        (void)ngroups;
+        bool any_check = false;
+        for (int b = 0; b < n; ++b) {
+          if (!act[b]) continue;
+          const int K = kb[b];
           for (int i = 0; i < K; ++i)
-            if (!(sel.cerr.test(b) && i == K - 1)) prev[b] -= scaledEps;
+            if (!(ends[b] && i == K - 1)) prev[b] -= scaledEps;
           nit[b] += K;
           ubit.flip(b);
           pbit.flip(b);
           pzero.clear(b);
           err[b] = DBL_MAX;
+          any_check = any_check || ends[b];
         }
-        if (chk.n > 0) {
-          hipLaunchKernelGGL(kb_reduce, dim3(chk.n), dim3(kBlock), 0, st, c->bpartials, blocks,
-                             chk, c->pinned_dev + 8);
+        if (any_check) {
           HIP_TRY(c, hipEventRecord(c->ev_check[0], st));
           HIP_TRY(c, hipEventSynchronize(c->ev_check[0]));
-          for (int j = 0; j < chk.n; ++j) {
-            const int b = chk.idx[j];
+          for (int b = 0; b < n; ++b) {
+            if (!act[b] || !ends[b]) continue;
             err[b] = c->pinned[8 + b];
             prev[b] = err[b];
             ++checks[b];
           }
         }
         nact = 0;
-        for (int j = 0; j < sel.n; ++j) {
-          const int b = sel.idx[j];
+        for (int b = 0; b < n; ++b) {
+          if (!act[b]) continue;
           act[b] = err[b] > scaledEps && nit[b] < prm.iterations;
           nact += act[b];
         }
@@ -1857,7 +1923,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
       }
       sb.iterations_total = tot;
       sb.checks_total = checks[b];
-      sb.speculation_misses = 0;
+      sb.speculation_misses = regathers[b];   // constants not stored, then needed (re-gathered)
       sb.algorithmic_bytes = survey_bytes(g, prm.warps, li);
       for (int k = 0; k < 4; ++k) {
         sb.kernel_ms[k] = 0.0;
@@ -2172,6 +2238,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_SPEC_TRACE")) c->spec_trace = atoi(m);
   if (const char *m = getenv("TVL1_FUSE_MIN")) c->fuse_min = atol(m);
   if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_BATCH_STORE")) c->batch_store_pred = atoi(m) == 0;
+  if (const char *m = getenv("TVL1_BATCH_GROUP")) c->batch_group = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);

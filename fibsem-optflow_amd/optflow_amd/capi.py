@@ -204,6 +204,13 @@ def load_engine() -> C.CDLL:
                                      C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, C.c_int32,
                                      C.c_void_p]
     lib.tvl1_postprocess.restype = C.c_int
+    lib.tvl1_postprocess_batch.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                           C.c_size_t, C.c_size_t, C.c_void_p, C.c_size_t,
+                                           C.c_size_t, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
+    lib.tvl1_postprocess_batch.restype = C.c_int
+    lib.tvl1_gather_flow.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                     C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.tvl1_gather_flow.restype = C.c_int
     lib.tvl1_stream.argtypes = [C.c_void_p]
     lib.tvl1_stream.restype = C.c_void_p
     lib.tvl1_set_profiling.argtypes = [C.c_void_p, C.c_int32]
@@ -380,6 +387,23 @@ class Engine:
         self._check(self.lib.tvl1_warp_affine_u8(self.ctx, C.c_void_p(src), sp, sw, sh,
                                                  C.c_void_p(dst), dp, dw, dh, a, None),
                     "tvl1_warp_affine_u8")
+
+    def postprocess_batch(self, n: int, du: int, dv: int, fpitch: int, fstride: int, dI1: int,
+                          pitch1: int, stride1: int, w: int, h: int, mode: int, stream: int = 0):
+        """tvl1_postprocess_batch: solve_wrapper's map grid + I1 <= 1 mask on n pairs."""
+        self._check(self.lib.tvl1_postprocess_batch(self.ctx, n, du, dv, fpitch, fstride, dI1,
+                                                    pitch1, stride1, w, h, mode, stream),
+                    "tvl1_postprocess_batch")
+
+    def gather_flow(self, du: int, dv: int, offsets, stream: int = 0):
+        """tvl1_gather_flow: (u[off], v[off]) for element offsets into device planes."""
+        off = np.ascontiguousarray(offsets, np.int64)
+        ou = np.zeros(len(off), np.float32)
+        ov = np.zeros(len(off), np.float32)
+        self._check(self.lib.tvl1_gather_flow(self.ctx, du, dv, off.ctypes.data, len(off),
+                                              ou.ctypes.data, ov.ctypes.data, stream),
+                    "tvl1_gather_flow")
+        return ou, ov
 
     def close(self):
         if self.ctx:

@@ -105,7 +105,9 @@ typedef struct tvl1_stats {
   int32_t *warp_iterations;
   int32_t warp_iterations_capacity;         /* number of int32 slots in warp_iterations */
   int32_t speculation_misses;               /* tvl1_calc: launches enqueued behind a residual check
-                                             * that ran empty (a wrong guess); 0 otherwise */
+                                             * that ran empty (a wrong guess);
+                                             * tvl1_calc_batch: warps whose constants were not
+                                             * stored but needed (re-gathered) */
   /* Filled only when profiling is enabled (tvl1_set_profiling): HIP-event time,
    * launch count and algorithmic bytes per kernel class, on the solve's stream.
    * Class 0 = fused primal-dual iteration (K6+K8+K7 partials), 1 = warpBackward

@@ -54,14 +54,19 @@ def pairs(n, w, h, seed):
     (1, 97, 40, dict(nscales=3, warps=3)),
     (5, 200, 60, dict(nscales=4, warps=3, epsilon=0.0, iterations=7)),   # fixed work
 ])
-@pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0", "TVL1_WI_NC=1"])
+@pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0", "TVL1_WI_NC=1", "TVL1_BATCH_STORE=1",
+                                 "TVL1_BATCH_GROUP=0"])
 @pytest.mark.parametrize("math", [0, 2])
 def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw, math):
     """kb_warp_iter (fused warp + first pass; 2 consumer wavefronts, or 1 with
-    TVL1_WI_NC=1), kb_warp_ring, kb_iterate_roll<K, 2>: IEEE and fma mode, each
-    bit-identical to the oracle in that mode."""
+    TVL1_WI_NC=1; constants stored on demand, or always with TVL1_BATCH_STORE=1), passes grouped
+    by their length (or r3's lock step with TVL1_BATCH_GROUP=0),
+    kb_warp_ring, kb_iterate_roll<K, 2>: IEEE and fma mode, each bit-identical to the oracle
+    in that mode."""
     monkeypatch.delenv("TVL1_BATCH_FUSE", raising=False)
     monkeypatch.delenv("TVL1_WI_NC", raising=False)
+    monkeypatch.delenv("TVL1_BATCH_STORE", raising=False)
+    monkeypatch.delenv("TVL1_BATCH_GROUP", raising=False)
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
     p = capi.make_params(fast_math=math, **kw)
@@ -284,3 +289,23 @@ def test_batch_profiling_classes_and_same_bits(built):
         assert st1[b]["kernel_launches"][0] > 0 and st1[b]["kernel_ms"][0] > 0
         assert st1[b]["kernel_hbm_bytes"][0] > 0 and st1[b]["kernel_bytes"][0] > 0
         assert st1[b]["kernel_ms"] == st1[0]["kernel_ms"]   # one chunk: shared launches
+
+
+def test_batch_constants_on_demand_regather(built, monkeypatch):
+    """Production strips (3072x100 of a device stack, nscales 10, warps 5): kb_warp_iter stores
+    the warp constants only for pairs predicted to continue past the first check; a pair that
+    continues anyway is re-gathered (kb_warp_ring) -- counted in speculation_misses.  The path
+    must run here and every pair stay bit-identical to the oracle."""
+    from optflow_amd.synth_device import DeviceStack
+    monkeypatch.delenv("TVL1_BATCH_STORE", raising=False)
+    n, w, h = 12, 3072, 100
+    gen = DeviceStack(w, h, torch.device("cuda", 0), seed=0x5EED)
+    s0 = gen.slice(0).cpu().numpy()
+    I0s = np.stack([s0] * n)
+    I1s = np.stack([gen.slice(z + 1).cpu().numpy() for z in range(n)])
+    p = capi.make_params(nscales=10, warps=5)
+    eng = capi.Engine(p)
+    u, v, st = run_batch(eng, I0s, I1s)
+    eng.close()
+    assert sum(s["speculation_misses"] for s in st) > 0
+    check_against_oracle(p, I0s, I1s, u, v, st)

@@ -197,3 +197,32 @@ def test_batch_relaid_across_streams_without_sync(built):
             np.testing.assert_array_equal(jb["st"][b]["warp_iters"], wr)
             assert bits_equal(u[b], ur) and bits_equal(v[b], vr), (jb["w"], b)
     eng.close()
+
+
+def test_postprocess_batch_and_gather_flow(built):
+    """ABI 8: tvl1_postprocess_batch equals tvl1_postprocess per pair (every mode, frame1
+    masks with zeros), and tvl1_gather_flow returns exactly the addressed values."""
+    dev = torch.device("cuda", 0)
+    n, w, h = 5, 70, 33
+    rng = np.random.default_rng(9)
+    u0 = torch.from_numpy(rng.standard_normal((n, h, w)).astype(np.float32)).to(dev)
+    v0 = torch.from_numpy(rng.standard_normal((n, h, w)).astype(np.float32)).to(dev)
+    I1 = rng.integers(0, 4, (n, h, w), dtype=np.uint8)
+    dI1 = torch.from_numpy(I1).to(dev)
+    eng = capi.Engine(capi.make_params())
+    for mode in (0, 1, 2):
+        ub, vb = u0.clone(), v0.clone()
+        eng.postprocess_batch(n, ub.data_ptr(), vb.data_ptr(), 4 * w, 4 * w * h, dI1.data_ptr(),
+                              w, w * h, w, h, mode)
+        for b in range(n):
+            us, vs = u0[b].clone(), v0[b].clone()
+            eng.lib.tvl1_postprocess(eng.ctx, us.data_ptr(), vs.data_ptr(), 4 * w,
+                                     dI1[b].data_ptr(), w, w, h, mode, None)
+            torch.cuda.synchronize()
+            assert torch.equal(ub[b].view(torch.int32), us.view(torch.int32)), (mode, b)
+            assert torch.equal(vb[b].view(torch.int32), vs.view(torch.int32)), (mode, b)
+    off = rng.integers(0, n * w * h, 1000)
+    gu, gv = eng.gather_flow(u0.data_ptr(), v0.data_ptr(), off)
+    np.testing.assert_array_equal(gu, u0.flatten().cpu().numpy()[off])
+    np.testing.assert_array_equal(gv, v0.flatten().cpu().numpy()[off])
+    eng.close()

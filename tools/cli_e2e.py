@@ -1,8 +1,15 @@
-"""End-to-end throughput of the optflow CLI on a PNG stack ("a separate run
-includes PNG decode"; 8(f) N2): PNG decode + pre-scale + upload + solve + point-match
-output, timed around the whole CLI process.
+"""End-to-end throughput of the optflow CLI on a slice stack ("a separate run
+includes PNG decode"; 8(f) N2): decode + pre-scale + upload + solve + point-match output,
+timed around the whole CLI process.
 
     python tools/cli_e2e.py [--slices 17] [--width 6144 --height 4096] [--out DIR]
+                            [--format png|tiff|tiff_deflate] [--jobs c2,strips]
+                            [--strip-batch 256,0] [--no-single-thread]
+
+--format tiff writes uncompressed one-strip TIFFs (the strip jobs then read only the ROIs'
+rows of each slice), tiff_deflate deflate TIFFs of 64-row strips (only the strips holding
+them).  --strip-batch runs the strip job once per value of the CLI's build-only
+"strip_batch" key (0 = one tvl1_calc per strip, the r3 path).
 
 Writes the slices once (device-generated synthetic texture, PNG), then runs two job
 configurations, each with the decode-ahead pool and with one decode thread:
@@ -28,17 +35,29 @@ sys.path.insert(0, str(ROOT / "fibsem-optflow_amd"))
 OPTFLOW = ROOT / "fibsem-optflow_amd" / "bin" / "optflow"
 
 
-def make_stack(d: Path, Z: int, W: int, H: int):
+def make_stack(d: Path, Z: int, W: int, H: int, fmt: str = "png"):
     import torch
     from PIL import Image
 
     from optflow_amd.synth_device import DeviceStack
     st = DeviceStack(W, H, torch.device("cuda", 0), seed=0x5EED)
-    slices = [st.slice(z).cpu().numpy() for z in range(Z)]
-    paths = [d / f"s{z:04d}.png" for z in range(Z)]
-    with ThreadPoolExecutor(8) as ex:
-        list(ex.map(lambda a: Image.fromarray(a[0]).save(a[1], compress_level=6),
-                    zip(slices, paths)))
+    ext = "png" if fmt == "png" else "tif"
+    paths = [d / f"s{z:04d}.{ext}" for z in range(Z)]
+
+    def save(z):
+        a = st_slices[z]
+        if fmt == "png":
+            Image.fromarray(a).save(paths[z], compress_level=6)
+        elif fmt == "tiff":
+            Image.fromarray(a).save(paths[z])   # uncompressed, one strip
+        else:
+            Image.fromarray(a).save(paths[z], compression="tiff_adobe_deflate",
+                                    tiffinfo={278: 64})
+    # generated and written in groups (a 6144x4096 slice is 25 MB of host memory)
+    for g in range(0, Z, 32):
+        st_slices = {z: st.slice(z).cpu().numpy() for z in range(g, min(Z, g + 32))}
+        with ThreadPoolExecutor(8) as ex:
+            list(ex.map(save, st_slices))
     return paths
 
 
@@ -76,23 +95,34 @@ def main():
     ap.add_argument("--height", type=int, default=4096)
     ap.add_argument("--out", default=None)
     ap.add_argument("--ab-pinned", action="store_true")
+    ap.add_argument("--format", choices=("png", "tiff", "tiff_deflate"), default="png")
+    ap.add_argument("--jobs", default="c2,strips")
+    ap.add_argument("--strip-batch", default=None,
+                    help="comma list of strip_batch values for the strip job (default: the CLI's)")
+    ap.add_argument("--no-single-thread", action="store_true",
+                    help="skip the one-decode-thread runs")
     args = ap.parse_args()
     d = Path(args.out or tempfile.mkdtemp(prefix="cli_e2e_"))
     d.mkdir(parents=True, exist_ok=True)
     t0 = time.perf_counter()
-    paths = make_stack(d, args.slices, args.width, args.height)
-    print(json.dumps({"stack": f"{args.slices} x {args.width}x{args.height} PNG",
+    paths = make_stack(d, args.slices, args.width, args.height, args.format)
+    print(json.dumps({"stack": f"{args.slices} x {args.width}x{args.height} {args.format}",
                       "bytes": sum(os.path.getsize(p) for p in paths),
                       "write_s": round(time.perf_counter() - t0, 1)}), flush=True)
     pairs = [{"p": str(paths[z]), "q": str(paths[z + 1]), "output_name": f"z{z}",
               "pId": f"{z}", "qId": f"{z + 1}", "pGroupId": f"{z}.0", "qGroupId": f"{z + 1}.0"}
              for z in range(args.slices - 1)]
     W, H = args.width, args.height
-    jobs = {
-        "c2_full_frame": {"scale": 1, "nscales": 5, "warps": 30,
-                          "rois": {"custom": [0, 0, W, H]}},
-        "production_strips": {"scale": 0.5, "rois": {"top": 100, "bottom": 100}},
-    }
+    jobs = {}
+    if "c2" in args.jobs:
+        jobs["c2_full_frame"] = {"scale": 1, "nscales": 5, "warps": 30,
+                                 "rois": {"custom": [0, 0, W, H]}}
+    if "strips" in args.jobs:
+        for sb in (args.strip_batch.split(",") if args.strip_batch else [None]):
+            key = "production_strips" + (f"_batch{sb}" if sb is not None else "")
+            jobs[key] = {"scale": 0.5, "rois": {"top": 100, "bottom": 100}}
+            if sb is not None:
+                jobs[key]["strip_batch"] = int(sb)
     if args.ab_pinned:
         for name, extra in jobs.items():
             for rep, pinned in enumerate((1, 0, 1, 0)):
@@ -107,7 +137,7 @@ def main():
                                   "steady_pairs_per_s": steady and round(steady, 2)}), flush=True)
         return
     for name, extra in jobs.items():
-        for threads in (None, 1):
+        for threads in ((None,) if args.no_single_thread else (None, 1)):
             cfg = {"output_dir": str(d / name), "output_type": "random_points",
                    "matches_file": str(d / name / "pm"), "images": pairs, **extra}
             if threads:
