@@ -929,6 +929,7 @@ static int from_file(Value &args, bool plan_only) {
   // the pairs the per-pair workers solve (all of them unless strip batching takes some)
   std::vector<size_t> todo;
   size_t m = 0;
+  std::vector<char> batch_ok(n, 0);     // the pair goes to the strip batch workers
   size_t chunk = 1;
   std::atomic<int> hard_error{0};
 
@@ -1080,6 +1081,7 @@ static int from_file(Value &args, bool plan_only) {
           pl["rois"] = rois;
           pl["output_type"] = output_type_of(im, args);
           pl["features"] = resolve_features(im, args);
+          pl["strip_batch"] = (bool)batch_ok[i];   // solved in a tvl1_calc_batch chunk
           const tvl1_params tp = generate_TV_args(im, args);
           pl["tv"]["tau"] = tp.tau;
           pl["tv"]["lambda"] = tp.lambda;
@@ -1500,7 +1502,7 @@ static int from_file(Value &args, bool plan_only) {
   // features, per-image ROIs / scales / TV parameters go the per-pair way.
   const int strip_batch = std::min(256, std::max(0, args.get("strip_batch", 256).asInt()));
   const std::string gotype = output_type_of(Value(), args);
-  const bool batching = !plan_only && strip_job && strip_batch > 1 && !resolve_features(Value(), args) &&
+  const bool batching = strip_job && strip_batch > 1 && !resolve_features(Value(), args) &&
                         (gotype == "map" || gotype == "flow" || gotype == "random_points");
   if (batching) {
     roi_keys = args["rois"].memberNames();
@@ -1513,6 +1515,12 @@ static int from_file(Value &args, bool plan_only) {
         ok = ok && std::find_if(std::begin(kProd), std::end(kProd), [&](const char *x) { return k == x; }) !=
                        std::end(kProd);
       (ok ? batched : todo).push_back(i);
+      batch_ok[i] = ok;
+    }
+    if (plan_only) {   // --plan reports the split; the per-pair worker resolves every pair
+      batched.clear();
+      todo.clear();
+      for (size_t i = 0; i < n; ++i) todo.push_back(i);
     }
   } else {
     for (size_t i = 0; i < n; ++i) todo.push_back(i);

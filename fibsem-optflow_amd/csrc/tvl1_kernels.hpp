@@ -105,6 +105,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *p, uns
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)bytes, 0x00020000);
 }
 constexpr unsigned kOOB = 0x7ffffff0u;   // byte offset beyond every plane: store dropped
+#ifndef TVL1_TB4_P2P   // k_iterate_tb4: neighbour flags instead of block barriers (r4)
+#define TVL1_TB4_P2P 0
+#endif
 #ifndef TVL1_WI_S2F   // k_warp_iter / kb_warp_iter: stage 2 fills the window ring (r4)
 #define TVL1_WI_S2F 1
 #endif
@@ -1597,9 +1600,130 @@ __device__ __forceinline__ void tb4_iterations(Row<false, 2> (&r)[NR], const int
   }
 }
 
+// The same iterations with point-to-point synchronisation instead of two block barriers per
+// iteration (r4; TVL1_TB4_P2P).  A wavefront holds row groups 2w (lanes
+// 0-31) and 2w + 1 (lanes 32-63).  The boundary between its two groups is crossed with a lane
+// swap (ds_bpermute, no barrier); the boundaries to the wavefronts above and below go through
+// LDS slots double-buffered by iteration parity, each published by a release store of the
+// iteration count to a per-wave LDS flag that the neighbour polls with an acquire load.  A
+// wave therefore waits only for its two neighbours, never for the slowest of the block's 8.
+// No cycle: at iteration n a wave publishes p (the last row of group 2w + 1) before it waits
+// for wave w - 1's p, and publishes u (the first row of group 2w) before it waits for wave
+// w + 1's u.  A slot of parity n & 1 is rewritten at n + 2 only after the reader published
+// its own iteration n + 1 data, which it does after reading.  Same operands, same bits.
+struct Tb4Xch {
+  float2 p[2][2][kTb4Groups / 2][32];   // [parity][p12, p22][wave][lane]: group 2w + 1's last row
+  float2 u[2][2][kTb4Groups / 2][32];   // [parity][u1, u2][wave][lane]: group 2w's first row
+  int flag_p[kTb4Groups / 2], flag_u[kTb4Groups / 2];
+};
+
+__device__ __forceinline__ void tb4_wait(const int *f, int n) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < n)
+    __builtin_amdgcn_s_sleep(1);
+}
+
+__device__ __forceinline__ float2 swap32(float2 v) {   // lane l <-> lane l ^ 32
+  return make_float2(__shfl_xor(v.x, 32), __shfl_xor(v.y, 32));
+}
+
+template <int FM, int NR, bool IN>
+__device__ __forceinline__ void tb4_iterations_p2p(Row<false, 2> (&r)[NR], const int (&Y)[NR],
+                                                   const bool (&out_ok)[NR], Tb4Xch &x,
+                                                   const IterArgs &a, int K, int X, int q, int c4,
+                                                   double &acc) {
+  constexpr int PX = 2, NW = kTb4Groups / 2;
+  const int w = q >> 1;
+  const bool hi = q & 1;
+  const int lane = threadIdx.x & 63;
+  for (int it = 0; it < K; ++it) {
+    const bool last = it == K - 1;
+    const int par = it & 1;
+    // ---- estimateU: p^{n-1} at y-1 for each group's first row
+    const float2 pl12 = pack(r[NR - 1].p12), pl22 = pack(r[NR - 1].p22);
+    if (hi && w < NW - 1) {
+      x.p[par][0][w][c4] = pl12;
+      x.p[par][1][w][c4] = pl22;
+    }
+    if (w < NW - 1 && lane == 32)
+      __hip_atomic_store(&x.flag_p[w], it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const float2 s12 = swap32(pl12), s22 = swap32(pl22);
+    float up12[PX], up22[PX], zero3[PX];
+    zerov<PX>(zero3);
+    if (w > 0) tb4_wait(&x.flag_p[w - 1], it + 1);
+    if (hi) {   // group 2w + 1 <- group 2w (this wave's lanes 0-31)
+      unpack(up12, s12);
+      unpack(up22, s22);
+    } else if (w > 0) {   // group 2w <- group 2w - 1 (wave w - 1's lanes 32-63)
+      unpack(up12, x.p[par][0][w - 1][c4]);
+      unpack(up22, x.p[par][1][w - 1][c4]);
+    } else {   // region row 0: its own row (k_iterate_tb's clamp)
+#pragma unroll
+      for (int k = 0; k < PX; ++k) up12[k] = r[0].p12[k], up22[k] = r[0].p22[k];
+    }
+#pragma unroll
+    for (int g = 0; g < NR; ++g) {
+      float n1[PX], n2[PX], n3[PX];
+      if (g == 0)
+        estimate_u<false, PX, FM>(r[0], up12, up22, zero3, IN ? 1 : X, IN ? 1 : Y[0], a, n1, n2, n3);
+      else
+        estimate_u<false, PX, FM>(r[g], r[g - 1].p12, r[g - 1].p22, zero3, IN ? 1 : X, IN ? 1 : Y[g], a,
+                                  n1, n2, n3);
+      if (last && a.calc_err && out_ok[g]) {
+#pragma unroll
+        for (int k = 0; k < PX; ++k)
+          if (X + k < a.W) acc += (double)residual_px<FM>(r[g].u1[k] - n1[k], r[g].u2[k] - n2[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < PX; ++k) {
+        r[g].u1[k] = n1[k];
+        r[g].u2[k] = n2[k];
+      }
+    }
+    // ---- estimateDualVariables: u^n at y+1 for each group's last row
+    const float2 uf1 = pack(r[0].u1), uf2 = pack(r[0].u2);
+    if (!hi && w > 0) {
+      x.u[par][0][w][c4] = uf1;
+      x.u[par][1][w][c4] = uf2;
+    }
+    if (w > 0 && lane == 0)
+      __hip_atomic_store(&x.flag_u[w], it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const float2 t1 = swap32(uf1), t2 = swap32(uf2);
+    float d1[PX], d2[PX];
+    if (w < NW - 1) tb4_wait(&x.flag_u[w + 1], it + 1);
+    if (!hi) {   // group 2w <- group 2w + 1 (this wave's lanes 32-63)
+      unpack(d1, t1);
+      unpack(d2, t2);
+    } else if (w < NW - 1) {   // group 2w + 1 <- group 2w + 2 (wave w + 1's lanes 0-31)
+      unpack(d1, x.u[par][0][w + 1][c4]);
+      unpack(d2, x.u[par][1][w + 1][c4]);
+    } else {   // region bottom row: its own row
+#pragma unroll
+      for (int k = 0; k < PX; ++k) d1[k] = r[NR - 1].u1[k], d2[k] = r[NR - 1].u2[k];
+    }
+#pragma unroll
+    for (int g = 0; g < NR; ++g) {
+      const bool has_down = IN || Y[g] + 1 < a.H;
+      const int xd = IN ? 0 : X, wd = IN ? 64 : a.W;
+      float q11[PX], q12[PX], q21[PX], q22[PX];
+      if (g < NR - 1) {
+        dual_component<PX, false, FM>(r[g].u1, r[g + 1].u1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12);
+        dual_component<PX, false, FM>(r[g].u2, r[g + 1].u2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22);
+      } else {
+        dual_component<PX, false, FM>(r[g].u1, d1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12);
+        dual_component<PX, false, FM>(r[g].u2, d2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22);
+      }
+#pragma unroll
+      for (int k = 0; k < PX; ++k) {
+        r[g].p11[k] = q11[k]; r[g].p12[k] = q12[k];
+        r[g].p21[k] = q21[k]; r[g].p22[k] = q22[k];
+      }
+    }
+  }
+}
+
 template <int FM, int NR, bool IN>
 __device__ __forceinline__ void tb4_body(const TBArgs &t, float2 (&lds)[4][kTb4Groups][32], int xr0,
-                                         int yr0) {
+                                         int yr0, Tb4Xch *xch = nullptr) {
   constexpr int PX = 2, LPR = 32, NGR = kTb4Groups, kTb4Rows = NR * NGR;
   constexpr int HALO = 4 / PX;   // lanes of the 4-px x halo
   const IterArgs &a = t.it;
@@ -1622,7 +1746,10 @@ __device__ __forceinline__ void tb4_body(const TBArgs &t, float2 (&lds)[4][kTb4G
                 Y[g] < a.H && X < a.W;
   }
   double acc = 0.0;
-  tb4_iterations<FM, NR, IN>(r, Y, out_ok, lds, a, K, X, q, c4, acc);
+  if (xch)
+    tb4_iterations_p2p<FM, NR, IN>(r, Y, out_ok, *xch, a, K, X, q, c4, acc);
+  else
+    tb4_iterations<FM, NR, IN>(r, Y, out_ok, lds, a, K, X, q, c4, acc);
 #pragma unroll
   for (int g = 0; g < NR; ++g) {
     if (out_ok[g]) {
@@ -1649,19 +1776,27 @@ __device__ __forceinline__ void tb4_body(const TBArgs &t, float2 (&lds)[4][kTb4G
   }
 }
 
-template <int FM, int NR = kTb4RowsPerThread>
+template <int FM, int NR = kTb4RowsPerThread, bool P2P = TVL1_TB4_P2P>
 __global__ __launch_bounds__(32 * kTb4Groups, 4) void k_iterate_tb4(TBArgs t) {
-  __shared__ float2 lds[4][kTb4Groups][32];   // [p12 last, p22 last, u1 first, u2 first][group][lane]
+  // !P2P: [p12 last, p22 last, u1 first, u2 first][group][lane]; P2P: the Tb4Xch slots + flags
+  constexpr size_t kBar = sizeof(float2) * 4 * kTb4Groups * 32;
+  __shared__ __attribute__((aligned(16))) char smem[P2P ? sizeof(Tb4Xch) : kBar];
   if (gated_off(t.it.gate, t.it.gate_seq)) return;   // whole grid
+  Tb4Xch *X = P2P ? reinterpret_cast<Tb4Xch *>(smem) : nullptr;
+  if (P2P) {   // flags start at 0 (every wave of the block passes this barrier once)
+    if (threadIdx.x < kTb4Groups / 2) X->flag_p[threadIdx.x] = X->flag_u[threadIdx.x] = 0;
+    __syncthreads();
+  }
   int bx, by;
   tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
   const int xr0 = bx * 56 - 4;
   const int yr0 = by * t.out_h - t.niter;
+  auto &L = *reinterpret_cast<float2 (*)[4][kTb4Groups][32]>(smem);   // !P2P only
   // wave-uniform: the whole region inside the image with a 1-px margin (tb4_iterations' IN)
   if (xr0 >= 1 && yr0 >= 1 && xr0 + 64 < t.it.W && yr0 + NR * kTb4Groups < t.it.H)
-    tb4_body<FM, NR, true>(t, lds, xr0, yr0);
+    tb4_body<FM, NR, true>(t, L, xr0, yr0, X);
   else
-    tb4_body<FM, NR, false>(t, lds, xr0, yr0);
+    tb4_body<FM, NR, false>(t, L, xr0, yr0, X);
 }
 
 // ---------------------------------------------------------------- K6+K8 wavefront pipeline

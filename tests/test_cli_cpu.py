@@ -387,3 +387,20 @@ def test_prescale_generic_matches_restatement(tmp_path, built, scale, W, H):
     rng = np.random.default_rng(W * 7 + H)
     a = rng.integers(0, 256, (H, W), dtype=np.uint8)
     assert np.array_equal(decode_scaled(tmp_path, a, scale), resize_linear_ref(a, scale))
+
+
+def test_plan_reports_strip_batching(tmp_path, slices):
+    """Strip jobs of the production shape (gen_cross_file_list.py: global top / bottom ROIs,
+    per-image keys only p, q, the ids and output_name) go to the batched path; a pair with its
+    own keys, features, or a job with other ROIs / strip_batch 0 does not."""
+    base = {"output_dir": str(tmp_path), "scale": 1, "rois": {"top": 10, "bottom": 12},
+            "output_type": "random_points",
+            "images": [{"p": str(slices[0]), "q": str(slices[1]), "pId": "a", "qId": "b",
+                        "pGroupId": "1.0", "qGroupId": "2.0", "output_name": "ab"},
+                       {"p": str(slices[1]), "q": str(slices[2]), "npoints": 4},
+                       {"p": str(slices[1]), "q": str(slices[2]), "features": 1}]}
+    pl = plan(write_cfg(tmp_path, base))
+    assert [e["strip_batch"] for e in pl] == [True, False, False]
+    for extra in ({"strip_batch": 0}, {"rois": {"custom": [0, 0, 20, 20]}}, {"features": 1}):
+        cfg = dict(base, **extra)
+        assert not any(e["strip_batch"] for e in plan(write_cfg(tmp_path, cfg, name="c2.json")))
