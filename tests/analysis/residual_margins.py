@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""How robust is the iteration schedule to the residual's accumulation?  (DESIGN 2.2,
+"""TEST INFRASTRUCTURE (analysis; runs the oracle, so it lives under tests/).
+How robust is the iteration schedule to the residual's accumulation?  (DESIGN 2.2,
 VERDICT r3 "next" item 3.)
 
 OpenCV 3.4.1's procOneScale decides when a warp stops from cuda::sum of the float diff
@@ -27,7 +28,7 @@ from pathlib import Path
 
 import numpy as np
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "fibsem-optflow_amd")]
 from optflow_amd import capi, synth  # noqa: E402
 from oracle import checker  # noqa: E402

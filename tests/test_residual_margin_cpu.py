@@ -11,7 +11,7 @@ from the reference's.  These tests pin, on the golden fixtures (tests/golden/):
     per-warp iteration counts, and its residuals stay within a factor SAFETY of those
     margins.
 The C2 / C3 / production-strip figures are in profiles/r4/residual_margins.md
-(tools/residual_margins.py)."""
+(tests/analysis/residual_margins.py)."""
 import json
 from pathlib import Path
 

@@ -18,5 +18,5 @@ done | tee $out/ab_strips.txt
 unset TVL1_ENGINE_SO
 bash tools/pmc_stall.sh r4_new > $out/stall_new.log 2>&1 || { echo STALL_FAIL; exit 1; }
 TVL1_ENGINE_SO=ab_head/libtvl1_hip.so bash tools/pmc_stall.sh r4_head > $out/stall_head.log 2>&1 || { echo STALL_FAIL; exit 1; }
-OMP_NUM_THREADS=16 timeout -k 10 500 python -u tools/residual_margins.py --device --out $out/residual_margins > $out/margins.log 2>&1 || { echo MARGINS_FAIL; tail -5 $out/margins.log; exit 1; }
+OMP_NUM_THREADS=16 timeout -k 10 500 python -u tests/analysis/residual_margins.py --device --out $out/residual_margins > $out/margins.log 2>&1 || { echo MARGINS_FAIL; tail -5 $out/margins.log; exit 1; }
 echo ALL_DONE
