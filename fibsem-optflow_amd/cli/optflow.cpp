@@ -1310,7 +1310,7 @@ static int from_file(Value &args, bool plan_only) {
         std::vector<std::vector<float>> dbg_fx(roi_keys.size()), dbg_fy(roi_keys.size());
         auto fail = [&](const std::string &what, tvl1_status st) {
           e = what + (dc.ctx ? std::string(": ") + tvl1_last_error(dc.ctx) : std::string());
-          dc.faulted = device_fault(st) || st == TVL1_OK;
+          dc.faulted = device_fault(st);
           ok = false;
         };
         if (attempt == 0 && inject) fail("injected device fault", TVL1_EHIP);
