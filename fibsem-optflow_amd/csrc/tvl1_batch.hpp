@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64 * NC + 128) void kb_warp_iter(BatchWI bw) {
   }
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves) return;
-  warp_iter_body<M, FM, 128, 0, NC, TVL1_WI_S2F && NC == 2>(w, wid, ring, cring, hring);
+  warp_iter_body<M, FM, 128, 0, NC>(w, wid, ring, cring, hring);
 }
 
 // K6+K8(+K7 partials): one pass of K iterations as a k_iterate_roll<false, K, PX> wavefront

@@ -132,8 +132,6 @@ struct tvl1_ctx {
   size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
   double *bpartials = nullptr;
   int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
-  int batch_segs = 1;                   // TVL1_BATCH_SEGS=0: batched launches' segments by
-                                        // roll_segment (r3) instead of roll_segment_all
   int batch_group = 1;                  // TVL1_BATCH_GROUP=0: r3's lock-step passes (the
                                         // shortest pass any pair allows, for all)
   int batch_store_pred = 1;             // TVL1_BATCH_STORE=1: kb_warp_iter always stores the
@@ -272,28 +270,6 @@ static int roll_segment(int bands, int lh, int k, int slots) {
       best_cost = cost;
       best = seg;
     }
-  }
-  return best;
-}
-
-// The same choice over every segment count (r4, the batched launches): a batch's waves run
-// to several rounds of resident slots, where roll_segment's R <= 4 rounds never try a
-// second segment per band (256 production strips: 6656 one-segment waves over 2048 slots =
-// 3.25 rounds, the 4th a quarter full; two 50-row segments fill 6.5 of 7).
-static int roll_segment_all(int bands, int lh, int k, int slots) {
-  if (slots <= 0) slots = 4096;
-  int best = lh;
-  long best_cost = -1;
-  for (int S = 1;; ++S) {
-    const int seg = std::max(kRollMinSeg, (lh + S - 1) / S);
-    const long waves = (long)bands * ((lh + seg - 1) / seg);
-    const long rounds = (waves + slots - 1) / slots;
-    const long cost = rounds * (seg + 2 * k);
-    if (best_cost < 0 || cost < best_cost) {
-      best_cost = cost;
-      best = seg;
-    }
-    if (seg <= kRollMinSeg) break;
   }
   return best;
 }
@@ -1523,10 +1499,6 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
     if (r != TVL1_OK) return r;
   }
   const size_t ps = c->bps;
-  // segment rows of the batched streaming launches (TVL1_BATCH_SEGS=0: r3's roll_segment)
-  auto bseg = [c](int bands, int lh, int k, int slots) {
-    return c->batch_segs ? roll_segment_all(bands, lh, k, slots) : roll_segment(bands, lh, k, slots);
-  };
   // counted as a solve in progress (single-pair solves speculate and size their launches
   // by this count); the batched launches themselves are sized for every resident slot (the
   // shared share measured neutral here: 2925 / 2901 against 2919 / 2928 strip solves/s,
@@ -1621,7 +1593,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         wi.w.ra.b = batch_bufs;
         wi.w.ra.it = it;
         wi.w.ra.bands = (lw + 123) / 124;
-        wi.w.ra.seg_rows = bseg(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots);
+        wi.w.ra.seg_rows = roll_segment(wi.w.ra.bands * n, lh, 2 + 6, c->witer_slots);
         wi.w.ra.waves = wi.w.ra.bands * ((lh + wi.w.ra.seg_rows - 1) / wi.w.ra.seg_rows);
         if (wi.w.ra.waves > c->bnblk)
           return set_err(c, TVL1_EHIP, "internal: %d blocks > batch partials %d", wi.w.ra.waves, c->bnblk);
@@ -1679,7 +1651,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         br.wa.H = lh;
         br.wa.P = P;
         br.wa.bands = (lw + 63) / 64;
-        br.wa.seg_rows = bseg(br.wa.bands * n, lh, 6, c->warp_ring_slots);
+        br.wa.seg_rows = roll_segment(br.wa.bands * n, lh, 6, c->warp_ring_slots);
         br.wa.waves = br.wa.bands * ((lh + br.wa.seg_rows - 1) / br.wa.seg_rows);
         br.I0 = c->bI0s[s];
         br.I1 = c->bI1s[s];
@@ -1730,7 +1702,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           br.wa.H = lh;
           br.wa.P = P;
           br.wa.bands = (lw + 63) / 64;
-          br.wa.seg_rows = bseg(br.wa.bands * regather.n, lh, 6, c->warp_ring_slots);
+          br.wa.seg_rows = roll_segment(br.wa.bands * regather.n, lh, 6, c->warp_ring_slots);
           br.wa.waves = br.wa.bands * ((lh + br.wa.seg_rows - 1) / br.wa.seg_rows);
           br.I0 = c->bI0s[s];
           br.I1 = c->bI1s[s];
@@ -1809,7 +1781,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
             br.ra.bands = (lw + 128 - 2 * halo - 1) / (128 - 2 * halo);
             // segments sized so the launch's wavefronts fill whole rounds of resident slots
             br.ra.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                             : bseg(br.ra.bands * sel.n, lh, K,
+                                             : roll_segment(br.ra.bands * sel.n, lh, K,
                                                             c->roll_slots[K][0][2]);
             br.ra.waves = br.ra.bands * ((lh + br.ra.seg_rows - 1) / br.ra.seg_rows);
             blocks = br.ra.waves;
@@ -2268,7 +2240,6 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BATCH_STORE")) c->batch_store_pred = atoi(m) == 0;
   if (const char *m = getenv("TVL1_BATCH_GROUP")) c->batch_group = atoi(m) != 0;
-  if (const char *m = getenv("TVL1_BATCH_SEGS")) c->batch_segs = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);

@@ -105,12 +105,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *p, uns
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)bytes, 0x00020000);
 }
 constexpr unsigned kOOB = 0x7ffffff0u;   // byte offset beyond every plane: store dropped
-#ifndef TVL1_TB4_P2P   // k_iterate_tb4: neighbour flags instead of block barriers (r4)
-#define TVL1_TB4_P2P 0
-#endif
-#ifndef TVL1_WI_S2F   // k_warp_iter / kb_warp_iter: stage 2 fills the window ring (r4)
-#define TVL1_WI_S2F 1
-#endif
 #ifndef TVL1_STORE_AUX
 #define TVL1_STORE_AUX 2
 #endif
@@ -1600,130 +1594,9 @@ __device__ __forceinline__ void tb4_iterations(Row<false, 2> (&r)[NR], const int
   }
 }
 
-// The same iterations with point-to-point synchronisation instead of two block barriers per
-// iteration (r4; TVL1_TB4_P2P).  A wavefront holds row groups 2w (lanes
-// 0-31) and 2w + 1 (lanes 32-63).  The boundary between its two groups is crossed with a lane
-// swap (ds_bpermute, no barrier); the boundaries to the wavefronts above and below go through
-// LDS slots double-buffered by iteration parity, each published by a release store of the
-// iteration count to a per-wave LDS flag that the neighbour polls with an acquire load.  A
-// wave therefore waits only for its two neighbours, never for the slowest of the block's 8.
-// No cycle: at iteration n a wave publishes p (the last row of group 2w + 1) before it waits
-// for wave w - 1's p, and publishes u (the first row of group 2w) before it waits for wave
-// w + 1's u.  A slot of parity n & 1 is rewritten at n + 2 only after the reader published
-// its own iteration n + 1 data, which it does after reading.  Same operands, same bits.
-struct Tb4Xch {
-  float2 p[2][2][kTb4Groups / 2][32];   // [parity][p12, p22][wave][lane]: group 2w + 1's last row
-  float2 u[2][2][kTb4Groups / 2][32];   // [parity][u1, u2][wave][lane]: group 2w's first row
-  int flag_p[kTb4Groups / 2], flag_u[kTb4Groups / 2];
-};
-
-__device__ __forceinline__ void tb4_wait(const int *f, int n) {
-  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < n)
-    __builtin_amdgcn_s_sleep(1);
-}
-
-__device__ __forceinline__ float2 swap32(float2 v) {   // lane l <-> lane l ^ 32
-  return make_float2(__shfl_xor(v.x, 32), __shfl_xor(v.y, 32));
-}
-
-template <int FM, int NR, bool IN>
-__device__ __forceinline__ void tb4_iterations_p2p(Row<false, 2> (&r)[NR], const int (&Y)[NR],
-                                                   const bool (&out_ok)[NR], Tb4Xch &x,
-                                                   const IterArgs &a, int K, int X, int q, int c4,
-                                                   double &acc) {
-  constexpr int PX = 2, NW = kTb4Groups / 2;
-  const int w = q >> 1;
-  const bool hi = q & 1;
-  const int lane = threadIdx.x & 63;
-  for (int it = 0; it < K; ++it) {
-    const bool last = it == K - 1;
-    const int par = it & 1;
-    // ---- estimateU: p^{n-1} at y-1 for each group's first row
-    const float2 pl12 = pack(r[NR - 1].p12), pl22 = pack(r[NR - 1].p22);
-    if (hi && w < NW - 1) {
-      x.p[par][0][w][c4] = pl12;
-      x.p[par][1][w][c4] = pl22;
-    }
-    if (w < NW - 1 && lane == 32)
-      __hip_atomic_store(&x.flag_p[w], it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const float2 s12 = swap32(pl12), s22 = swap32(pl22);
-    float up12[PX], up22[PX], zero3[PX];
-    zerov<PX>(zero3);
-    if (w > 0) tb4_wait(&x.flag_p[w - 1], it + 1);
-    if (hi) {   // group 2w + 1 <- group 2w (this wave's lanes 0-31)
-      unpack(up12, s12);
-      unpack(up22, s22);
-    } else if (w > 0) {   // group 2w <- group 2w - 1 (wave w - 1's lanes 32-63)
-      unpack(up12, x.p[par][0][w - 1][c4]);
-      unpack(up22, x.p[par][1][w - 1][c4]);
-    } else {   // region row 0: its own row (k_iterate_tb's clamp)
-#pragma unroll
-      for (int k = 0; k < PX; ++k) up12[k] = r[0].p12[k], up22[k] = r[0].p22[k];
-    }
-#pragma unroll
-    for (int g = 0; g < NR; ++g) {
-      float n1[PX], n2[PX], n3[PX];
-      if (g == 0)
-        estimate_u<false, PX, FM>(r[0], up12, up22, zero3, IN ? 1 : X, IN ? 1 : Y[0], a, n1, n2, n3);
-      else
-        estimate_u<false, PX, FM>(r[g], r[g - 1].p12, r[g - 1].p22, zero3, IN ? 1 : X, IN ? 1 : Y[g], a,
-                                  n1, n2, n3);
-      if (last && a.calc_err && out_ok[g]) {
-#pragma unroll
-        for (int k = 0; k < PX; ++k)
-          if (X + k < a.W) acc += (double)residual_px<FM>(r[g].u1[k] - n1[k], r[g].u2[k] - n2[k]);
-      }
-#pragma unroll
-      for (int k = 0; k < PX; ++k) {
-        r[g].u1[k] = n1[k];
-        r[g].u2[k] = n2[k];
-      }
-    }
-    // ---- estimateDualVariables: u^n at y+1 for each group's last row
-    const float2 uf1 = pack(r[0].u1), uf2 = pack(r[0].u2);
-    if (!hi && w > 0) {
-      x.u[par][0][w][c4] = uf1;
-      x.u[par][1][w][c4] = uf2;
-    }
-    if (w > 0 && lane == 0)
-      __hip_atomic_store(&x.flag_u[w], it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const float2 t1 = swap32(uf1), t2 = swap32(uf2);
-    float d1[PX], d2[PX];
-    if (w < NW - 1) tb4_wait(&x.flag_u[w + 1], it + 1);
-    if (!hi) {   // group 2w <- group 2w + 1 (this wave's lanes 32-63)
-      unpack(d1, t1);
-      unpack(d2, t2);
-    } else if (w < NW - 1) {   // group 2w + 1 <- group 2w + 2 (wave w + 1's lanes 0-31)
-      unpack(d1, x.u[par][0][w + 1][c4]);
-      unpack(d2, x.u[par][1][w + 1][c4]);
-    } else {   // region bottom row: its own row
-#pragma unroll
-      for (int k = 0; k < PX; ++k) d1[k] = r[NR - 1].u1[k], d2[k] = r[NR - 1].u2[k];
-    }
-#pragma unroll
-    for (int g = 0; g < NR; ++g) {
-      const bool has_down = IN || Y[g] + 1 < a.H;
-      const int xd = IN ? 0 : X, wd = IN ? 64 : a.W;
-      float q11[PX], q12[PX], q21[PX], q22[PX];
-      if (g < NR - 1) {
-        dual_component<PX, false, FM>(r[g].u1, r[g + 1].u1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12);
-        dual_component<PX, false, FM>(r[g].u2, r[g + 1].u2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22);
-      } else {
-        dual_component<PX, false, FM>(r[g].u1, d1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12);
-        dual_component<PX, false, FM>(r[g].u2, d2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22);
-      }
-#pragma unroll
-      for (int k = 0; k < PX; ++k) {
-        r[g].p11[k] = q11[k]; r[g].p12[k] = q12[k];
-        r[g].p21[k] = q21[k]; r[g].p22[k] = q22[k];
-      }
-    }
-  }
-}
-
 template <int FM, int NR, bool IN>
 __device__ __forceinline__ void tb4_body(const TBArgs &t, float2 (&lds)[4][kTb4Groups][32], int xr0,
-                                         int yr0, Tb4Xch *xch = nullptr) {
+                                         int yr0) {
   constexpr int PX = 2, LPR = 32, NGR = kTb4Groups, kTb4Rows = NR * NGR;
   constexpr int HALO = 4 / PX;   // lanes of the 4-px x halo
   const IterArgs &a = t.it;
@@ -1746,10 +1619,7 @@ __device__ __forceinline__ void tb4_body(const TBArgs &t, float2 (&lds)[4][kTb4G
                 Y[g] < a.H && X < a.W;
   }
   double acc = 0.0;
-  if (xch)
-    tb4_iterations_p2p<FM, NR, IN>(r, Y, out_ok, *xch, a, K, X, q, c4, acc);
-  else
-    tb4_iterations<FM, NR, IN>(r, Y, out_ok, lds, a, K, X, q, c4, acc);
+  tb4_iterations<FM, NR, IN>(r, Y, out_ok, lds, a, K, X, q, c4, acc);
 #pragma unroll
   for (int g = 0; g < NR; ++g) {
     if (out_ok[g]) {
@@ -1776,27 +1646,19 @@ __device__ __forceinline__ void tb4_body(const TBArgs &t, float2 (&lds)[4][kTb4G
   }
 }
 
-template <int FM, int NR = kTb4RowsPerThread, bool P2P = TVL1_TB4_P2P>
+template <int FM, int NR = kTb4RowsPerThread>
 __global__ __launch_bounds__(32 * kTb4Groups, 4) void k_iterate_tb4(TBArgs t) {
-  // !P2P: [p12 last, p22 last, u1 first, u2 first][group][lane]; P2P: the Tb4Xch slots + flags
-  constexpr size_t kBar = sizeof(float2) * 4 * kTb4Groups * 32;
-  __shared__ __attribute__((aligned(16))) char smem[P2P ? sizeof(Tb4Xch) : kBar];
+  __shared__ float2 lds[4][kTb4Groups][32];   // [p12 last, p22 last, u1 first, u2 first][group][lane]
   if (gated_off(t.it.gate, t.it.gate_seq)) return;   // whole grid
-  Tb4Xch *X = P2P ? reinterpret_cast<Tb4Xch *>(smem) : nullptr;
-  if (P2P) {   // flags start at 0 (every wave of the block passes this barrier once)
-    if (threadIdx.x < kTb4Groups / 2) X->flag_p[threadIdx.x] = X->flag_u[threadIdx.x] = 0;
-    __syncthreads();
-  }
   int bx, by;
   tile_of_block(blockIdx.x, gridDim.x, t.tiles_x, gridDim.x / t.tiles_x, bx, by);
   const int xr0 = bx * 56 - 4;
   const int yr0 = by * t.out_h - t.niter;
-  auto &L = *reinterpret_cast<float2 (*)[4][kTb4Groups][32]>(smem);   // !P2P only
   // wave-uniform: the whole region inside the image with a 1-px margin (tb4_iterations' IN)
   if (xr0 >= 1 && yr0 >= 1 && xr0 + 64 < t.it.W && yr0 + NR * kTb4Groups < t.it.H)
-    tb4_body<FM, NR, true>(t, L, xr0, yr0, X);
+    tb4_body<FM, NR, true>(t, lds, xr0, yr0);
   else
-    tb4_body<FM, NR, false>(t, L, xr0, yr0, X);
+    tb4_body<FM, NR, false>(t, lds, xr0, yr0);
 }
 
 // ---------------------------------------------------------------- K6+K8 wavefront pipeline
@@ -2260,9 +2122,7 @@ struct WiLane {
 // THP: the producer also does the first iteration's TH step and the C ring carries v (one
 // consumer wavefront); otherwise it carries u^0 and stage 1's wavefront does the step (two
 // consumers, where the producers set the block's pace: 1.5 % faster, tools/wi_probe.hip)
-// FILL: the producer also fills the window ring (window row g + M before the barrier);
-// otherwise stage 2's wavefront does (wi_s2_fill, the r4 default with two consumers).
-template <int M, int FM, int BW, bool THP = true, bool FILL = true>
+template <int M, int FM, int BW, bool THP = true>
 __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__restrict__ cring,
                                              const WarpRowI &cur, WarpRowI &ahead,
                                              const WarpRingArgs &wa, const WarpIterArgs &w,
@@ -2271,10 +2131,10 @@ __device__ __forceinline__ void wi_prod_step(float *__restrict__ ring, float *__
                                              unsigned nb, unsigned rowb) {
   constexpr int WW = wi_ww<M, BW>();
   // loads for row g + kWarpAhead: window row g + kWarpAhead + M and its flow row
-  if (FILL) warp_ring_load(ahead, wa, nb, rowb, g + kWarpAhead + M, xs);
+  warp_ring_load(ahead, wa, nb, rowb, g + kWarpAhead + M, xs);
   warp_flow_load(ahead, wa, nb, rowb, g + kWarpAhead, P.xcb);
   __builtin_amdgcn_sched_barrier(0);
-  if (FILL) wi_ring_put<M, BW>(ring, cur, g + M, p, lane);
+  wi_ring_put<M, BW>(ring, cur, g + M, p, lane);
   lds_barrier();
   // rows past the image bottom repeat row H-1 (the pass clamps its input rows)
   const int gy = imin(g, wa.H - 1);
@@ -2494,73 +2354,14 @@ __device__ __forceinline__ void wi_s1_step(WiS1<PX> &S, const float *__restrict_
   lds_put<PX>(h + 7 * BW, q22);
 }
 
-// ---- the window ring filled by stage 2 (S2F, r4).  With two consumers the producers set
-// the block's pace (barrier waits: producers 6-8 %, stage 1 15 %, stage 2 30-34 % of their
-// lives), so stage 2's wavefront takes over the producers' ring fill: the I1 loads
-// of each window row, centeredGradient at each slot and the three plane writes.  Stage 2's
-// step r lies between the block's barriers r - r0 + 2 and r - r0 + 3; the producers gather row
-// r0 + b after barrier b from rows up to r0 + b + M, so stage 2 writes window row r + 3 + M at
-// its step r (one interval ahead; live rows r0+b-M .. r0+b+1+M = 2M + 2 <= the ring's 16) and
-// the rows r0 - M .. r0 + M + 2 before barrier 0.  Each lane fills up to 3 slots: lane, 64 +
-// lane and, lanes < 2 MX, 128 + lane (BW = 128); the values are wi_ring_put's, so the ring's
-// contents -- and every result -- are unchanged.
-struct WarpRow3 {   // one window row's stencils at a lane's 3 slots (raw I1)
-  float c[3], l[3], r[3], n[3], s[3];
-};
-
-__device__ __forceinline__ void wi_fill_load(WarpRow3 &v, const WarpRingArgs &a, unsigned nb,
-                                             unsigned rowb, int gy, const unsigned (&xs)[3][3]) {
-  const int r = imin(imax(gy, 0), a.H - 1);
-  const unsigned so = (unsigned)r * rowb, su = (unsigned)imax(r - 1, 0) * rowb,
-                 sd = (unsigned)imin(r + 1, a.H - 1) * rowb;
-  float t[1];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    bload<1>(t, a.I1, nb, xs[k][0], so); v.c[k] = t[0];
-    bload<1>(t, a.I1, nb, xs[k][1], so); v.l[k] = t[0];
-    bload<1>(t, a.I1, nb, xs[k][2], so); v.r[k] = t[0];
-    bload<1>(t, a.I1, nb, xs[k][0], su); v.n[k] = t[0];
-    bload<1>(t, a.I1, nb, xs[k][0], sd); v.s[k] = t[0];
-  }
-}
-
-template <int M, int BW>
-__device__ __forceinline__ void wi_fill_put(float *__restrict__ ring, const WarpRow3 &v, int r,
-                                            int lane) {
-  constexpr int WW = wi_ww<M, BW>();
-  float *dst = ring + wi_slot<M>(r) * ring_pitch(WW);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    if (k < 2 || lane < 2 * ring_mx<M>()) {
-      const int o = 64 * k + lane;
-      dst[o] = v.c[k];
-      dst[WW + o] = 0.5f * (v.r[k] - v.l[k]);
-      dst[2 * WW + o] = 0.5f * (v.s[k] - v.n[k]);
-    }
-  }
-}
-
 // Stage 2 at input row r (one barrier after stage 1's step r): u^2(r-1) = v^2(r-1) +
 // theta div p^1, the residual term (u^1(r-1) - u^2(r-1))^2, p^2(r-2); stores u^2 and p^2.
-struct WiFill {   // stage 2's ring fill: the level image and the lane's 3 slot columns
-  WarpRingArgs wa;
-  unsigned xs[3][3];   // byte offsets: clamped column, its clamped x-1 and x+1
-  unsigned nb;         // plane bytes
-};
-
-template <int FM, int PX, int M = 6, bool S2F = false>
+template <int FM, int PX>
 __device__ __forceinline__ void wi_s2_step(WiS2<PX> &S, const float *__restrict__ hring,
                                            const IterArgs &a, const RollBufs &B, int r,
                                            const RollLane &L, int lane, unsigned rowb,
-                                           double &acc, float *__restrict__ ring,
-                                           const WarpRow3 &fcur, WarpRow3 &fahead,
-                                           const WiFill &F) {
-  if (S2F) {   // window row r + 5 + M loads (two steps ahead); row r + 3 + M enters the ring
-    wi_fill_load(fahead, F.wa, F.nb, rowb, r + 5 + M, F.xs);
-    __builtin_amdgcn_sched_barrier(0);
-  }
+                                           double &acc) {
   lds_barrier();   // hand-off row r was written at the previous step
-  if (S2F) wi_fill_put<M, 64 * PX>(ring, fcur, r + 3 + M, lane);
   constexpr int BW = 64 * PX;
   const unsigned ps = B.pstride;
   const float *h = hring + (r & 1) * (kWiH * BW) + PX * lane;
@@ -2625,13 +2426,11 @@ __device__ __forceinline__ void wi_s2_step(WiS2<PX> &S, const float *__restrict_
   }
 }
 
-// NC = 2 also moves the first iteration's TH step from the producers to stage 1's wavefront;
-// S2F (NC = 2 only) moves the window-ring fill from the producers to stage 2's wavefront
-template <int M, int FM, int BW, int PRIO = 0, int NC = 1, bool S2F = false>
+// NC = 2 also moves the first iteration's TH step from the producers to stage 1's wavefront
+template <int M, int FM, int BW, int PRIO = 0, int NC = 1>
 __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, float *__restrict__ ring,
                                                float *__restrict__ cring,
                                                float *__restrict__ hring = nullptr) {
-  static_assert(!S2F || (NC == 2 && BW == 128), "stage-2 fill: two consumers, 128-px bands");
   constexpr int K = 2, PX = BW / 64, HALO = roll_halo<2, PX>(), WW = wi_ww<M, BW>();
   static_assert(BW == 64 || BW == 128, "one producer per 64 columns, PX = 1 or 2");
   static_assert(2 * M + 2 <= wi_rows<M>(), "window ring too small for the margin");
@@ -2697,44 +2496,14 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
         S.Q11p[j] = S.Q12p[j] = S.Q21p[j] = S.Q22p[j] = 0.0f;
         S.U1c[j] = S.U2c[j] = S.U1p[j] = S.U2p[j] = 0.0f;
       }
-      WiFill F;
-      WarpRow3 FA, FB, FC;
-      if (S2F) {
-        F.wa.I1 = w.I1;
-        F.wa.W = a.W;
-        F.wa.H = a.H;
-        F.wa.P = a.P;
-        F.nb = nb;
-        const int xw0 = X0 - ring_mx<M>();
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {   // slot 64k + lane (k = 2: lanes < 2 MX, else a re-read)
-          const int slot = k < 2 || lane < 2 * ring_mx<M>() ? 64 * k + lane : lane;
-          const int cc = imin(imax(xw0 + slot, 0), a.W - 1);
-          F.xs[k][0] = 4u * cc;
-          F.xs[k][1] = 4u * imax(cc - 1, 0);
-          F.xs[k][2] = 4u * imin(cc + 1, a.W - 1);
-        }
-        // the ring prologue: window rows r0 - M .. r0 + M + 2, three rows' loads at a time
-        for (int y = r0 - M; y <= r0 + M + 2; y += 3) {
-          wi_fill_load(FA, F.wa, nb, rowb, y, F.xs);
-          wi_fill_load(FB, F.wa, nb, rowb, y + 1, F.xs);
-          wi_fill_load(FC, F.wa, nb, rowb, y + 2, F.xs);
-          wi_fill_put<M, BW>(ring, FA, y, lane);
-          if (y + 1 <= r0 + M + 2) wi_fill_put<M, BW>(ring, FB, y + 1, lane);
-          if (y + 2 <= r0 + M + 2) wi_fill_put<M, BW>(ring, FC, y + 2, lane);
-        }
-        // the register ring: rows r0 + 3 + M (step r0) and r0 + 4 + M (step r0 + 1)
-        wi_fill_load(FA, F.wa, nb, rowb, r0 + 3 + M, F.xs);
-        wi_fill_load(FB, F.wa, nb, rowb, r0 + 4 + M, F.xs);
-      }
       lds_barrier();
       lds_barrier();
       double acc = 0.0;
       for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
         progress_prio<PRIO>(h, thirds);
-        wi_s2_step<FM, PX, M, S2F>(S, hring, a, Bf, r, L, lane, rowb, acc, ring, FA, FC, F);
-        wi_s2_step<FM, PX, M, S2F>(S, hring, a, Bf, r + 1, L, lane, rowb, acc, ring, FB, FA, F);
-        wi_s2_step<FM, PX, M, S2F>(S, hring, a, Bf, r + 2, L, lane, rowb, acc, ring, FC, FB, F);
+        wi_s2_step<FM, PX>(S, hring, a, Bf, r, L, lane, rowb, acc);
+        wi_s2_step<FM, PX>(S, hring, a, Bf, r + 1, L, lane, rowb, acc);
+        wi_s2_step<FM, PX>(S, hring, a, Bf, r + 2, L, lane, rowb, acc);
       }
       lds_barrier();
       if (a.calc_err) {
@@ -2831,41 +2600,38 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
       xs[k][1] = 4u * imax(cc - 1, 0);
       xs[k][2] = 4u * imin(cc + 1, a.W - 1);
     }
-    // ring prologue: window rows r0 - M .. r0 + M - 1, loads issued M rows at a time (with
-    // S2F stage 2 fills the ring)
-    if (!S2F) {
+    // ring prologue: window rows r0 - M .. r0 + M - 1, loads issued M rows at a time
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        WarpRowI t[M];
+    for (int b = 0; b < 2; ++b) {
+      WarpRowI t[M];
 #pragma unroll
-        for (int i = 0; i < M; ++i) warp_ring_load(t[i], wa, nb, rowb, r0 - M + b * M + i, xs);
+      for (int i = 0; i < M; ++i) warp_ring_load(t[i], wa, nb, rowb, r0 - M + b * M + i, xs);
 #pragma unroll
-        for (int i = 0; i < M; ++i) wi_ring_put<M, BW>(ring, t[i], r0 - M + b * M + i, p, lane);
-      }
+      for (int i = 0; i < M; ++i) wi_ring_put<M, BW>(ring, t[i], r0 - M + b * M + i, p, lane);
     }
     WarpRowI A, B, C;
-    if (!S2F) warp_ring_load(A, wa, nb, rowb, r0 + M, xs);
+    warp_ring_load(A, wa, nb, rowb, r0 + M, xs);
     warp_flow_load(A, wa, nb, rowb, r0, P.xcb);
-    if (!S2F) warp_ring_load(B, wa, nb, rowb, r0 + 1 + M, xs);
+    warp_ring_load(B, wa, nb, rowb, r0 + 1 + M, xs);
     warp_flow_load(B, wa, nb, rowb, r0 + 1, P.xcb);
     for (int h = 0, g = r0; h <= thirds; ++h, g += 3) {
       progress_prio<PRIO>(h, thirds);
       constexpr bool THP = NC == 1;
-      wi_prod_step<M, FM, BW, THP, !S2F>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
-      wi_prod_step<M, FM, BW, THP, !S2F>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
-      wi_prod_step<M, FM, BW, THP, !S2F>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM, BW, THP>(ring, cring, A, C, wa, w, g, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM, BW, THP>(ring, cring, B, A, wa, w, g + 1, p, lane, P, xs, ys, ye, nb, rowb);
+      wi_prod_step<M, FM, BW, THP>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
     }
   }
 }
 
-template <int M, int FM = 0, int BW = 128, int PRIO = 1, int NC = 1, bool S2F = TVL1_WI_S2F>
+template <int M, int FM = 0, int BW = 128, int PRIO = 1, int NC = 1>
 __global__ __launch_bounds__(64 * NC + BW) void k_warp_iter(WarpIterArgs w) {
   __shared__ float ring[wi_rows<M>() * ring_pitch(wi_ww<M, BW>())];
   __shared__ float cring[2 * 5 * BW];
   __shared__ float hring[NC == 2 ? 2 * kWiH * BW : 1];
   const int wid = __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x));
   if (wid >= w.ra.waves || gated_off(w.ra.it.gate, w.ra.it.gate_seq)) return;   // whole blocks
-  warp_iter_body<M, FM, BW, PRIO, NC, S2F && NC == 2 && BW == 128>(w, wid, ring, cring, hring);
+  warp_iter_body<M, FM, BW, PRIO, NC>(w, wid, ring, cring, hring);
 }
 
 // K7: fixed-order sum of the per-block partials (one block).

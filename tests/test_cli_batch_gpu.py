@@ -73,7 +73,7 @@ def test_batched_strips_byte_identical_to_per_pair(stack, tmp_path, ext, otype):
         assert eb["ok"] and eu["ok"]
         assert len(eb["solves"]) == 2
         for a, b in zip(eb["solves"], eu["solves"]):
-            assert a["batch"] == 8 and "batch" not in b
+            assert a["batch"] == 4 and "batch" not in b   # 8 pairs over 2 batch workers
             assert a["roi"] == b["roi"] and a["warp_iterations"] == b["warp_iterations"]
             assert a["read_rows_only"] is (ext == "tif")
     assert sorted(rb.stdout.splitlines()) == sorted(ru.stdout.splitlines())
@@ -158,5 +158,5 @@ def test_mixed_job_and_fault_recovery(stack, tmp_path):
     assert ob.keys() == ou.keys() and len(ob) == 9 * 4
     for k in ob:
         assert ob[k] == ou[k], k
-    assert "batch" not in sb[1]["solves"][0] and sb[0]["solves"][0]["batch"] == 7
+    assert "batch" not in sb[1]["solves"][0] and sb[0]["solves"][0]["batch"] == 4   # 7 = 4 + 3
     assert all(e["ok"] for e in sb)

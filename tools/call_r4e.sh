@@ -4,7 +4,7 @@
 set -o pipefail
 out=gpurun_out/r4e
 mkdir -p $out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_batch.py tests/test_cli_batch_gpu.py tests/test_gpu_lifecycle.py > $out/tests.log 2>&1 || { echo TESTS_FAIL; tail -40 $out/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_cli_batch_gpu.py tests/test_gpu_lifecycle.py tests/test_gpu_batch.py -k "not matches_oracle" > $out/tests.log 2>&1 || { echo TESTS_FAIL; tail -40 $out/tests.log; exit 1; }
 tail -3 $out/tests.log
 # the point-to-point k_iterate_tb4 first on its own, short: a small parity subset under 90 s
 TVL1_ENGINE_SO=ab_p2p/libtvl1_hip.so timeout -k 10 90 python -u -m pytest -x -q --timeout 60 --timeout-method thread tests/test_gpu_parity.py -k "golden" > $out/p2p_smoke.log 2>&1 || { echo P2P_FAIL; tail -20 $out/p2p_smoke.log; exit 1; }

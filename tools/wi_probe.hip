@@ -54,7 +54,7 @@ __global__ __launch_bounds__(64 * NC + BW) WI_ATTR void k_probe(WarpIterArgs w, 
   if (wid >= w.ra.waves) return;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-  warp_iter_body<M, FM, BW, PRIO, NC, TVL1_WI_S2F && NC == 2 && BW == 128>(w, wid, ring, cring, hring);
+  warp_iter_body<M, FM, BW, PRIO, NC>(w, wid, ring, cring, hring);
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long c1 = __builtin_amdgcn_s_memtime();
 #ifdef WI_BARRIER
