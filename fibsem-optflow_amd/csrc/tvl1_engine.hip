@@ -132,8 +132,6 @@ struct tvl1_ctx {
   size_t bps = 0;                       // pair stride of the level-0-sized planes (floats)
   double *bpartials = nullptr;
   int batch_fuse = 1;                   // TVL1_BATCH_FUSE=0: no fused warp + first pass
-  int batch_px4 = 0;                    // TVL1_BATCH_PX4=1: <= 2-iteration batched passes with
-                                        // 4 px per lane
   int batch_group = 1;                  // TVL1_BATCH_GROUP=0: r3's lock-step passes (the
                                         // shortest pass any pair allows, for all)
   int batch_store_pred = 1;             // TVL1_BATCH_STORE=1: kb_warp_iter always stores the
@@ -1775,19 +1773,16 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           sel.pbit = pbit;
           sel.pzero = pzero;
           int blocks;   // residual partials per pair (pair stride c->bnblk)
-          {   // wavefront pipelines: 64*PX-px bands down the whole level, one per wave
+          {   // wavefront pipelines: 128-px bands down the whole level, one per wave
             BatchRoll br{};
             br.ra.b = batch_bufs;
             br.ra.it = it;
-            // TVL1_BATCH_PX4=1: passes of <= 2 iterations with 4 px per lane (256-px bands,
-            // 16-byte accesses), as k_iterate_roll on large single-pair levels
-            const int px = K <= 2 && c->batch_px4 ? 4 : 2;
-            const int halo = (K + px - 1) / px * px;   // roll_halo<K, PX>
-            br.ra.bands = (lw + 64 * px - 2 * halo - 1) / (64 * px - 2 * halo);
+            const int halo = (K + 1) / 2 * 2;   // roll_halo<K, 2>
+            br.ra.bands = (lw + 128 - 2 * halo - 1) / (128 - 2 * halo);
             // segments sized so the launch's wavefronts fill whole rounds of resident slots
             br.ra.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
                                              : roll_segment(br.ra.bands * sel.n, lh, K,
-                                                            c->roll_slots[K][0][px]);
+                                                            c->roll_slots[K][0][2]);
             br.ra.waves = br.ra.bands * ((lh + br.ra.seg_rows - 1) / br.ra.seg_rows);
             blocks = br.ra.waves;
             if (blocks > c->bnblk)
@@ -1803,19 +1798,17 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
             br.sel = sel;
             const dim3 grid((br.ra.waves + 3) / 4, sel.n);
             const size_t tkp = prof_begin(c, st);
-#define KB_ROLL_M(FM) hipLaunchKernelGGL((kb_iterate_roll<KK, PP, FM>), grid, dim3(256), 0, st, br);
-#define KB_ROLL(K_, P_)             \
+#define KB_ROLL_M(FM) hipLaunchKernelGGL((kb_iterate_roll<KK, 2, FM>), grid, dim3(256), 0, st, br);
+#define KB_ROLL(K_)                 \
   {                                 \
-    constexpr int KK = K_, PP = P_; \
+    constexpr int KK = K_;          \
     MATH_SWITCH(math, KB_ROLL_M)    \
   }
-            switch (K * 8 + px) {
-              case 1 * 8 + 2: KB_ROLL(1, 2) break;
-              case 2 * 8 + 2: KB_ROLL(2, 2) break;
-              case 3 * 8 + 2: KB_ROLL(3, 2) break;
-              case 1 * 8 + 4: KB_ROLL(1, 4) break;
-              case 2 * 8 + 4: KB_ROLL(2, 4) break;
-              default: KB_ROLL(4, 2) break;
+            switch (K) {
+              case 1: KB_ROLL(1) break;
+              case 2: KB_ROLL(2) break;
+              case 3: KB_ROLL(3) break;
+              default: KB_ROLL(4) break;
             }
 #undef KB_ROLL
 #undef KB_ROLL_M
@@ -1829,7 +1822,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
               const double Nl = (double)lw * lh;
               int nz = 0;
               for (int j = 0; j < sel.n; ++j) nz += pzero.test(sel.idx[j]) ? 1 : 0;
-              const double band_bytes = (double)br.ra.bands * 64 * px * rows * 4.0;
+              const double band_bytes = (double)br.ra.bands * 128 * rows * 4.0;
               const double hbm = band_bytes * ((double)sel.n * 5 + (double)(sel.n - nz) * 4) +
                                  (double)sel.n * Nl * 4.0 * 6.0;
               prof_end(c, st, tkp, 0, (double)sel.n * Nl * 64.0 * K, hbm);
@@ -2247,7 +2240,6 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BATCH_STORE")) c->batch_store_pred = atoi(m) == 0;
   if (const char *m = getenv("TVL1_BATCH_GROUP")) c->batch_group = atoi(m) != 0;
-  if (const char *m = getenv("TVL1_BATCH_PX4")) c->batch_px4 = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);

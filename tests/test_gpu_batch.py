@@ -55,20 +55,18 @@ def pairs(n, w, h, seed):
     (5, 200, 60, dict(nscales=4, warps=3, epsilon=0.0, iterations=7)),   # fixed work
 ])
 @pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0", "TVL1_WI_NC=1", "TVL1_BATCH_STORE=1",
-                                 "TVL1_BATCH_GROUP=0", "TVL1_BATCH_PX4=1"])
+                                 "TVL1_BATCH_GROUP=0"])
 @pytest.mark.parametrize("math", [0, 2])
 def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw, math):
     """kb_warp_iter (fused warp + first pass; 2 consumer wavefronts, or 1 with
     TVL1_WI_NC=1; constants stored on demand, or always with TVL1_BATCH_STORE=1), passes grouped
-    by their length (or r3's lock step with TVL1_BATCH_GROUP=0), short passes with 2 or (opt-in
-    TVL1_BATCH_PX4=1) 4 px per lane,
+    by their length (or r3's lock step with TVL1_BATCH_GROUP=0),
     kb_warp_ring, kb_iterate_roll<K, 2>: IEEE and fma mode, each bit-identical to the oracle
     in that mode."""
     monkeypatch.delenv("TVL1_BATCH_FUSE", raising=False)
     monkeypatch.delenv("TVL1_WI_NC", raising=False)
     monkeypatch.delenv("TVL1_BATCH_STORE", raising=False)
     monkeypatch.delenv("TVL1_BATCH_GROUP", raising=False)
-    monkeypatch.delenv("TVL1_BATCH_PX4", raising=False)
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
     p = capi.make_params(fast_math=math, **kw)
