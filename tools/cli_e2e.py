@@ -101,6 +101,9 @@ def main():
                     help="comma list of strip_batch values for the strip job (default: the CLI's)")
     ap.add_argument("--no-single-thread", action="store_true",
                     help="skip the one-decode-thread runs")
+    ap.add_argument("--strides", default="1",
+                    help="pairs (z, z + s) for each s: a comma list, or A-B for every s in it "
+                         "(gen_cross-style long-range pairs; long jobs over one stack)")
     args = ap.parse_args()
     d = Path(args.out or tempfile.mkdtemp(prefix="cli_e2e_"))
     d.mkdir(parents=True, exist_ok=True)
@@ -109,9 +112,14 @@ def main():
     print(json.dumps({"stack": f"{args.slices} x {args.width}x{args.height} {args.format}",
                       "bytes": sum(os.path.getsize(p) for p in paths),
                       "write_s": round(time.perf_counter() - t0, 1)}), flush=True)
-    pairs = [{"p": str(paths[z]), "q": str(paths[z + 1]), "output_name": f"z{z}",
-              "pId": f"{z}", "qId": f"{z + 1}", "pGroupId": f"{z}.0", "qGroupId": f"{z + 1}.0"}
-             for z in range(args.slices - 1)]
+    if "-" in args.strides:
+        lo, hi = (int(t) for t in args.strides.split("-"))
+        strides = list(range(lo, hi + 1))
+    else:
+        strides = [int(t) for t in args.strides.split(",")]
+    pairs = [{"p": str(paths[z]), "q": str(paths[z + s]), "output_name": f"z{z}_s{s}",
+              "pId": f"{z}", "qId": f"{z + s}", "pGroupId": f"{z}.0", "qGroupId": f"{z + s}.0"}
+             for s in strides for z in range(args.slices - s)]
     W, H = args.width, args.height
     jobs = {}
     if "c2" in args.jobs:
