@@ -151,10 +151,14 @@ def main():
             if threads:
                 cfg["decode_threads"] = threads
             (d / name).mkdir(exist_ok=True)
+            for f in (d / name).glob("pm_*.json"):
+                f.unlink()
             dt, steady = run(cfg, d, f"{name}_{threads or 'pool'}")
             n = len(pairs)
+            # every pair's point-match record was written (random_points output)
+            recs = sum(len(json.loads(f.read_text())) for f in (d / name).glob("pm_*.json"))
             print(json.dumps({"job": name, "decode_threads": threads or "default (pool)",
-                              "pairs": n, "wall_s": round(dt, 3),
+                              "pairs": n, "point_match_records": recs, "wall_s": round(dt, 3),
                               "pairs_per_s": round(n / dt, 2),
                               "steady_pairs_per_s": steady and round(steady, 2)}), flush=True)
 
