@@ -61,9 +61,10 @@ def test_bench_line_carries_the_contract_fields(bench):
         assert e["mean"] <= 1e-3 and e["p99.9"] <= 2e-2 and e["max"] <= 0.5
 
 
-# ---- round 3: one box, one evidence set (tools/final_profile.sh -> profiles/r3/final/):
-# the default bench line, one C2 pair alone and one production strip batch alone
-FINAL = PROF / "r3" / "final"
+# ---- rounds 3 and 4: one box, one evidence set each (tools/final_profile.sh ->
+# profiles/r3/final/, profiles/r4/final/): the default bench line, one C2 pair alone and one
+# production strip batch alone
+FINALS = [PROF / "r3" / "final", PROF / "r4" / "final"]
 
 
 def _class_avg_us(stats_csv, prefixes):
@@ -76,9 +77,9 @@ def _class_avg_us(stats_csv, prefixes):
     return ns / calls / 1e3, calls
 
 
-@pytest.mark.skipif(not FINAL.exists(), reason="no r3 final evidence set")
+@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4"])
 @pytest.mark.parametrize("which", ["pair", "strips"])
-def test_r3_roofline_reproduces_by_hand(which):
+def test_final_roofline_reproduces_by_hand(FINAL, which):
     """The bench line's `roofline.frac` (live byte accounting / HIP-event launch time) by hand
     from the same bytes over the rocprofv3 kernel-trace launch average, within 5 %, and the
     accounted bytes against the PMC FETCH x 2 + WRITE bytes of the same class -- for the C2
@@ -106,10 +107,27 @@ def test_r3_roofline_reproduces_by_hand(which):
     assert roof["model_bytes_over_peak"] > 1.0 > roof["frac"]
 
 
-@pytest.mark.skipif(not FINAL.exists(), reason="no r3 final evidence set")
-def test_r3_bench_line_fields():
+@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4"])
+def test_final_bench_line_fields(FINAL):
     d = json.loads((FINAL / "bench_c2.json").read_text().splitlines()[-1])
     assert d["config"]["workload"].startswith("C2") and d["n_gpus"] == 1
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and "build" in cb
     assert d["production_strips"]["roofline"]["launches"] > 0
+
+
+def test_bench_reads_the_r4_traffic_record():
+    """profiles/traffic*.json (bench.py's `traffic`) are the r4 evidence set's records."""
+    for name in ("traffic.json", "traffic_strips.json"):
+        top = json.loads((PROF / name).read_text())
+        r4 = json.loads((PROF / "r4" / "final" / name).read_text())
+        assert top == r4 and "profiles/r4/final/" in top["source"]
+
+
+def test_r4_kb_warp_iter_writes_below_fetches():
+    """with the warp constants stored on demand, kb_warp_iter's PMC writes
+    per dispatch fall below its fetches (r3: 897 MB written against 800 MB fetched)."""
+    txt = (PROF / "r4" / "final" / "pmc_summary_strip_batch.txt").read_text()
+    per_kernel = json.JSONDecoder().raw_decode(txt[txt.index("\n{") + 1:])[0]
+    k = per_kernel["kb_warp_iter<6, 0, 2>"]
+    assert k["write_bytes_per_dispatch"] < k["fetch_bytes_per_dispatch_x2"]
