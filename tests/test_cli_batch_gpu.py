@@ -160,3 +160,18 @@ def test_mixed_job_and_fault_recovery(stack, tmp_path):
         assert ob[k] == ou[k], k
     assert "batch" not in sb[1]["solves"][0] and sb[0]["solves"][0]["batch"] == 4   # 7 = 4 + 3
     assert all(e["ok"] for e in sb)
+
+
+def test_batched_strips_over_two_device_workers(stack, tmp_path):
+    """The CLI's `devices` sharding with batch workers (one per listed device, here the one
+    GPU twice, one batch in flight each): every pair once, outputs identical to one worker."""
+    d, _ = stack
+    r2, s2 = run(job(d, "tif", "flow", tmp_path / "two", devices=[0, 0], inflight=1), tmp_path / "two")
+    r1, s1 = run(job(d, "tif", "flow", tmp_path / "one", inflight=1), tmp_path / "one")
+    o2, o1 = outputs(tmp_path / "two"), outputs(tmp_path / "one")
+    assert o2.keys() == o1.keys() and len(o1) == 8 * 2 * 2
+    for k in o1:
+        assert o2[k] == o1[k], k
+    assert all(e["ok"] for e in s2) and len(s2) == 8
+    assert sorted(r2.stdout.splitlines()) == sorted(r1.stdout.splitlines())
+    assert {e["solves"][0]["batch"] for e in s2} == {4} and {e["solves"][0]["batch"] for e in s1} == {8}
