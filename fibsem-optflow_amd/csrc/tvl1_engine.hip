@@ -41,6 +41,12 @@ thread_local std::string g_create_error;
 constexpr int kStripRows = 32;   // rows per wave strip in k_iterate
 constexpr int kTbMax = 4;        // max iterations fused per pass in k_iterate_tb
 constexpr int kRollMinSeg = 8;   // smallest k_iterate_roll segment (rows)
+// Batched passes on levels at most this wide use 64-px bands, kb_iterate_roll<K, 1> (95
+// VGPRs, 5 wavefronts per SIMD, against 189 and 2 for <4, 2>): the production strips' levels
+// of 515-1573 x 17-51 px give a batch too few 128-px bands to fill the SIMDs, so twice the
+// wavefronts with half the work each finish sooner.  Measured on the strip workload: cut-off
+// 1700 +2.4 %, 1100 +1.2 %, 2500 +1.8 %, every level -3 %.
+constexpr int kBatchPx1W = 1700;
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -136,6 +142,9 @@ struct tvl1_ctx {
                                         // shortest pass any pair allows, for all)
   int batch_store_pred = 1;             // TVL1_BATCH_STORE=1: kb_warp_iter always stores the
                                         // warp constants (r3); default: only predicted pairs
+  int batch_px1_w = kBatchPx1W;         // TVL1_BATCH_PX1_W: batched passes on levels at most
+                                        // this wide run 64-px bands (1 px per lane)
+  int kb1_slots[kRollMax + 1] = {};     // resident kb_iterate_roll<K, 1> wavefronts
   char *gather_scratch = nullptr;       // tvl1_gather_flow's offsets and values
   size_t gather_bytes = 0;
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
@@ -1773,16 +1782,19 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           sel.pbit = pbit;
           sel.pzero = pzero;
           int blocks;   // residual partials per pair (pair stride c->bnblk)
-          {   // wavefront pipelines: 128-px bands down the whole level, one per wave
+          {   // wavefront pipelines: 64*PX-px bands down the whole level, one per wave
             BatchRoll br{};
             br.ra.b = batch_bufs;
             br.ra.it = it;
-            const int halo = (K + 1) / 2 * 2;   // roll_halo<K, 2>
-            br.ra.bands = (lw + 128 - 2 * halo - 1) / (128 - 2 * halo);
+            // PX = 1 (64-px bands) on narrow levels when TVL1_BATCH_PX1_W asks for it
+            const int px = lw <= c->batch_px1_w ? 1 : 2;
+            const int halo = px == 1 ? K : (K + 1) / 2 * 2;   // roll_halo<K, PX>
+            br.ra.bands = (lw + 64 * px - 2 * halo - 1) / (64 * px - 2 * halo);
             // segments sized so the launch's wavefronts fill whole rounds of resident slots
             br.ra.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
                                              : roll_segment(br.ra.bands * sel.n, lh, K,
-                                                            c->roll_slots[K][0][2]);
+                                                            px == 1 ? c->kb1_slots[K]
+                                                                    : c->roll_slots[K][0][2]);
             br.ra.waves = br.ra.bands * ((lh + br.ra.seg_rows - 1) / br.ra.seg_rows);
             blocks = br.ra.waves;
             if (blocks > c->bnblk)
@@ -1798,7 +1810,11 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
             br.sel = sel;
             const dim3 grid((br.ra.waves + 3) / 4, sel.n);
             const size_t tkp = prof_begin(c, st);
-#define KB_ROLL_M(FM) hipLaunchKernelGGL((kb_iterate_roll<KK, 2, FM>), grid, dim3(256), 0, st, br);
+#define KB_ROLL_M(FM)                                                                       \
+  if (px == 1)                                                                            \
+    hipLaunchKernelGGL((kb_iterate_roll<KK, 1, FM>), grid, dim3(256), 0, st, br);         \
+  else                                                                                    \
+    hipLaunchKernelGGL((kb_iterate_roll<KK, 2, FM>), grid, dim3(256), 0, st, br);
 #define KB_ROLL(K_)                 \
   {                                 \
     constexpr int KK = K_;          \
@@ -1812,7 +1828,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
             }
 #undef KB_ROLL
 #undef KB_ROLL_M
-            if (tkp) {   // k_iterate_roll's accounting (PX = 2 bands) per pair of the launch
+            if (tkp) {   // k_iterate_roll's accounting (64*PX-px bands) per pair of the launch
               const int seg = br.ra.seg_rows, segs = (lh + seg - 1) / seg;
               double rows = 0.0;
               for (int sg = 0; sg < segs; ++sg) {
@@ -1822,7 +1838,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
               const double Nl = (double)lw * lh;
               int nz = 0;
               for (int j = 0; j < sel.n; ++j) nz += pzero.test(sel.idx[j]) ? 1 : 0;
-              const double band_bytes = (double)br.ra.bands * 128 * rows * 4.0;
+              const double band_bytes = (double)br.ra.bands * 64 * px * rows * 4.0;
               const double hbm = band_bytes * ((double)sel.n * 5 + (double)(sel.n - nz) * 4) +
                                  (double)sel.n * Nl * 4.0 * 6.0;
               prof_end(c, st, tkp, 0, (double)sel.n * Nl * 64.0 * K, hbm);
@@ -2240,6 +2256,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_BATCH_FUSE")) c->batch_fuse = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BATCH_STORE")) c->batch_store_pred = atoi(m) == 0;
   if (const char *m = getenv("TVL1_BATCH_GROUP")) c->batch_group = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_BATCH_PX1_W")) c->batch_px1_w = atoi(m);
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);
@@ -2275,6 +2292,10 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     ROLL_SLOTS(true, 1, 2) ROLL_SLOTS(true, 2, 2) ROLL_SLOTS(true, 3, 2) ROLL_SLOTS(true, 4, 2)
     ROLL_SLOTS(false, 1, 4) ROLL_SLOTS(false, 2, 4) ROLL_SLOTS(true, 1, 4) ROLL_SLOTS(true, 2, 4)
 #undef ROLL_SLOTS
+    c->kb1_slots[1] = 4 * blocks_of((const void *)kb_iterate_roll<1, 1, kIEEE>, 256);
+    c->kb1_slots[2] = 4 * blocks_of((const void *)kb_iterate_roll<2, 1, kIEEE>, 256);
+    c->kb1_slots[3] = 4 * blocks_of((const void *)kb_iterate_roll<3, 1, kIEEE>, 256);
+    c->kb1_slots[4] = 4 * blocks_of((const void *)kb_iterate_roll<4, 1, kIEEE>, 256);
     c->warp_ring_slots = blocks_of((const void *)k_warp_ring<6, 2>, 128);
     c->witer_slots = c->wi_nc == 2 ? blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 2>, 256)
                                    : blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 1>, 192);

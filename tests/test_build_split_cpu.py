@@ -22,6 +22,7 @@ def _expected():
         for k in (1, 2, 3, 4):
             ks.add(f"k_iterate_roll<false, {k}, 2, {fm}>(tvl1k::RollArgs)")
             ks.add(f"kb_iterate_roll<{k}, 2, {fm}>(tvl1k::BatchRoll)")
+            ks.add(f"kb_iterate_roll<{k}, 1, {fm}>(tvl1k::BatchRoll)")
         for k in (1, 2):
             ks.add(f"k_iterate_roll<false, {k}, 4, {fm}>(tvl1k::RollArgs)")
         ks.add(f"k_iterate_tb4<{fm}, 3>(tvl1k::TBArgs)")
@@ -44,7 +45,7 @@ def _kernels(obj, kinds):
 def test_passes_defined_once_in_their_own_unit():
     exp = _expected()
     inc = (PKG / "csrc" / "tvl1_passes.inc").read_text()
-    assert inc.count("TVL1_PASS_INSTANCE(") == 6 + 11   # 6 gamma forms, 11 per arithmetic mode
+    assert inc.count("TVL1_PASS_INSTANCE(") == 6 + 15   # 6 gamma forms, 15 per arithmetic mode
     defined = _kernels(LIB / "tvl1_passes.o", "VvWw")
     assert exp <= set(defined), sorted(exp - set(defined))
     assert all(n == 2 for k, n in defined.items() if k in exp)   # handle + stub, once each

@@ -55,18 +55,21 @@ def pairs(n, w, h, seed):
     (5, 200, 60, dict(nscales=4, warps=3, epsilon=0.0, iterations=7)),   # fixed work
 ])
 @pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0", "TVL1_WI_NC=1", "TVL1_BATCH_STORE=1",
-                                 "TVL1_BATCH_GROUP=0"])
+                                 "TVL1_BATCH_GROUP=0", "TVL1_BATCH_PX1_W=0",
+                                 "TVL1_BATCH_PX1_W=150"])
 @pytest.mark.parametrize("math", [0, 2])
 def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw, math):
     """kb_warp_iter (fused warp + first pass; 2 consumer wavefronts, or 1 with
     TVL1_WI_NC=1; constants stored on demand, or always with TVL1_BATCH_STORE=1), passes grouped
     by their length (or r3's lock step with TVL1_BATCH_GROUP=0),
-    kb_warp_ring, kb_iterate_roll<K, 2>: IEEE and fma mode, each bit-identical to the oracle
-    in that mode."""
+    kb_warp_ring, kb_iterate_roll<K, 1> (every level of these sizes is under the 1700-px
+    cut-off; <K, 2> everywhere with TVL1_BATCH_PX1_W=0, above 150 px with =150): IEEE and fma
+    mode, each bit-identical to the oracle in that mode."""
     monkeypatch.delenv("TVL1_BATCH_FUSE", raising=False)
     monkeypatch.delenv("TVL1_WI_NC", raising=False)
     monkeypatch.delenv("TVL1_BATCH_STORE", raising=False)
     monkeypatch.delenv("TVL1_BATCH_GROUP", raising=False)
+    monkeypatch.delenv("TVL1_BATCH_PX1_W", raising=False)
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
     p = capi.make_params(fast_math=math, **kw)
@@ -120,11 +123,12 @@ def test_batch_median(built, kw):
     check_against_oracle(p, I0s, I1s, u, v, st)
 
 
-@pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0"])
+@pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0", "TVL1_BATCH_PX1_W=0"])
 def test_batch_fast_math_within_tolerance(built, monkeypatch, env):
     """fast_math = 1 batches: the oracle's iteration schedule, mean EPE <= 1e-3 px
     (tests/test_gpu_fastmath.py's bar)."""
     monkeypatch.delenv("TVL1_BATCH_FUSE", raising=False)
+    monkeypatch.delenv("TVL1_BATCH_PX1_W", raising=False)
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
     kw = dict(nscales=10, warps=5)
