@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void kb_iterate_roll(BatchRoll br) {
   const int wid =
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
   if (wid >= ra.waves) return;
-  roll_body<false, K, PX, FM>(ra, wid);
+  roll_body<false, K, PX, FM, 0, kb_roll_ahead<K, PX>()>(ra, wid);
 }
 
 // build-only median filter (k_median) of every selected pair's current u set into the

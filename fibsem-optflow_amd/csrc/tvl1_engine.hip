@@ -145,6 +145,8 @@ struct tvl1_ctx {
   int batch_px1_w = kBatchPx1W;         // TVL1_BATCH_PX1_W: batched passes on levels at most
                                         // this wide run 64-px bands (1 px per lane)
   int kb1_slots[kRollMax + 1] = {};     // resident kb_iterate_roll<K, 1> wavefronts
+  int probe_lds = 0;                    // TVL1_PROBE_ROLL_LDS: dynamic LDS per k_iterate_roll
+                                        // block (occupancy probe only)
   char *gather_scratch = nullptr;       // tvl1_gather_flow's offsets and values
   size_t gather_bytes = 0;
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
@@ -1035,8 +1037,11 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           const dim3 grid((ra.waves + 3) / 4);
 #define ROLL_G(K, PX) \
   hipLaunchKernelGGL((k_iterate_roll<true, K, PX>), grid, dim3(256), 0, st, ra);
-#define ROLL_M(FM, K, PX) \
-  hipLaunchKernelGGL((k_iterate_roll<false, K, PX, FM>), grid, dim3(256), 0, st, ra);
+#define ROLL_M(FM, K, PX)                                                                  \
+  if (c->probe_lds > 0)                                                                    \
+    (void)hipFuncSetAttribute((const void *)k_iterate_roll<false, K, PX, FM>,              \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, c->probe_lds);   \
+  hipLaunchKernelGGL((k_iterate_roll<false, K, PX, FM>), grid, dim3(256), c->probe_lds, st, ra);
 #define ROLL(K, PX)                     \
   if (gam) {                            \
     ROLL_G(K, PX)                       \
@@ -2257,6 +2262,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_BATCH_STORE")) c->batch_store_pred = atoi(m) == 0;
   if (const char *m = getenv("TVL1_BATCH_GROUP")) c->batch_group = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BATCH_PX1_W")) c->batch_px1_w = atoi(m);
+  if (const char *m = getenv("TVL1_PROBE_ROLL_LDS")) c->probe_lds = atoi(m);
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);

@@ -1687,6 +1687,11 @@ constexpr int kRollAhead = 2;   // input rows loaded ahead of the row entering t
 // flight one row ahead as 8-byte loads two rows ahead, with one ring row less
 template <int K, int PX>
 constexpr int roll_ahead() { return PX == 4 ? 1 : kRollAhead; }
+// ... by kb_iterate_roll: one row for the 3- and 4-iteration passes on 128-px bands (174
+// instead of 189 VGPRs, the same 2 wavefronts per SIMD): strips +1.1 %, where the single-pair
+// passes measured -0.3 % (profiles/r4/ab/roll_ahead_r4l/)
+template <int K, int PX>
+constexpr int kb_roll_ahead() { return K >= 3 && PX == 2 ? 1 : roll_ahead<K, PX>(); }
 
 // The planes of a streaming pass as five buffer groups, one 4-SGPR descriptor each: the
 // warp constants (I1wx, I1wy, rho), the u set read and the u set written (u1, u2, u3), the
@@ -1803,13 +1808,12 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
                                              const IterArgs &a, const RollBufs &B, int r,
                                              const RollLane &L, unsigned rowb, double &acc);
 
-template <bool G, int K, int PX, int FM>
+template <bool G, int K, int PX, int FM, int AH>
 __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                           RollIn<G, PX> &ahead, const IterArgs &a,
                                           const RollBufs &B, int r, const RollLane &L,
                                           unsigned rowb, double &acc) {
-  roll_load<G, PX>(ahead, B, (unsigned)imin(r + roll_ahead<K, PX>(), a.H - 1) * rowb, L.vload,
-                   L.vloadp);
+  roll_load<G, PX>(ahead, B, (unsigned)imin(r + AH, a.H - 1) * rowb, L.vload, L.vloadp);
   // keep the loads of row r + roll_ahead ahead of this step's stores: waiting for them
   // roll_ahead steps later then leaves the younger stores and loads in flight (vmcnt
   // counts in issue order)
@@ -1943,7 +1947,8 @@ constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
 // waves dispatched last on a SIMD would finish last (one C2 pair alone: <4,2> 317 -> 307 us,
 // <2,2> 52.2 -> 50.5 us per launch; in flight neutral; the batched passes keep 0, where it
 // measured -0.7 %: profiles/r3/ab_roll_prio.txt)
-template <bool G, int K, int PX, int FM, int PRIO = 0>
+// AH: input rows loaded ahead (1: a 2-row ring, 2: a 3-row ring)
+template <bool G, int K, int PX, int FM, int PRIO = 0, int AH = roll_ahead<K, PX>()>
 __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
   constexpr int HALO = roll_halo<K, PX>();
   constexpr int BW = 64 * PX;            // band width (px)
@@ -2010,18 +2015,18 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
     }
   };
   double acc = 0.0;
-  if constexpr (roll_ahead<K, PX>() == 1) {   // 2-row ring, steps unrolled by 2
+  if constexpr (AH == 1) {   // 2-row ring, steps unrolled by 2
     RollIn<G, PX> A, Bx;
     roll_load<G, PX>(A, B, (unsigned)r0 * rowb, L.vload, L.vloadp);
     dummy_stores();
     const int halves = (L.ye + K - r0 + 1) / 2;
     for (int h = 0, r = r0; h < halves; ++h, r += 2) {
       progress_prio<PRIO>(h, halves);
-      roll_step<G, K, PX, FM>(S, A, Bx, a, B, r, L, rowb, acc);
-      roll_step<G, K, PX, FM>(S, Bx, A, a, B, r + 1, L, rowb, acc);
+      roll_step<G, K, PX, FM, AH>(S, A, Bx, a, B, r, L, rowb, acc);
+      roll_step<G, K, PX, FM, AH>(S, Bx, A, a, B, r + 1, L, rowb, acc);
     }
   } else {   // 3-row ring, steps unrolled by 3
-    static_assert(roll_ahead<K, PX>() == 2, "the step loop below is unrolled for a 3-row ring");
+    static_assert(AH == 2, "the step loop below is unrolled for a 3-row ring");
     RollIn<G, PX> A, Bx, C;
     roll_load<G, PX>(A, B, (unsigned)r0 * rowb, L.vload, L.vloadp);
     dummy_stores();
@@ -2031,9 +2036,9 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
     const int thirds = (L.ye + K - r0 + 2) / 3;
     for (int h = 0, r = r0; h < thirds; ++h, r += 3) {
       progress_prio<PRIO>(h, thirds);
-      roll_step<G, K, PX, FM>(S, A, C, a, B, r, L, rowb, acc);
-      roll_step<G, K, PX, FM>(S, Bx, A, a, B, r + 1, L, rowb, acc);
-      roll_step<G, K, PX, FM>(S, C, Bx, a, B, r + 2, L, rowb, acc);
+      roll_step<G, K, PX, FM, AH>(S, A, C, a, B, r, L, rowb, acc);
+      roll_step<G, K, PX, FM, AH>(S, Bx, A, a, B, r + 1, L, rowb, acc);
+      roll_step<G, K, PX, FM, AH>(S, C, Bx, a, B, r + 2, L, rowb, acc);
     }
   }
   if (a.calc_err) {
