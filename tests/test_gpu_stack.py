@@ -74,6 +74,27 @@ def test_plain_launch_runs_n_ranks(built, tmp_path):
     assert {int(np.load(f)["rank"]) for f in tmp_path.glob("*.npz")} <= {0, 1}
 
 
+def test_plain_launch_default_pair_line(built):
+    """The driver's multi-GPU command as written (`bench.py --gpus N --steps K --warmup W`, no
+    launcher, the default pair workload with its extra lines): 2 ranks (gloo, on the one GPU),
+    every collective of the math-mode and production-strip legs reached by both ranks, one
+    JSON line from rank 0 claiming both GPUs, no CPU baseline above one GPU."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--width", "320", "--height", "240", "--inflight", "2"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=200, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["process_group"] == "gloo"
+    assert out["value"] > 0 and out["cpu_baseline"] is None
+    assert set(out["math_modes"]) == {"fast", "fma"}
+    assert out["production_strips"]["value"] > 0
+
+
 def expected_pairs():
     return {(s, z) for s in STRIDES for z in range(Z - s)}
 
