@@ -172,6 +172,8 @@ struct BatchRoll {
 };
 template <int K, int PX, int FM>
 __global__ __launch_bounds__(256) void kb_iterate_roll(BatchRoll br) {
+  constexpr bool LDSR = roll_lds_on<false, K, PX>();
+  __shared__ float lds[LDSR ? 4 * kRollLdsWave : 1];
   const int b = br.sel.idx[blockIdx.y];
   RollArgs ra = br.ra;
   IterArgs &a = ra.it;
@@ -206,7 +208,8 @@ __global__ __launch_bounds__(256) void kb_iterate_roll(BatchRoll br) {
   const int wid =
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
   if (wid >= ra.waves) return;
-  roll_body<false, K, PX, FM, 0, kb_roll_ahead<K, PX>()>(ra, wid);
+  roll_body<false, K, PX, FM, 0, kb_roll_ahead<K, PX>(), LDSR>(
+      ra, wid, lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (LDSR ? kRollLdsWave : 0));
 }
 
 // build-only median filter (k_median) of every selected pair's current u set into the

@@ -1936,6 +1936,98 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
   }
 }
 
+// ---- LDS-staged input rows (LDSR; the 3- and 4-iteration passes on 128-px bands).
+// The register ring of rows loaded ahead (RollIn A, Bx, C: 54 VGPRs of <4, 2>'s 189) is
+// what holds those passes at 2 wavefronts per SIMD, and they are bound per wavefront (one
+// wavefront per SIMD: 1.65x the time).  Here the rows go HBM -> LDS by the
+// buffer unit's LDS path (buffer_load_dwordx4 ... lds: 1 KiB per wave-instruction, lanes
+// 0-31 one plane's 128 px, lanes 32-63 the next plane's), two slots per wavefront: the
+// row read at step r is at least 2 steps old, and the slot read is refilled (row r + 2)
+// right after the read.  The reads are inline ds_read_b64 (the lane's 2 px of each of the 9
+// planes) with their own lgkmcnt wait, and the wait for the row's DMA is a counted vmcnt
+// written here: the compiler's wait pass, which would otherwise wait for every DMA in
+// flight before any LDS read, sees neither.  Same operands, same arithmetic: same bits.
+constexpr int kRollLdsSlot = 1280;                 // floats: 5 pieces of 2 x 128
+constexpr int kRollLdsWave = 2 * kRollLdsSlot;     // two slots per wavefront
+constexpr int kRollDmaPerRow = 5;                  // DMA pieces per row (G = false)
+constexpr int kRollStPerStep = 6;                  // b64 stores per step: u1, u2, p11..p22
+#ifndef TVL1_ROLL_LDS
+#define TVL1_ROLL_LDS 1
+#endif
+template <bool G, int K, int PX>
+constexpr bool roll_lds_on() { return TVL1_ROLL_LDS && !G && K >= 3 && PX == 2; }
+
+struct RollDma {   // per-lane byte offsets of the 5 pieces (the row in the scalar offset)
+  unsigned c1, c2, u, p1, p2;
+};
+
+__device__ __forceinline__ void roll_dma_piece(const float *base, unsigned bytes, float *lds,
+                                               unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(plane_rsrc(base, bytes),
+                                           (__attribute__((address_space(3))) void *)lds, 16,
+                                           (int)voff, (int)soff, 0, 0);
+}
+
+// row (scalar offset soff) -> LDS slot: [wx | wy] [rh | -] [u1 | u2] [p11 | p12] [p21 | p22]
+__device__ __forceinline__ void roll_dma_row(float *slot, const RollBufs &B, unsigned soff,
+                                             const RollDma &D) {
+  roll_dma_piece(B.c, B.cb, slot, D.c1, soff);
+  roll_dma_piece(B.c, B.cb, slot + 256, D.c2, soff);
+  roll_dma_piece(B.us, B.ub, slot + 512, D.u, soff);
+  roll_dma_piece(B.ps, B.pb, slot + 768, D.p1, soff);
+  roll_dma_piece(B.ps, B.pb, slot + 1024, D.p2, soff);
+}
+
+// the lane's 2 px of the 9 planes of a slot (addr: LDS byte address of the slot + 8 * lane)
+__device__ __forceinline__ void roll_lds_read(RollIn<false, 2> &in, unsigned addr, bool pz) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 wx, wy, rh, u1, u2, p11, p12, p21, p22;
+  asm volatile(
+      "ds_read_b64 %0, %9\n"
+      "ds_read_b64 %1, %9 offset:512\n"
+      "ds_read_b64 %2, %9 offset:1024\n"
+      "ds_read_b64 %3, %9 offset:2048\n"
+      "ds_read_b64 %4, %9 offset:2560\n"
+      "ds_read_b64 %5, %9 offset:3072\n"
+      "ds_read_b64 %6, %9 offset:3584\n"
+      "ds_read_b64 %7, %9 offset:4096\n"
+      "ds_read_b64 %8, %9 offset:4608\n"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(wx), "=v"(wy), "=v"(rh), "=v"(u1), "=v"(u2), "=v"(p11), "=v"(p12), "=v"(p21),
+        "=v"(p22)
+      : "v"(addr)
+      : "memory");
+  in.wx[0] = wx.x; in.wx[1] = wx.y;
+  in.wy[0] = wy.x; in.wy[1] = wy.y;
+  in.rh[0] = rh.x; in.rh[1] = rh.y;
+  in.u1[0] = u1.x; in.u1[1] = u1.y;
+  in.u2[0] = u2.x; in.u2[1] = u2.y;
+  in.u3[0] = in.u3[1] = 0.0f;
+  // p = 0 on a level's first pass (its pieces were loaded from kOOB)
+  in.p11[0] = pz ? 0.0f : p11.x; in.p11[1] = pz ? 0.0f : p11.y;
+  in.p12[0] = pz ? 0.0f : p12.x; in.p12[1] = pz ? 0.0f : p12.y;
+  in.p21[0] = pz ? 0.0f : p21.x; in.p21[1] = pz ? 0.0f : p21.y;
+  in.p22[0] = pz ? 0.0f : p22.x; in.p22[1] = pz ? 0.0f : p22.y;
+  in.p31[0] = in.p31[1] = in.p32[0] = in.p32[1] = 0.0f;
+}
+
+// One step at input row r from LDS slot `slot` (LDS byte address `addr` + 8 * lane): wait for
+// the row's DMA (issued 2 steps ago: the stores of that step, the next row's pieces and the
+// stores of the step between are younger), read it, refill the slot with row r + 2, advance.
+template <int K, int FM>
+__device__ __forceinline__ void roll_step_lds(RollPipe<false, K, 2> &S, float *slot, unsigned addr,
+                                              const IterArgs &a, const RollBufs &B, int r,
+                                              const RollLane &L, unsigned rowb, const RollDma &D,
+                                              double &acc) {
+  static_assert(2 * kRollStPerStep + kRollDmaPerRow == 17, "the vmcnt below");
+  asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+  RollIn<false, 2> in;
+  roll_lds_read(in, addr, a.p_zero != 0);
+  roll_dma_row(slot, B, (unsigned)imin(r + 2, a.H - 1) * rowb, D);
+  __builtin_amdgcn_sched_barrier(0);
+  roll_advance<false, K, 2, false, FM>(S, in, a, B, r, L, rowb, acc);
+}
+
 // halo of a band: K px, rounded up to whole lanes' worth of px (8-byte aligned loads)
 template <int K, int PX>
 constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
@@ -1947,9 +2039,11 @@ constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
 // waves dispatched last on a SIMD would finish last (one C2 pair alone: <4,2> 317 -> 307 us,
 // <2,2> 52.2 -> 50.5 us per launch; in flight neutral; the batched passes keep 0, where it
 // measured -0.7 %: profiles/r3/ab_roll_prio.txt)
-// AH: input rows loaded ahead (1: a 2-row ring, 2: a 3-row ring)
-template <bool G, int K, int PX, int FM, int PRIO = 0, int AH = roll_ahead<K, PX>()>
-__device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
+// AH: input rows loaded ahead (1: a 2-row ring, 2: a 3-row ring); LDSR: rows staged in
+// LDS (lds: this wavefront's kRollLdsWave floats), see roll_step_lds
+template <bool G, int K, int PX, int FM, int PRIO = 0, int AH = roll_ahead<K, PX>(),
+          bool LDSR = false>
+__device__ __forceinline__ void roll_body(const RollArgs &ra, int wid, float *lds = nullptr) {
   constexpr int HALO = roll_halo<K, PX>();
   constexpr int BW = 64 * PX;            // band width (px)
   // The long pipelines (and the gamma ones) run at 2 waves/SIMD with VGPRs to spare but
@@ -2015,7 +2109,36 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
     }
   };
   double acc = 0.0;
-  if constexpr (AH == 1) {   // 2-row ring, steps unrolled by 2
+  if constexpr (LDSR) {   // two LDS slots, steps unrolled by 2
+    static_assert(!G && PX == 2, "LDS-staged rows: the 9 planes of G = false, 2 px per lane");
+    const int X0 = band * (BW - 2 * HALO) - HALO;
+    const bool hi = lane >= 32;
+    const unsigned col = 4u * (unsigned)imin(imax(X0 + 4 * (lane & 31), 0), a.P - 4);
+    const unsigned ps = B.pstride;
+    RollDma D;
+    D.c1 = col + (hi ? ps : 0u);
+    D.c2 = hi ? kOOB : col + 2 * ps;
+    D.u = col + (hi ? ps : 0u);
+    D.p1 = a.p_zero ? kOOB : col + (hi ? ps : 0u);
+    D.p2 = a.p_zero ? kOOB : col + 2 * ps + (hi ? ps : 0u);
+    float *s0 = lds, *s1 = lds + kRollLdsSlot;
+    const unsigned a0 =
+        (unsigned)(size_t)(__attribute__((address_space(3))) float *)s0 + 8u * (unsigned)lane;
+    const unsigned a1 = a0 + 4u * kRollLdsSlot;
+    roll_dma_row(s0, B, (unsigned)r0 * rowb, D);
+    dummy_stores();
+    roll_dma_row(s1, B, (unsigned)imin(r0 + 1, a.H - 1) * rowb, D);
+    dummy_stores();
+    const int halves = (L.ye + K - r0 + 1) / 2;
+    for (int h = 0, r = r0; h < halves; ++h, r += 2) {
+      progress_prio<PRIO>(h, halves);
+      roll_step_lds<K, FM>(S, s0, a0, a, B, r, L, rowb, D, acc);
+      roll_step_lds<K, FM>(S, s1, a1, a, B, r + 1, L, rowb, D, acc);
+    }
+    // the last steps' refills (rows past the segment) land before the block's LDS is
+    // released to another block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if constexpr (AH == 1) {   // 2-row ring, steps unrolled by 2
     RollIn<G, PX> A, Bx;
     roll_load<G, PX>(A, B, (unsigned)r0 * rowb, L.vload, L.vloadp);
     dummy_stores();
@@ -2050,11 +2173,14 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid) {
 
 template <bool G, int K, int PX, int FM = 0>
 __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
+  constexpr bool LDSR = roll_lds_on<G, K, PX>();
+  __shared__ float lds[LDSR ? 4 * kRollLdsWave : 1];
   // wave-uniform (scalar) band / segment
   const int wid =
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
   if (wid >= ra.waves || gated_off(ra.it.gate, ra.it.gate_seq)) return;   // whole wavefronts
-  roll_body<G, K, PX, FM, 1>(ra, wid);
+  roll_body<G, K, PX, FM, 1, roll_ahead<K, PX>(), LDSR>(
+      ra, wid, lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (LDSR ? kRollLdsWave : 0));
 }
 
 // ---------------------------------------------------------------- K5 + first pass, two roles
