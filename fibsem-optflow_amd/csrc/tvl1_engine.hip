@@ -147,6 +147,7 @@ struct tvl1_ctx {
   int kb1_slots[kRollMax + 1] = {};     // resident kb_iterate_roll<K, 1> wavefronts
   int probe_lds = 0;                    // TVL1_PROBE_ROLL_LDS: dynamic LDS per k_iterate_roll
                                         // block (occupancy probe only)
+  int probe_wi_lds = 0;                 // TVL1_PROBE_WI_LDS: the same for k_warp_iter (< 64 KiB)
   char *gather_scratch = nullptr;       // tvl1_gather_flow's offsets and values
   size_t gather_bytes = 0;
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
@@ -995,7 +996,8 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
                            c->partials_cap);
 #define WITER(FM)                                                                           \
   if (c->wi_nc == 2)                                                                       \
-    hipLaunchKernelGGL((k_warp_iter<M, FM, BW, 1, 2>), dim3(w.ra.waves), dim3(128 + BW), 0, st, w); \
+    hipLaunchKernelGGL((k_warp_iter<M, FM, BW, 1, 2>), dim3(w.ra.waves), dim3(128 + BW),    \
+                       c->probe_wi_lds, st, w);                                             \
   else                                                                                     \
     hipLaunchKernelGGL((k_warp_iter<M, FM, BW, 1, 1>), dim3(w.ra.waves), dim3(64 + BW), 0, st, w);
           MATH_SWITCH(math, WITER)
@@ -2263,6 +2265,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_BATCH_GROUP")) c->batch_group = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BATCH_PX1_W")) c->batch_px1_w = atoi(m);
   if (const char *m = getenv("TVL1_PROBE_ROLL_LDS")) c->probe_lds = atoi(m);
+  if (const char *m = getenv("TVL1_PROBE_WI_LDS")) c->probe_wi_lds = std::min(atoi(m), 32768);
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
     c->buf_limit = std::min(c->buf_limit, (size_t)std::max(0LL, atoll(m)));
   if (const char *m = getenv("TVL1_CHECK")) c->check = atoi(m);

@@ -99,9 +99,10 @@ def test_final_roofline_reproduces_by_hand(FINAL, which):
     by_hand = roof["bytes_per_launch"] / (avg_us * 1e-6) / 8e12
     assert abs(roof["frac"] / by_hand - 1) < 0.05, (which, roof["frac"], by_hand)
     # the bytes: the engine's accounting against the PMC bytes of the same launch class (the
-    # strip batch's tiny levels fetch ~6 % beyond the tiling's compulsory bytes)
+    # strip batch's tiny levels fetch ~6-7 % beyond the tiling's compulsory bytes, DESIGN 5:
+    # since r4 their 64-px bands (256-B rows at 224-B steps) straddle one more 128-B line)
     pmc_frac = traffic["iterate_hbm_bytes_per_launch"] / (avg_us * 1e-6) / 8e12
-    assert abs(roof["bytes_per_launch"] / traffic["iterate_hbm_bytes_per_launch"] - 1) < 0.07
+    assert abs(roof["bytes_per_launch"] / traffic["iterate_hbm_bytes_per_launch"] - 1) < 0.08
     assert abs(roof["frac"] / pmc_frac - 1) < 0.10, (which, roof["frac"], pmc_frac)
     assert 0 < traffic["iterate_valu_frac"] < 1
     assert roof["model_bytes_over_peak"] > 1.0 > roof["frac"]
