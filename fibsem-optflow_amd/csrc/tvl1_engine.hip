@@ -2308,6 +2308,13 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     c->warp_ring_slots = blocks_of((const void *)k_warp_ring<6, 2>, 128);
     c->witer_slots = c->wi_nc == 2 ? blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 2>, 256)
                                    : blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 1>, 192);
+    if (c->probe_wi_lds > 0 && c->wi_nc == 2) {   // the probe's segments fill its own residency
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)k_warp_iter<6, 0, 128, 1, 2>,
+                                                       256, c->probe_wi_lds) == hipSuccess && nb > 0)
+        c->witer_slots = nb * prop.multiProcessorCount;
+      (void)hipGetLastError();
+    }
     // >= 3-iteration passes stream when the level has at least 4 wavefronts' worth of 56 x 32
     // tiles per SIMD (the measured crossover against 64 x 32 blocked regions)
     c->roll_long_min = 16L * prop.multiProcessorCount;
