@@ -42,10 +42,11 @@ constexpr int kStripRows = 32;   // rows per wave strip in k_iterate
 constexpr int kTbMax = 4;        // max iterations fused per pass in k_iterate_tb
 constexpr int kRollMinSeg = 8;   // smallest k_iterate_roll segment (rows)
 // Batched passes on levels at most this wide use 64-px bands, kb_iterate_roll<K, 1> (95
-// VGPRs, 5 wavefronts per SIMD, against 189 and 2 for <4, 2>): the production strips' levels
-// of 515-1573 x 17-51 px give a batch too few 128-px bands to fill the SIMDs, so twice the
-// wavefronts with half the work each finish sooner.  Measured on the strip workload: cut-off
-// 1700 +2.4 %, 1100 +1.2 %, 2500 +1.8 %, every level -3 %.
+// VGPRs, 5 wavefronts per SIMD, against 3 for the LDS-staged <4, 2>): the production strips'
+// levels of 515-1573 x 17-51 px give a batch too few 128-px bands to fill the SIMDs, so twice
+// the wavefronts with half the work each finish sooner.  Measured on the strip workload (with
+// the register-ring <4, 2>): cut-off 1700 +2.4 %, 1100 +1.2 %, 2500 +1.8 %, every level -3 %;
+// with the LDS-staged one 1700 and 1100 +1.3 %, 2500 +0.2 %.
 constexpr int kBatchPx1W = 1700;
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -146,7 +147,8 @@ struct tvl1_ctx {
                                         // this wide run 64-px bands (1 px per lane)
   int kb1_slots[kRollMax + 1] = {};     // resident kb_iterate_roll<K, 1> wavefronts
   int probe_lds = 0;                    // TVL1_PROBE_ROLL_LDS: dynamic LDS per k_iterate_roll
-                                        // block (occupancy probe only)
+                                        // block (occupancy probe only; with the LDS-staged
+                                        // passes' 40 KiB, at most 120 KiB)
   int probe_wi_lds = 0;                 // TVL1_PROBE_WI_LDS: the same for k_warp_iter (< 64 KiB)
   char *gather_scratch = nullptr;       // tvl1_gather_flow's offsets and values
   size_t gather_bytes = 0;
