@@ -41,6 +41,12 @@ thread_local std::string g_create_error;
 constexpr int kStripRows = 32;   // rows per wave strip in k_iterate
 constexpr int kTbMax = 4;        // max iterations fused per pass in k_iterate_tb
 constexpr int kRollMinSeg = 8;   // smallest k_iterate_roll segment (rows)
+#ifndef TVL1_WI_M
+#define TVL1_WI_M 6
+#endif
+// k_warp_iter's window margin (px): flows within about +-(M - 1) px gather from its LDS
+// window ring, larger ones from HBM (the same taps)
+constexpr int kWiMargin = TVL1_WI_M;
 // Batched passes on levels at most this wide use 64-px bands, kb_iterate_roll<K, 1> (95
 // VGPRs, 5 wavefronts per SIMD, against 3 for the LDS-staged <4, 2>): the production strips'
 // levels of 515-1573 x 17-51 px give a batch too few 128-px bands to fill the SIMDs, so twice
@@ -985,7 +991,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           // a level's first warp, else when the previous warp did not stop at its first
           // check (a wrong guess recomputes them with the warp kernel after the check)
           w.store_c = store_c ? 1 : 0;
-          constexpr int M = 6, BW = 128;
+          constexpr int M = kWiMargin, BW = 128;
           w.ra.bands = (lw + BW - 5) / (BW - 4);
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
                                           : roll_segment(w.ra.bands, lh, 2 + M, c->witer_slots * fill_now() / 100);
@@ -2308,11 +2314,11 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     c->kb1_slots[3] = 4 * blocks_of((const void *)kb_iterate_roll<3, 1, kIEEE>, 256);
     c->kb1_slots[4] = 4 * blocks_of((const void *)kb_iterate_roll<4, 1, kIEEE>, 256);
     c->warp_ring_slots = blocks_of((const void *)k_warp_ring<6, 2>, 128);
-    c->witer_slots = c->wi_nc == 2 ? blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 2>, 256)
-                                   : blocks_of((const void *)k_warp_iter<6, 0, 128, 1, 1>, 192);
+    c->witer_slots = c->wi_nc == 2 ? blocks_of((const void *)k_warp_iter<kWiMargin, 0, 128, 1, 2>, 256)
+                                   : blocks_of((const void *)k_warp_iter<kWiMargin, 0, 128, 1, 1>, 192);
     if (c->probe_wi_lds > 0 && c->wi_nc == 2) {   // the probe's segments fill its own residency
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)k_warp_iter<6, 0, 128, 1, 2>,
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)k_warp_iter<kWiMargin, 0, 128, 1, 2>,
                                                        256, c->probe_wi_lds) == hipSuccess && nb > 0)
         c->witer_slots = nb * prop.multiProcessorCount;
       (void)hipGetLastError();
