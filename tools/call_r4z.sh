@@ -2,10 +2,11 @@
 # r4 A/B: k_warp_iter producers one issue-priority level above the consumers (ab_pp; the
 # barrier probe: producers wait least, they set the pace) against the in-tree build.
 # Parity subset on the variant, kernel trace of one C2 pair each, C2 alternations.
+# (ab_pp: tools/build_variant.sh ab_pp "-DTVL1_WI_PPRIO=1" ..., a since-removed knob.)
 set -o pipefail
 out=gpurun_out/r4z
 mkdir -p $out
-export TVL1_ENGINE_SO=<variant dir>/libtvl1_hip.so
+export TVL1_ENGINE_SO=ab_pp/libtvl1_hip.so
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_batch.py -x -q --timeout 200 --timeout-method thread > $out/t_pp.log 2>&1 || { echo "PARITY_FAIL"; tail -30 $out/t_pp.log; exit 1; }
 echo "pp parity: $(tail -1 $out/t_pp.log)"
 unset TVL1_ENGINE_SO
