@@ -106,7 +106,8 @@ def roofline(k_bytes, k_hbm, k_ms, k_launch, traffic, kernel):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     # defaults None: C2's 6144x4096 / 5 scales / 30 warps, or for --workload strips the
@@ -157,6 +158,11 @@ def parse():
                          "rank to DIR/pair_s<s>_z<z>.npz (tests/test_gpu_stack.py; not timed "
                          "for the bench line)")
     args = ap.parse_args()
+    # `torchrun --nproc-per-node N bench.py` without --gpus: the launcher's WORLD_SIZE (an
+    # explicit --gpus that disagrees with it stays an error in main())
+    args.gpus_explicit = args.gpus is not None
+    if args.gpus is None:
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     geo = (3072, 100, 10, 5) if args.workload == "strips" else (6144, 4096, 5, 30)
     for k, d in zip(("width", "height", "nscales", "warps"), geo):
         if getattr(args, k) is None:
@@ -165,6 +171,45 @@ def parse():
         # pairs: 3 (+1.5 % over 2 on the C2 pair, 4 is slower); strip batches: 2
         args.inflight = 2 if args.workload == "strips" else 3
     return args
+
+
+def cpu_allotment():
+    """The host CPUs this process may use, and the oracle thread count taken from them
+    (the CPU baseline runs on all the host cores it is given).  A gpurun box
+    shows the whole machine to os.cpu_count() but allots a share through the cgroup CPU
+    quota and OMP_NUM_THREADS; every figure is recorded so the line explains its `cores`."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:   # cgroup v2: "<quota> <period>" or "max <period>"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    omp = int(env) if env and env.isdigit() and int(env) > 0 else None
+    threads = min(x for x in (aff, quota, omp) if x is not None)
+    return {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "omp_num_threads_env": omp,
+            "machine_cpus": os.cpu_count(), "threads": threads}
+
+
+def rank_records(dist, local_rank, pairs, iterations, elapsed):
+    """One record per rank, gathered after the timed region: the device
+    each rank solved on (PCI domain:bus:device, which must be N distinct GPUs on an N-GPU
+    line under nccl; ranks share the one card under the gloo rehearsal), the pairs it solved
+    and its own elapsed time, so the line shows placement and balance, not only the
+    max-over-ranks time."""
+    import torch
+    pr = torch.cuda.get_device_properties(local_rank)
+    rec = {"rank": int(os.environ.get("RANK", "0")), "local_rank": local_rank,
+           "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}",
+           "device": pr.name, "pairs": pairs, "iterations": iterations,
+           "elapsed_s": round(elapsed, 4)}
+    if not dist:
+        return [rec]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, rec)
+    return out
 
 
 _NATIVE_ORACLE = None
@@ -221,6 +266,8 @@ def cpu_baseline(I0, I1, params, sample: str):
     b = np.ascontiguousarray(I1[:sh, :sw])
     so, build = native_oracle()
     lib = checker.load_oracle(so)
+    allot = cpu_allotment()
+    lib.orc_set_num_threads(allot["threads"])
     threads = int(lib.orc_num_threads())
     t0 = time.perf_counter()
     _, _, st, _ = checker.oracle_calc(a, b, params, warp_iters=False, so=so)
@@ -230,6 +277,7 @@ def cpu_baseline(I0, I1, params, sample: str):
         "value": 1.0 / (dt * scale),
         "unit": "slice-pairs/s",
         "cores": threads,
+        "allotment": allot,
         "kind": "port",
         "build": build,
         "sample": ((f"oracle/ CPU restatement, {threads} OpenMP threads, one {sw}x{sh} crop of "
@@ -341,6 +389,7 @@ def run_stack(args, rank, world, local_rank, dist):
     elapsed = time.perf_counter() - t0
     if errors:
         raise RuntimeError("; ".join(errors))
+    ranks = rank_records(dist, local_rank, sum(done), sum(iters), elapsed)
     mine = torch.tensor([float(sum(done)), float(sum(iters)), elapsed], dtype=torch.float64,
                         device="cpu" if RED_CPU else dev)
     if dist:
@@ -382,6 +431,7 @@ def run_stack(args, rank, world, local_rank, dist):
             "pairs": int(pairs_done),
             "iterations_per_pair": round(iters_done / max(1.0, pairs_done), 1),
         },
+        "ranks": ranks,
     }
     print(json.dumps(out), flush=True)
 
@@ -443,6 +493,7 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ranks = rank_records(dist, local_rank, args.steps * F * B, iters, elapsed)
     # one batch alone on the GPU after the timed steps, with HIP events around every launch
     # (tvl1_set_profiling): the batched iteration class's roofline
     roof = None
@@ -474,13 +525,16 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
         a, c = st0[0].cpu().numpy(), st0[1].cpu().numpy()
         so, build = native_oracle()
         lib = checker.load_oracle(so)
+        allot = cpu_allotment()
+        lib.orc_set_num_threads(allot["threads"])
         t1 = time.perf_counter()
         n_rep = 4
         for _ in range(n_rep):
             checker.oracle_calc(a, c, params, warp_iters=False, so=so)
         dt = (time.perf_counter() - t1) / n_rep
         cpu = {"value": round(1.0 / dt, 3), "unit": "strip solves/s",
-               "cores": int(lib.orc_num_threads()), "kind": "port", "build": build,
+               "cores": int(lib.orc_num_threads()), "allotment": allot, "kind": "port",
+               "build": build,
                "sample": f"oracle/ CPU restatement, {n_rep} solves of one {W}x{H} strip pair"}
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "strip solves/s",
@@ -497,6 +551,7 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
                    "iterations_per_strip": round(iters / (args.steps * F * B), 1)},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "ranks": ranks,
     }
     if standalone:
         print(json.dumps(out), flush=True)
@@ -520,6 +575,7 @@ def strips_line(args, rank, world, local_rank, dist):
             "iterations_per_strip": o["config"]["iterations_per_strip"],
             "roofline": o["roofline"],
             "cpu_baseline": o["cpu_baseline"],
+            "ranks": o["ranks"],
             "api": "tvl1_calc_batch (DESIGN.md 4.6)"}
 
 
@@ -652,14 +708,16 @@ def main():
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        elapsed = time.perf_counter() - t0
+        own = elapsed = time.perf_counter() - t0
         if dist:
             t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if RED_CPU else dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        return elapsed, stats
+        return elapsed, stats, own
 
-    elapsed, stats = timed(args.warmup, args.steps)
+    elapsed, stats, own = timed(args.warmup, args.steps)
+    ranks = rank_records(dist, local_rank, len(stats), sum(s["iterations_total"] for s in stats),
+                         own)
     I0h, I1h = slots[0]["I0h"], slots[0]["I1h"]
     # one pair alone on the GPU, twice (not timed): with HIP events around every launch for
     # clean per-kernel-class durations (the roofline; no interleaving with other pairs), then
@@ -696,7 +754,7 @@ def main():
             for sl in slots:
                 sl["eng"].set_params(mp)
                 sl["eng"].set_profiling(False)
-            m_elapsed, m_stats = timed(1, args.steps)
+            m_elapsed, m_stats, _ = timed(1, args.steps)
             solve(slots[0])
             torch.cuda.synchronize(dev)
             e = torch.sqrt((slots[0]["u"] - u_ref) ** 2 + (slots[0]["v"] - v_ref) ** 2).flatten()
@@ -786,6 +844,8 @@ def main():
         "cpu_baseline": None,
         "math_modes": modes,
         "production_strips": strips,
+        # per rank: device (PCI id), pairs solved, own elapsed time of the timed steps
+        "ranks": ranks,
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(I0h, I1h, params, args.cpu_sample)

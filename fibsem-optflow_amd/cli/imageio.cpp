@@ -938,6 +938,10 @@ static int tiff_rows(const std::string &path, int &W, int &H,
     return 1;
   if (!rps || rps > h) rps = h;
   if ((uint64_t)offs.size() * rps < h) return 1;   // whole decode reports the missing rows
+  // every strip inside the file, not only the ones the bands need: a truncated or corrupt
+  // file takes the whole decode, which reports it, as the per-pair path does
+  for (size_t s = 0; s < offs.size(); ++s)
+    if ((uint64_t)offs[s] + cnts[s] > f.size) return 1;
   W = (int)w, H = (int)h;
   rows.assign(h, {});
   std::vector<uint8_t> strip;
@@ -959,6 +963,8 @@ static int tiff_rows(const std::string &path, int &W, int &H,
           err = "TIFF: strip out of range";
           return -1;
         }
+        if (pred == 2)   // horizontal differencing, per row, as the whole decode applies it
+          for (uint32_t i = 1; i < w; ++i) o[i] = (uint8_t)(o[i] + o[i - 1]);
       } else {
         if (have_strip != (long)s) {
           std::vector<uint8_t> src(cnts[s]);

@@ -384,12 +384,6 @@ void random_points(const float *fx, const float *fy, int W, int H,
   emit_points(pts, vx, vy, !loc.empty(), im, r0, r1, inv_scale, features);
 }
 
-// random_points without the debug flag, where the reference seeds rand() with the time
-// (optflow.cpp:532-535) and keeps the first npoints of a random_shuffle of all the masked
-// px: npoints distinct uniformly random masked px in random order is the same distribution.
-// Drawn by a partial Fisher-Yates over the implicit list (row counts + a sparse swap map),
-// and only those px's flow values are read back: no 25 M-entry shuffle, no full download.
-// Debug runs keep the exact shuffle (random_points above) so their output is reproducible.
 // An engine status that leaves the device context in doubt (a HIP call failed, memory ran
 // out): the pair is retried on a rebuilt context.  TVL1_EINVAL / TVL1_ESIZE are input or
 // config errors (a bad medianFiltering, an ROI the solver rejects): reported like the
@@ -445,6 +439,12 @@ std::vector<std::pair<int, int>> sample_points(R0 row0, R1 row1, int W, int H, i
   return pts;
 }
 
+// random_points without the debug flag, where the reference seeds rand() with the time
+// (optflow.cpp:532-535) and keeps the first npoints of a random_shuffle of all the masked
+// px: npoints distinct uniformly random masked px in random order is the same distribution.
+// Drawn by a partial Fisher-Yates over the implicit list (row counts + a sparse swap map),
+// and only those px's flow values are read back: no 25 M-entry shuffle, no full download.
+// Debug runs keep the exact shuffle (random_points above) so their output is reproducible.
 bool random_points_sampled(DeviceCtx &dc, size_t fp, int W, int H, const ofio::Image8 &f0,
                            const ofio::Image8 &f1, const Rect &r0, const Rect &r1, Value &im,
                            const Value &args, bool features, std::string &err) {
@@ -461,8 +461,9 @@ bool random_points_sampled(DeviceCtx &dc, size_t fp, int W, int H, const ofio::I
     off[i] = (int64_t)(pts[i].second * (fp / 4) + pts[i].first);
   // only the chosen px's flow crosses PCIe (tvl1_gather_flow: one upload, one gather, one
   // download), synchronous
-  if (const tvl1_status s = tvl1_gather_flow(dc.ctx, dc.du, dc.dv, off.data(), (int32_t)off.size(),
-                                             vx.data(), vy.data(), dc.stream);
+  if (const tvl1_status s = tvl1_gather_flow(dc.ctx, dc.du, dc.dv,
+                                             (int64_t)((size_t)(H - 1) * (fp / 4) + W), off.data(),
+                                             (int32_t)off.size(), vx.data(), vy.data(), dc.stream);
       s != TVL1_OK) {
     err = std::string("flow read-back failed: ") + tvl1_last_error(dc.ctx), dc.faulted = device_fault(s);
     return false;
@@ -1372,8 +1373,8 @@ static int from_file(Value &args, bool plan_only) {
             }
             fx.resize(off.size());
             fy.resize(off.size());
-            sc = tvl1_gather_flow(dc.ctx, dU, dV, off.data(), (int32_t)off.size(), fx.data(),
-                                  fy.data(), dc.stream);
+            sc = tvl1_gather_flow(dc.ctx, dU, dV, (int64_t)(px * nb), off.data(), (int32_t)off.size(),
+                                  fx.data(), fy.data(), dc.stream);
             if (sc != TVL1_OK) {
               fail("flow read-back", sc);
               break;
@@ -1429,6 +1430,10 @@ static int from_file(Value &args, bool plan_only) {
             dbg_fy[kk].swap(fy);
           }
         }
+        // hP / hQ are reused page-locked buffers: after a failure the chunk's uploads from
+        // them may still be queued, so the stream is drained before the retry or the next
+        // chunk refills them (PinnedPool's rule, as solve_rois' SyncOnFailure)
+        if (!ok && dc.stream) (void)hipStreamSynchronize(dc.stream);
         if (items.empty()) break;   // handed to the per-pair path
         if (ok && otype == "random_points" && debug) {   // the exact shuffle (random_points)
           for (int b = 0; b < nb; ++b)

@@ -2758,14 +2758,17 @@ tvl1_status tvl1_postprocess_batch(tvl1_ctx *c, int32_t n, float *u, float *v, s
   return TVL1_OK;
 }
 
-tvl1_status tvl1_gather_flow(tvl1_ctx *c, const float *u, const float *v, const int64_t *offsets,
-                             int32_t n, float *out_u, float *out_v, void *stream) {
+tvl1_status tvl1_gather_flow(tvl1_ctx *c, const float *u, const float *v, int64_t plane_elems,
+                             const int64_t *offsets, int32_t n, float *out_u, float *out_v,
+                             void *stream) {
   if (!c) return set_err(nullptr, TVL1_EINVAL, "ctx is NULL");
   if (n < 0 || (n > 0 && (!u || !v || !offsets || !out_u || !out_v)))
     return set_err(c, TVL1_EINVAL, "bad argument");
   if (n == 0) return TVL1_OK;
   for (int32_t i = 0; i < n; ++i)
-    if (offsets[i] < 0) return set_err(c, TVL1_EINVAL, "negative offset at %d", i);
+    if (offsets[i] < 0 || offsets[i] >= plane_elems)   // never an out-of-range device read
+      return set_err(c, TVL1_EINVAL, "offset %lld at %d outside [0, %lld)",
+                     (long long)offsets[i], i, (long long)plane_elems);
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
   order_streams(c, st);

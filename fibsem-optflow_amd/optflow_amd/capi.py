@@ -18,7 +18,7 @@ REPO_ROOT = PKG_ROOT.parent
 ENGINE_SO = PKG_ROOT / "lib" / "libtvl1_hip.so"
 
 TVL1_MAX_LEVELS = 32
-ABI_VERSION = 8          # TVL1_ABI_VERSION of include/tvl1.h
+ABI_VERSION = 9          # TVL1_ABI_VERSION of include/tvl1.h
 STATUS = {0: "TVL1_OK", 1: "TVL1_EINVAL", 2: "TVL1_ESIZE", 3: "TVL1_EHIP",
           4: "TVL1_ENOMEM", 5: "TVL1_ENODEV"}
 
@@ -208,7 +208,8 @@ def load_engine() -> C.CDLL:
                                            C.c_size_t, C.c_size_t, C.c_void_p, C.c_size_t,
                                            C.c_size_t, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
     lib.tvl1_postprocess_batch.restype = C.c_int
-    lib.tvl1_gather_flow.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+    lib.tvl1_gather_flow.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
+                                     C.c_int32,
                                      C.c_void_p, C.c_void_p, C.c_void_p]
     lib.tvl1_gather_flow.restype = C.c_int
     lib.tvl1_stream.argtypes = [C.c_void_p]
@@ -395,12 +396,14 @@ class Engine:
                                                     pitch1, stride1, w, h, mode, stream),
                     "tvl1_postprocess_batch")
 
-    def gather_flow(self, du: int, dv: int, offsets, stream: int = 0):
-        """tvl1_gather_flow: (u[off], v[off]) for element offsets into device planes."""
+    def gather_flow(self, du: int, dv: int, plane_elems: int, offsets, stream: int = 0):
+        """tvl1_gather_flow: (u[off], v[off]) for element offsets in [0, plane_elems) into
+        device planes (any other offset raises, TVL1_EINVAL)."""
         off = np.ascontiguousarray(offsets, np.int64)
         ou = np.zeros(len(off), np.float32)
         ov = np.zeros(len(off), np.float32)
-        self._check(self.lib.tvl1_gather_flow(self.ctx, du, dv, off.ctypes.data, len(off),
+        self._check(self.lib.tvl1_gather_flow(self.ctx, du, dv, plane_elems, off.ctypes.data,
+                                              len(off),
                                               ou.ctypes.data, ov.ctypes.data, stream),
                     "tvl1_gather_flow")
         return ou, ov

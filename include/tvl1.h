@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TVL1_ABI_VERSION 8
+#define TVL1_ABI_VERSION 9
 #define TVL1_MAX_LEVELS 32
 
 typedef enum tvl1_status {
@@ -269,11 +269,14 @@ tvl1_status tvl1_postprocess_batch(tvl1_ctx *ctx, int32_t n, float *u, float *v,
                                    const uint8_t *I1, size_t pitch1, size_t pair_stride1,
                                    int32_t width, int32_t height, int32_t mode, void *stream);
 
-/* The flow values of a few chosen px (ABI 8): out_u[i] = u[offsets[i]], out_v[i] =
- * v[offsets[i]], offsets in floats from the device pointers u / v (host array of n).  The
- * point-match output draws npoints px per ROI (random_points, optflow.cpp:522-572) and needs
- * only their flow, not the whole field.  Host outputs; synchronous on stream. */
-tvl1_status tvl1_gather_flow(tvl1_ctx *ctx, const float *u, const float *v,
+/* The flow values of a few chosen px (ABI 8; plane_elems since ABI 9): out_u[i] =
+ * u[offsets[i]], out_v[i] = v[offsets[i]], offsets in floats from the device pointers u / v
+ * (host array of n).  Every offset must lie in [0, plane_elems), the number of floats
+ * addressable from u and from v (for a batch: pairs x pair stride); any other offset is
+ * TVL1_EINVAL before anything is launched.  The point-match output draws npoints px per ROI
+ * (random_points, optflow.cpp:522-572) and needs only their flow, not the whole field.
+ * Host outputs; synchronous on stream. */
+tvl1_status tvl1_gather_flow(tvl1_ctx *ctx, const float *u, const float *v, int64_t plane_elems,
                              const int64_t *offsets, int32_t n, float *out_u, float *out_v,
                              void *stream);
 

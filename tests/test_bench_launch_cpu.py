@@ -51,3 +51,26 @@ def test_launcher_world_size_must_match_gpus():
     assert r.returncode != 0
     assert "WORLD_SIZE 2" in r.stderr
     assert not r.stdout.strip()
+
+
+def test_launcher_without_gpus_takes_world_size():
+    """`torchrun --nproc-per-node 2 bench.py` without --gpus: --gpus defaults to
+    the launcher's WORLD_SIZE, so the mismatch check does not fire (the run then fails on
+    this GPU-less host, later, for want of a device or a rendezvous)."""
+    r = run(["--steps", "1"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    assert "but the launcher started" not in r.stderr
+
+
+def test_cpu_allotment_records_the_share(monkeypatch):
+    """cpu_baseline's thread count is the smallest of the affinity mask, the cgroup quota and
+    OMP_NUM_THREADS, and every one of them is recorded."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    a = bench.cpu_allotment()
+    assert a["affinity_cpus"] == len(os.sched_getaffinity(0))
+    assert a["omp_num_threads_env"] == 3
+    assert a["threads"] == min(x for x in (a["affinity_cpus"], a["cgroup_quota_cpus"], 3) if x)
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    b = bench.cpu_allotment()
+    assert b["omp_num_threads_env"] is None and 1 <= b["threads"] <= b["affinity_cpus"]

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol(built):
 
 def test_abi_version_and_defaults(built):
     lib = capi.load_engine()
-    assert lib.tvl1_abi_version() == 8
+    assert lib.tvl1_abi_version() == 9
     p = capi.TVL1Params()
     lib.tvl1_params_default(C.byref(p))
     # generate_TV_args defaults, /root/reference/src/optflow.cpp:503-512

@@ -201,7 +201,8 @@ def test_batch_relaid_across_streams_without_sync(built):
 
 def test_postprocess_batch_and_gather_flow(built):
     """ABI 8: tvl1_postprocess_batch equals tvl1_postprocess per pair (every mode, frame1
-    masks with zeros), and tvl1_gather_flow returns exactly the addressed values."""
+    masks with zeros), and tvl1_gather_flow returns exactly the addressed values; ABI 9: an
+    offset outside [0, plane_elems) is TVL1_EINVAL, never a device read."""
     dev = torch.device("cuda", 0)
     n, w, h = 5, 70, 33
     rng = np.random.default_rng(9)
@@ -222,7 +223,13 @@ def test_postprocess_batch_and_gather_flow(built):
             assert torch.equal(ub[b].view(torch.int32), us.view(torch.int32)), (mode, b)
             assert torch.equal(vb[b].view(torch.int32), vs.view(torch.int32)), (mode, b)
     off = rng.integers(0, n * w * h, 1000)
-    gu, gv = eng.gather_flow(u0.data_ptr(), v0.data_ptr(), off)
+    gu, gv = eng.gather_flow(u0.data_ptr(), v0.data_ptr(), n * w * h, off)
     np.testing.assert_array_equal(gu, u0.flatten().cpu().numpy()[off])
     np.testing.assert_array_equal(gv, v0.flatten().cpu().numpy()[off])
+    last = np.array([n * w * h - 1])
+    gu, gv = eng.gather_flow(u0.data_ptr(), v0.data_ptr(), n * w * h, last)
+    assert gu[0] == u0.flatten()[-1].item() and gv[0] == v0.flatten()[-1].item()
+    for bad in (n * w * h, -1, 1 << 40):
+        with pytest.raises(capi.TVL1Error, match="outside"):
+            eng.gather_flow(u0.data_ptr(), v0.data_ptr(), n * w * h, np.array([0, bad]))
     eng.close()

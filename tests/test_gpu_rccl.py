@@ -20,11 +20,11 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
 
 
-def torchrun(args, timeout=110):
+def torchrun(args, timeout=110, gpus_flag=True):
     port = 29500 + os.getpid() % 150
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"),
-           "--gpus", "1", *args]
+           *(["--gpus", "1"] if gpus_flag else []), *args]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     env.pop("BENCH_DIST_BACKEND", None)   # the default: nccl (= RCCL)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env,
@@ -42,6 +42,17 @@ def test_pair_bench_under_rccl(built):
     assert out["n_gpus"] == 1 and out["steps"] == 2
     assert out["value"] > 0 and out["ms_per_step"] > 0
     assert out["config"]["iterations_per_pair"] > 0
+    # the per-rank records travel through all_gather_object on the nccl group
+    assert [r["rank"] for r in out["ranks"]] == [0] and out["ranks"][0]["pairs"] == 2 * 2
+    assert out["ranks"][0]["pci"].count(":") == 2
+
+
+def test_torchrun_without_gpus_flag(built):
+    """`torchrun --nproc-per-node 1 bench.py` with no --gpus takes WORLD_SIZE."""
+    out = torchrun(["--width", "320", "--height", "240", "--steps", "1", "--warmup", "1",
+                    "--inflight", "1", "--no-cpu-baseline", "--no-strips-line",
+                    "--no-fast-math-line"], gpus_flag=False)
+    assert out["n_gpus"] == 1 and out["config"]["process_group"] == "nccl"
 
 
 def test_stack_bench_under_rccl(built):
@@ -52,3 +63,4 @@ def test_stack_bench_under_rccl(built):
     # every (z, z + s) pair once: 9 adjacent + 6 at stride 4, counted by the all_reduce
     assert out["config"]["pairs"] == 9 + 6
     assert out["value"] > 0
+    assert len(out["ranks"]) == 1 and out["ranks"][0]["pairs"] == 9 + 6

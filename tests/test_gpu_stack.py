@@ -72,6 +72,12 @@ def test_plain_launch_runs_n_ranks(built, tmp_path):
            for f in tmp_path.glob("pair_s*_z*_r*.npz")]
     assert sorted(got) == sorted(want)
     assert {int(np.load(f)["rank"]) for f in tmp_path.glob("*.npz")} <= {0, 1}
+    # one record per rank; under gloo both ranks share the one card
+    rk = out["ranks"]
+    assert [r["rank"] for r in rk] == [0, 1]
+    assert len({r["pci"] for r in rk}) == 1
+    assert sum(r["pairs"] for r in rk) == len(want)
+    assert all(r["elapsed_s"] > 0 for r in rk)
 
 
 def test_plain_launch_default_pair_line(built):
@@ -93,6 +99,9 @@ def test_plain_launch_default_pair_line(built):
     assert out["value"] > 0 and out["cpu_baseline"] is None
     assert set(out["math_modes"]) == {"fast", "fma"}
     assert out["production_strips"]["value"] > 0
+    for rk in (out["ranks"], out["production_strips"]["ranks"]):
+        assert [r["rank"] for r in rk] == [0, 1] and len({r["pci"] for r in rk}) == 1
+    assert [r["pairs"] for r in out["ranks"]] == [2 * 2, 2 * 2]   # steps x in flight
 
 
 def expected_pairs():

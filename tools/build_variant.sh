@@ -1,6 +1,6 @@
 # Builds an engine library variant into DIR from the working tree: per-TU extra flags.
 # Usage: bash tools/build_variant.sh DIR "<engine-TU extra flags>" "<passes-TU extra flags>"
-# (the Makefile's flags otherwise; e.g. "-mllvm -amdgpu-sched-strategy=max-ilp -DTVL1_WI_MINW=4")
+# (the Makefile's flags otherwise; e.g. "-mllvm -amdgpu-sched-strategy=max-ilp -DTVL1_ROLL_LDS=0")
 set -e
 D=$1; EF=$2; PF=$3
 F="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall --offload-arch=gfx950"
