@@ -203,7 +203,7 @@ def rank_records(dist, local_rank, pairs, iterations, elapsed):
     pr = torch.cuda.get_device_properties(local_rank)
     rec = {"rank": int(os.environ.get("RANK", "0")), "local_rank": local_rank,
            "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}",
-           "device": pr.name, "pairs": pairs, "iterations": iterations,
+           "device": pr.name or pr.gcnArchName, "pairs": pairs, "iterations": iterations,
            "elapsed_s": round(elapsed, 4)}
     if not dist:
         return [rec]

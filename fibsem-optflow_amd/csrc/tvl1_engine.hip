@@ -152,6 +152,9 @@ struct tvl1_ctx {
   int batch_px1_w = kBatchPx1W;         // TVL1_BATCH_PX1_W: batched passes on levels at most
                                         // this wide run 64-px bands (1 px per lane)
   int kb1_slots[kRollMax + 1] = {};     // resident kb_iterate_roll<K, 1> wavefronts
+  int batch_seg_min = 128;              // TVL1_BATCH_SEG_MIN: batched passes never split a
+                                        // level into segments shorter than min(rows, this)
+                                        // (0: roll_segment alone)
   int probe_lds = 0;                    // TVL1_PROBE_ROLL_LDS: dynamic LDS per k_iterate_roll
                                         // block (occupancy probe only; with the LDS-staged
                                         // passes' 40 KiB, at most 120 KiB)
@@ -1805,11 +1808,17 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
             const int px = lw <= c->batch_px1_w ? 1 : 2;
             const int halo = px == 1 ? K : (K + 1) / 2 * 2;   // roll_halo<K, PX>
             br.ra.bands = (lw + 64 * px - 2 * halo - 1) / (64 * px - 2 * halo);
-            // segments sized so the launch's wavefronts fill whole rounds of resident slots
+            // segments sized so the launch's wavefronts fill whole rounds of resident slots,
+            // but never shorter than min(rows, batch_seg_min): a pass group of a few pairs (or
+            // a tiny level) would otherwise be cut into short segments that repeat the 2K-row
+            // halo to fill slots the other batch in flight fills anyway (r5: one segment per
+            // band on the strips' <= 100-row levels, +1.7 % strip solves/s,
+            // profiles/r5/ab/strips_seg/)
             br.ra.seg_rows = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                             : roll_segment(br.ra.bands * sel.n, lh, K,
-                                                            px == 1 ? c->kb1_slots[K]
-                                                                    : c->roll_slots[K][0][2]);
+                                             : std::max(roll_segment(br.ra.bands * sel.n, lh, K,
+                                                                     px == 1 ? c->kb1_slots[K]
+                                                                             : c->roll_slots[K][0][2]),
+                                                        std::min(lh, c->batch_seg_min));
             br.ra.waves = br.ra.bands * ((lh + br.ra.seg_rows - 1) / br.ra.seg_rows);
             blocks = br.ra.waves;
             if (blocks > c->bnblk)
@@ -2272,6 +2281,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_BATCH_STORE")) c->batch_store_pred = atoi(m) == 0;
   if (const char *m = getenv("TVL1_BATCH_GROUP")) c->batch_group = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BATCH_PX1_W")) c->batch_px1_w = atoi(m);
+  if (const char *m = getenv("TVL1_BATCH_SEG_MIN")) c->batch_seg_min = atoi(m);
   if (const char *m = getenv("TVL1_PROBE_ROLL_LDS")) c->probe_lds = atoi(m);
   if (const char *m = getenv("TVL1_PROBE_WI_LDS")) c->probe_wi_lds = std::min(atoi(m), 32768);
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels

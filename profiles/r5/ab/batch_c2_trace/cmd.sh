@@ -5,5 +5,5 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r5_trace; mkdir -p $O
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/pair -o pair -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-fast-math-line --no-strips-line --no-kernel-timing > $O/pair.json 2> $O/pair.err &&
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/batch -o batch -- python3 bench.py --workload strips --width 6144 --height 4096 --nscales 5 --warps 30 --batch 3 --inflight 1 --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing > $O/batch.json 2> $O/batch.err
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d $O/pair -o pair -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-fast-math-line --no-strips-line --no-kernel-timing > $O/pair.json 2> $O/pair.err &&
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d $O/batch -o batch -- python3 bench.py --workload strips --width 6144 --height 4096 --nscales 5 --warps 30 --batch 3 --inflight 1 --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-timing > $O/batch.json 2> $O/batch.err

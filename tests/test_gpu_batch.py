@@ -56,7 +56,8 @@ def pairs(n, w, h, seed):
 ])
 @pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0", "TVL1_WI_NC=1", "TVL1_BATCH_STORE=1",
                                  "TVL1_BATCH_GROUP=0", "TVL1_BATCH_PX1_W=0",
-                                 "TVL1_BATCH_PX1_W=150"])
+                                 "TVL1_BATCH_PX1_W=150", "TVL1_BATCH_SEG_MIN=0",
+                                 "TVL1_BATCH_SEG_MIN=16"])
 @pytest.mark.parametrize("math", [0, 2])
 def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw, math):
     """kb_warp_iter (fused warp + first pass; 2 consumer wavefronts, or 1 with
@@ -70,11 +71,25 @@ def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw, math):
     monkeypatch.delenv("TVL1_BATCH_STORE", raising=False)
     monkeypatch.delenv("TVL1_BATCH_GROUP", raising=False)
     monkeypatch.delenv("TVL1_BATCH_PX1_W", raising=False)
+    monkeypatch.delenv("TVL1_BATCH_SEG_MIN", raising=False)
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
     p = capi.make_params(fast_math=math, **kw)
     eng = capi.Engine(p)
     I0s, I1s = pairs(n, w, h, seed=100 + n)
+    u, v, st = run_batch(eng, I0s, I1s)
+    eng.close()
+    check_against_oracle(p, I0s, I1s, u, v, st)
+
+
+def test_batch_of_full_frame_geometry_pairs(built):
+    """C2's pyramid and schedule at a quarter of its width and height -- 3
+    pairs of 1536x1024, nscales 5, warps 30, iterations 300, epsilon 0.01 -- through one
+    tvl1_calc_batch, every pair bit-identical to the oracle with the same per-warp counts
+    (the A/B against 3 single-pair solves in flight is profiles/r5/ab/batch_c2/)."""
+    p = capi.make_params(nscales=5, warps=30, iterations=300, epsilon=0.01)
+    eng = capi.Engine(p)
+    I0s, I1s = pairs(3, 1536, 1024, seed=0x5EED)
     u, v, st = run_batch(eng, I0s, I1s)
     eng.close()
     check_against_oracle(p, I0s, I1s, u, v, st)
@@ -129,6 +144,7 @@ def test_batch_fast_math_within_tolerance(built, monkeypatch, env):
     (tests/test_gpu_fastmath.py's bar)."""
     monkeypatch.delenv("TVL1_BATCH_FUSE", raising=False)
     monkeypatch.delenv("TVL1_BATCH_PX1_W", raising=False)
+    monkeypatch.delenv("TVL1_BATCH_SEG_MIN", raising=False)
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
     kw = dict(nscales=10, warps=5)
