@@ -462,6 +462,7 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
         stack = torch.stack([gen.slice(z) for z in range(B + 1)])
         eng = capi.Engine(params, device=local_rank)
         slots.append(dict(eng=eng, stack=stack,
+                          ts=torch.cuda.ExternalStream(eng.stream, device=dev),
                           u=torch.empty((B, H, W), dtype=torch.float32, device=dev),
                           v=torch.empty((B, H, W), dtype=torch.float32, device=dev)))
     torch.cuda.synchronize(dev)
@@ -471,7 +472,7 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
         st = sl["eng"].calc_batch_device(B, base, W, 0, base + W * H, W, W * H, W, H,
                                          sl["u"].data_ptr(), sl["v"].data_ptr(),
                                          4 * W, 4 * W * H, stream=sl["eng"].stream)
-        torch.cuda.synchronize(dev)
+        sl["ts"].synchronize()   # this slot's stream only: the other slots keep running
         return st
 
     pool = ThreadPoolExecutor(max_workers=F)
