@@ -152,6 +152,9 @@ struct tvl1_ctx {
   int batch_px1_w = kBatchPx1W;         // TVL1_BATCH_PX1_W: batched passes on levels at most
                                         // this wide run 64-px bands (1 px per lane)
   int kb1_slots[kRollMax + 1] = {};     // resident kb_iterate_roll<K, 1> wavefronts
+  int batch_k2_w = 0;                   // TVL1_BATCH_K2_W: batched passes on levels at most this
+                                        // wide run <= 2 iterations (a 2-px halo instead of 4:
+                                        // less recompute on tiny levels; r5 A/B)
   int batch_seg_min = 128;              // TVL1_BATCH_SEG_MIN: batched passes never split a
                                         // level into segments shorter than min(rows, this)
                                         // (0: roll_segment alone)
@@ -1589,6 +1592,9 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
       batch_bufs.ub = (unsigned)(bstride + lvl);
       batch_bufs.pb = (unsigned)(3 * bstride + lvl);
     }
+    // passes of at most kmax_l iterations (every pair still runs exactly its single-pair
+    // schedule: a pass ends at its check or at kmax_l, whichever comes first)
+    const int kmax_l = lw <= c->batch_k2_w ? 2 : kTbMax;
     IterArgs it{};   // pass geometry and scalars (plane pointers are set per pair)
     it.W = lw;
     it.H = lh;
@@ -1761,7 +1767,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           if (!act[b]) continue;
           int k = 0;
           double ps_ = prev[b];
-          while (k < kTbMax && nit[b] + k < prm.iterations) {
+          while (k < kmax_l && nit[b] + k < prm.iterations) {
             const bool ce = (prm.epsilon > 0) && ((nit[b] + k) & 1) && (ps_ < scaledEps);
             ++k;
             if (ce) {
@@ -2282,6 +2288,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_BATCH_GROUP")) c->batch_group = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BATCH_PX1_W")) c->batch_px1_w = atoi(m);
   if (const char *m = getenv("TVL1_BATCH_SEG_MIN")) c->batch_seg_min = atoi(m);
+  if (const char *m = getenv("TVL1_BATCH_K2_W")) c->batch_k2_w = atoi(m);
   if (const char *m = getenv("TVL1_PROBE_ROLL_LDS")) c->probe_lds = atoi(m);
   if (const char *m = getenv("TVL1_PROBE_WI_LDS")) c->probe_wi_lds = std::min(atoi(m), 32768);
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels

@@ -64,7 +64,7 @@ def test_bench_line_carries_the_contract_fields(bench):
 # ---- rounds 3 and 4: one box, one evidence set each (tools/final_profile.sh ->
 # profiles/r3/final/, profiles/r4/final/): the default bench line, one C2 pair alone and one
 # production strip batch alone
-FINALS = [PROF / "r3" / "final", PROF / "r4" / "final"]
+FINALS = [PROF / "r3" / "final", PROF / "r4" / "final", PROF / "r5" / "final"]
 
 
 def _class_avg_us(stats_csv, prefixes):
@@ -77,7 +77,7 @@ def _class_avg_us(stats_csv, prefixes):
     return ns / calls / 1e3, calls
 
 
-@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4"])
+@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4", "r5"])
 @pytest.mark.parametrize("which", ["pair", "strips"])
 def test_final_roofline_reproduces_by_hand(FINAL, which):
     """The bench line's `roofline.frac` (live byte accounting / HIP-event launch time) by hand
@@ -108,7 +108,7 @@ def test_final_roofline_reproduces_by_hand(FINAL, which):
     assert roof["model_bytes_over_peak"] > 1.0 > roof["frac"]
 
 
-@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4"])
+@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4", "r5"])
 def test_final_bench_line_fields(FINAL):
     d = json.loads((FINAL / "bench_c2.json").read_text().splitlines()[-1])
     assert d["config"]["workload"].startswith("C2") and d["n_gpus"] == 1
@@ -117,12 +117,25 @@ def test_final_bench_line_fields(FINAL):
     assert d["production_strips"]["roofline"]["launches"] > 0
 
 
-def test_bench_reads_the_r4_traffic_record():
-    """profiles/traffic*.json (bench.py's `traffic`) are the r4 evidence set's records."""
+def test_bench_reads_the_r5_traffic_record():
+    """profiles/traffic*.json (bench.py's `traffic`) are the r5 evidence set's records."""
     for name in ("traffic.json", "traffic_strips.json"):
         top = json.loads((PROF / name).read_text())
-        r4 = json.loads((PROF / "r4" / "final" / name).read_text())
-        assert top == r4 and "profiles/r4/final/" in top["source"]
+        r5 = json.loads((PROF / "r5" / "final" / name).read_text())
+        assert top == r5 and "profiles/r5/final/" in top["source"]
+
+
+def test_r5_bench_line_carries_rank_records_and_allotment():
+    """VERDICT r4 items 5-6 in the r5 evidence line: one rank record with a PCI id, and the
+    CPU baseline's allotment (affinity mask, cgroup quota, OMP_NUM_THREADS) with the oracle
+    run on the smallest of them."""
+    d = json.loads((PROF / "r5" / "final" / "bench_c2.json").read_text().splitlines()[-1])
+    rk = d["ranks"]
+    assert len(rk) == 1 and rk[0]["pci"].count(":") == 2 and rk[0]["pairs"] > 0
+    a = d["cpu_baseline"]["allotment"]
+    assert d["cpu_baseline"]["cores"] == a["threads"]
+    assert a["threads"] == min(x for x in (a["affinity_cpus"], a["cgroup_quota_cpus"],
+                                           a["omp_num_threads_env"]) if x)
 
 
 def test_r4_kb_warp_iter_writes_below_fetches():
