@@ -15,6 +15,8 @@
 // resize_px), so every pair's flow is bit-identical to oracle/.
 #pragma once
 
+#include <cfloat>
+
 namespace tvl1k {
 
 constexpr int kBatchMax = 256;
@@ -243,6 +245,212 @@ TVL1_PLAIN __global__ void kb_median(BatchMedian w) {
     v[j + 1] = t;
   }
   w.U[us ^ 1][c][b * w.ps + (size_t)y * w.P + x] = v[n / 2];
+}
+
+// ---- The coarsest level of a batch, one workgroup per pair, entirely on chip (r5).
+// The production strip's coarsest level (515 x 17 px at nscales 10) is where a batch spends
+// the most per px-iteration: its streaming passes are one wavefront's 21-step walk long,
+// recompute 1.4x (8 of every 64 band columns, 4 drained rows of 17) and end in a host-read
+// residual check every few iterations -- 89 launches and ~45 host round trips per batch, for
+// 204 iterations per pair.  Here one workgroup holds a whole pair's level: lane x
+// of the workgroup owns column x, its rows' u and p in registers, the warp constants and I1
+// in LDS.  It runs procOneScale's loop for every warp of the level -- warpBackward, then the
+// iterations with the residual summed by the workgroup and the stopping rule evaluated on
+// chip -- with x-neighbours by DPP inside a wavefront and through LDS across wavefronts, and
+// two barriers per iteration.  Nothing is recomputed, nothing goes to HBM between
+// iterations, and the host waits once per level.  The arithmetic is warp_gather_fn (taps at
+// clamped coordinates, centeredGradient per tap as k_warp_ring's global path),
+// estimate_u_px and dual_px with their general border forms: the same operations as the
+// streaming kernels, so the same bits.  The residual is summed in double per column (rows
+// in order) and over the workgroup in a fixed order; the stopping decisions sit >= 1e-4
+// (relative) from their thresholds on every input measured, and the parity
+// tests compare every pair's flow and per-warp counts with the oracle bitwise.
+constexpr int kSmallR = 17;         // rows per lane: the level's height, at most
+constexpr int kSmallWaves = 9;      // 576 lanes, one column each: the level's width, at most
+constexpr int kSmallPx = 9000;      // LDS planes of W * H floats: I1 and the three constants
+
+struct BatchSmall {
+  const float *I0, *I1;   // the level's images of pair 0 (pair stride ips)
+  float *u1, *u2;         // u set written (pair stride ps); the level starts from u = 0
+  size_t ips, ps;
+  int W, H, P;            // level geometry; P = plane pitch in floats
+  int warps, iterations, eps_pos;
+  double thr;             // scaledEps = eps^2 * W * H
+  IterArgs it;            // l_t, theta, taut (gamma = 0)
+  int *warp_iters;        // [pair][warps] iterations each warp ran
+  int *checks;            // [pair] residual checks
+  BatchSel sel;
+};
+
+template <int FM>
+__global__ __launch_bounds__(64 * kSmallWaves) void kb_small_level(BatchSmall a) {
+  __shared__ float sI1[kSmallPx];
+  __shared__ float sC[3][kSmallPx];
+  __shared__ float xu[kSmallWaves][2][kSmallR];   // each wavefront's lane 0: u1, u2 (new)
+  __shared__ float xp[kSmallWaves][2][kSmallR];   // each wavefront's lane 63: p11, p21
+  __shared__ double red[kSmallWaves];
+  constexpr int R = kSmallR;
+  const int b = a.sel.idx[blockIdx.x];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6;
+  const int W = a.W, H = a.H, P = a.P;
+  const int x = threadIdx.x;
+  const bool valid = x < W;
+  const int xs = imin(x, W - 1);   // lanes past the level's width compute on column W - 1
+  const float *I0 = a.I0 + b * a.ips;
+  const float *I1 = a.I1 + b * a.ips;
+  for (int i = threadIdx.x; i < W * H; i += blockDim.x) {
+    const int yy = i / W;
+    sI1[i] = I1[(size_t)yy * P + (i - yy * W)];
+  }
+  float u1[R], u2[R], p11[R], p12[R], p21[R], p22[R];
+#pragma unroll
+  for (int y = 0; y < R; ++y) u1[y] = u2[y] = p11[y] = p12[y] = p21[y] = p22[y] = 0.0f;
+  if (lane == 63)
+    for (int y = 0; y < R; ++y) xp[wv][0][y] = xp[wv][1][y] = 0.0f;
+  __syncthreads();
+  int checks = 0;
+  for (int wp = 0; wp < a.warps; ++wp) {
+    // K5 warpBackward of this lane's column (+ K3 centeredGradient per tap), constants to LDS.
+    // One row per trip of a loop that is not unrolled (one gather's code): row y's u is
+    // always u1[0] / u2[0] and the arrays rotate by one row per trip, R trips in all, so
+    // they end where they began (register arrays take constant indices only)
+    for (int y = 0; y < R; ++y) {
+      const float cu1 = u1[0], cu2 = u2[0];
+#pragma unroll
+      for (int i = 0; i < R - 1; ++i) {
+        u1[i] = u1[i + 1];
+        u2[i] = u2[i + 1];
+      }
+      u1[R - 1] = cu1;
+      u2[R - 1] = cu2;
+      if (y >= H) continue;
+      const float wx = (float)xs + cu1;
+      const float wy = (float)y + cu2;
+      const int fx = tap_floor(wx);
+      const int fy = tap_floor(wy);
+      float sum = 0.0f, sumx = 0.0f, sumy = 0.0f, wsum = 0.0f;
+      warp_gather_fn<FM>(
+          [&](int cy, int cx) {
+            const int rx = imin(imax(cx, 0), W - 1), ry = imin(imax(cy, 0), H - 1);
+            const float *row = sI1 + ry * W;
+            const float gx = 0.5f * (row[imin(rx + 1, W - 1)] - row[imax(rx - 1, 0)]);
+            const float gyv = 0.5f * (sI1[imin(ry + 1, H - 1) * W + rx] - sI1[imax(ry - 1, 0) * W + rx]);
+            return Tap3{row[rx], gx, gyv};
+          },
+          wx, wy, fx, fy, sum, sumx, sumy, wsum);
+      const float coeff = approx(FM) ? __builtin_amdgcn_rcpf(wsum) : recip_rn(wsum);
+      const float I1wv = sum * coeff;
+      const float I1wxv = sumx * coeff;
+      const float I1wyv = sumy * coeff;
+      if (valid) {
+        sC[0][y * W + x] = I1wxv;
+        sC[1][y * W + x] = I1wyv;
+        sC[2][y * W + x] = rho_c<FM>(I1wv, I1wxv, I1wyv, cu1, cu2, I0[(size_t)y * P + x]);
+      }
+    }
+    // procOneScale's iterations (each thread reads only its own column's constants: no
+    // barrier needed after the gather)
+    double error = DBL_MAX, prevError = 0.0;
+    int n;
+    for (n = 0; error > a.thr && n < a.iterations; ++n) {
+      const bool calc = a.eps_pos && (n & 1) && prevError < a.thr;
+      // estimateU: u^n = TH(u^{n-1}) + theta div p^{n-1}; p of the left column by DPP, and for
+      // lane 0 from the left wavefront's lane 63 (published after the previous iteration)
+      double acc = 0.0;
+      // the lane's constants' LDS index, advanced by a row per row: opaque per iteration so
+      // the compiler does not keep 17 row addresses live across the loop
+      int ci = xs;
+      asm volatile("" : "+v"(ci));
+#pragma unroll
+      for (int y = 0; y < R; ++y) {
+        if (y >= H) continue;   // (a fixed trip count: fully unrolled)
+        float l11 = from_left(p11[y]), l21 = from_left(p21[y]);
+        if (lane == 0 && wv > 0) {
+          l11 = xp[wv - 1][0][y];
+          l21 = xp[wv - 1][1][y];
+        }
+        const float c0 = sC[0][ci], c1 = sC[1][ci], c2 = sC[2][ci];
+        ci += W;
+        float n1, n2, n3;
+        const int yu = y > 0 ? y - 1 : 0;   // (never a negative register index)
+        estimate_u_px<false, FM>(c0, c1, c2, u1[y], u2[y], 0.0f, p11[y], l11, p12[y],
+                                 y > 0 ? p12[yu] : 0.0f, p21[y], l21, p22[y],
+                                 y > 0 ? p22[yu] : 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, xs, y, a.it,
+                                 n1, n2, n3);
+        if (calc && valid) acc += (double)residual_px<FM>(u1[y] - n1, u2[y] - n2);
+        u1[y] = n1;
+        u2[y] = n2;
+        __builtin_amdgcn_sched_barrier(0);   // rows one after another: no hoisting, low pressure
+      }
+      if (calc) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == 0) red[wv] = acc;
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int y = 0; y < R; ++y) {   // (register arrays: constant indices only)
+          if (y >= H) continue;   // (a fixed trip count: fully unrolled)
+          xu[wv][0][y] = u1[y];
+          xu[wv][1][y] = u2[y];
+        }
+      }
+      __syncthreads();
+      if (calc) {   // cuda::sum and the stopping rule, the same double for every lane
+        double e = 0.0;
+        for (int w = 0; w < nw; ++w) e += red[w];
+        error = e;
+        prevError = e;
+        ++checks;
+      } else {
+        error = DBL_MAX;
+        prevError -= a.thr;
+      }
+      // estimateDualVariables: u^n of the right column by DPP, and for lane 63 from the right
+      // wavefront's lane 0; p updated in place (each row reads only u)
+#pragma unroll
+      for (int y = 0; y < R; ++y) {
+        if (y >= H) continue;   // (a fixed trip count: fully unrolled)
+        float r1 = from_right(u1[y]), r2 = from_right(u2[y]);
+        if (lane == 63 && wv + 1 < nw) {
+          r1 = xu[wv + 1][0][y];
+          r2 = xu[wv + 1][1][y];
+        }
+        const bool has_down = y + 1 < H;
+        const float d1 = has_down ? u1[imin(y + 1, R - 1)] : u1[y];
+        const float d2 = has_down ? u2[imin(y + 1, R - 1)] : u2[y];
+        float q11, q12, q21, q22;
+        dual_px<false, false, FM>(u1[y], r1, d1, xs + 1 < W, has_down, a.it.taut, p11[y], p12[y],
+                                  q11, q12);
+        dual_px<false, false, FM>(u2[y], r2, d2, xs + 1 < W, has_down, a.it.taut, p21[y], p22[y],
+                                  q21, q22);
+        p11[y] = q11; p12[y] = q12;
+        p21[y] = q21; p22[y] = q22;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (lane == 63) {
+#pragma unroll
+        for (int y = 0; y < R; ++y) {
+          if (y >= H) continue;   // (a fixed trip count: fully unrolled)
+          xp[wv][0][y] = p11[y];
+          xp[wv][1][y] = p21[y];
+        }
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) a.warp_iters[(size_t)b * a.warps + wp] = n;
+  }
+  if (valid) {
+#pragma unroll
+    for (int y = 0; y < R; ++y) {
+      if (y >= H) continue;   // (a fixed trip count: fully unrolled)
+      a.u1[b * a.ps + (size_t)y * P + x] = u1[y];
+      a.u2[b * a.ps + (size_t)y * P + x] = u2[y];
+    }
+  }
+  if (threadIdx.x == 0) a.checks[b] = checks;
 }
 
 // K7 for the selected pairs: fixed-order sum of pair b's n partials (at partials + b * stride)

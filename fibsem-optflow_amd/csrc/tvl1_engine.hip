@@ -152,9 +152,6 @@ struct tvl1_ctx {
   int batch_px1_w = kBatchPx1W;         // TVL1_BATCH_PX1_W: batched passes on levels at most
                                         // this wide run 64-px bands (1 px per lane)
   int kb1_slots[kRollMax + 1] = {};     // resident kb_iterate_roll<K, 1> wavefronts
-  int batch_k2_w = 0;                   // TVL1_BATCH_K2_W: batched passes on levels at most this
-                                        // wide run <= 2 iterations (a 2-px halo instead of 4:
-                                        // less recompute on tiny levels; r5 A/B)
   int batch_seg_min = 128;              // TVL1_BATCH_SEG_MIN: batched passes never split a
                                         // level into segments shorter than min(rows, this)
                                         // (0: roll_segment alone)
@@ -164,6 +161,10 @@ struct tvl1_ctx {
   int probe_wi_lds = 0;                 // TVL1_PROBE_WI_LDS: the same for k_warp_iter (< 64 KiB)
   char *gather_scratch = nullptr;       // tvl1_gather_flow's offsets and values
   size_t gather_bytes = 0;
+  int batch_small = 1;                  // TVL1_BATCH_SMALL=0: the coarsest level of a batch
+                                        // streams like the others (no kb_small_level)
+  char *small_scratch = nullptr;        // kb_small_level's per-warp iteration counts
+  size_t small_bytes = 0;
   float *map_scratch = nullptr;         // tvl1_postprocess_affine's staged map planes
   size_t map_bytes = 0;
   char *align_scratch = nullptr;        // tvl1_find_alignment's pyramid, keys, descriptors
@@ -1592,9 +1593,6 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
       batch_bufs.ub = (unsigned)(bstride + lvl);
       batch_bufs.pb = (unsigned)(3 * bstride + lvl);
     }
-    // passes of at most kmax_l iterations (every pair still runs exactly its single-pair
-    // schedule: a pass ends at its check or at kmax_l, whichever comes first)
-    const int kmax_l = lw <= c->batch_k2_w ? 2 : kTbMax;
     IterArgs it{};   // pass geometry and scalars (plane pointers are set per pair)
     it.W = lw;
     it.H = lh;
@@ -1603,7 +1601,64 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
     it.theta = (float)prm.theta;
     it.gamma = 0.0f;
     it.taut = taut;
-    for (int wp = 0; wp < prm.warps; ++wp) {
+    // The coarsest level on chip (kb_small_level, one workgroup per pair: every warp's gather,
+    // iterations, residuals and stopping rule without leaving the workgroup) when it fits one
+    // workgroup's registers and LDS; u enters as 0 in set 0 and leaves there, and p is reset
+    // at every level anyway
+    const bool small = c->batch_small && s == L - 1 && prm.median_filtering <= 1 &&
+                       lw <= 64 * kSmallWaves && lh <= kSmallR && lw * lh <= kSmallPx;
+    if (small) {
+      const size_t need = (size_t)n * (prm.warps + 1) * sizeof(int);
+      if (need > c->small_bytes) {
+        const tvl1_status r = arena_alloc(c, &c->small_scratch, &c->small_bytes,
+                                          std::max<size_t>(need, 64 << 10), st);
+        if (r != TVL1_OK) return r;
+      }
+      BatchSmall sm{};
+      sm.I0 = c->bI0s[s];
+      sm.I1 = c->bI1s[s];
+      sm.u1 = c->bU[0][0];
+      sm.u2 = c->bU[0][1];
+      sm.ips = c->bips[s];
+      sm.ps = ps;
+      sm.W = lw;
+      sm.H = lh;
+      sm.P = P;
+      sm.warps = prm.warps;
+      sm.iterations = prm.iterations;
+      sm.eps_pos = prm.epsilon > 0;
+      sm.thr = scaledEps;
+      sm.it = it;
+      sm.warp_iters = reinterpret_cast<int *>(c->small_scratch);
+      sm.checks = sm.warp_iters + (size_t)n * prm.warps;
+      sm.sel = all;
+      const size_t tks = prof_begin(c, st);
+#define KB_SMALL(FM) \
+  hipLaunchKernelGGL((kb_small_level<FM>), dim3(n), dim3(64 * ((lw + 63) / 64)), 0, st, sm);
+      MATH_SWITCH(math, KB_SMALL)
+#undef KB_SMALL
+      HIP_TRY(c, hipGetLastError());
+      std::vector<int> hw((size_t)n * (prm.warps + 1));
+      HIP_TRY(c, hipMemcpyAsync(hw.data(), c->small_scratch, need, hipMemcpyDeviceToHost, st));
+      HIP_TRY(c, hipStreamSynchronize(st));
+      int64_t it_sum = 0;
+      for (int b = 0; b < n; ++b) {
+        for (int wp = 0; wp < prm.warps; ++wp) {
+          const int nb = hw[(size_t)b * prm.warps + wp];
+          level_iters[(size_t)b * TVL1_MAX_LEVELS + s] += nb;
+          it_sum += nb;
+          if (stats && stats[b].warp_iterations &&
+              s * prm.warps + wp < stats[b].warp_iterations_capacity)
+            stats[b].warp_iterations[s * prm.warps + wp] = nb;
+        }
+        checks[b] += hw[(size_t)n * prm.warps + b];
+      }
+      // iteration class: the SURVEY 8(d) bytes of every iteration and warp it ran; from HBM
+      // it only reads I0, I1 and writes u once
+      prof_end(c, st, tks, 0, (double)lw * lh * (64.0 * it_sum + 40.0 * n * prm.warps),
+               (double)lw * lh * 16.0 * n);
+    }
+    for (int wp = 0; wp < (small ? 0 : prm.warps); ++wp) {
       if (prm.median_filtering > 1) {   // build-only median of u before each warp
         BatchMedian md{};
         for (int k = 0; k < 2; ++k)
@@ -1767,7 +1822,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
           if (!act[b]) continue;
           int k = 0;
           double ps_ = prev[b];
-          while (k < kmax_l && nit[b] + k < prm.iterations) {
+          while (k < kTbMax && nit[b] + k < prm.iterations) {
             const bool ce = (prm.epsilon > 0) && ((nit[b] + k) & 1) && (ps_ < scaledEps);
             ++k;
             if (ce) {
@@ -2288,7 +2343,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_BATCH_GROUP")) c->batch_group = atoi(m) != 0;
   if (const char *m = getenv("TVL1_BATCH_PX1_W")) c->batch_px1_w = atoi(m);
   if (const char *m = getenv("TVL1_BATCH_SEG_MIN")) c->batch_seg_min = atoi(m);
-  if (const char *m = getenv("TVL1_BATCH_K2_W")) c->batch_k2_w = atoi(m);
+  if (const char *m = getenv("TVL1_BATCH_SMALL")) c->batch_small = atoi(m) != 0;
   if (const char *m = getenv("TVL1_PROBE_ROLL_LDS")) c->probe_lds = atoi(m);
   if (const char *m = getenv("TVL1_PROBE_WI_LDS")) c->probe_wi_lds = std::min(atoi(m), 32768);
   if (const char *m = getenv("TVL1_BUF_LIMIT"))   // force the 64-bit-addressed kernels
@@ -2842,6 +2897,7 @@ void tvl1_destroy(tvl1_ctx *c) {
   if (c->align_scratch) (void)hipFree(c->align_scratch);
   if (c->map_scratch) (void)hipFree(c->map_scratch);
   if (c->gather_scratch) (void)hipFree(c->gather_scratch);
+  if (c->small_scratch) (void)hipFree(c->small_scratch);
   for (auto &r : c->retired) free_retired(r);
   if (c->align_pat) (void)hipFree(c->align_pat);
   if (c->pinned) (void)hipHostFree(c->pinned);

@@ -1510,7 +1510,7 @@ __global__ __launch_bounds__((64 / PX) * RH / NG, PX == 2 ? 8 : 1) void k_iterat
 // thread, 64 x 64 regions, needs 165 VGPRs -- one block per CU -- and was 49 % slower.)  Same
 // estimate_u / dual_component arithmetic, so the same bits (the region-edge rows take their
 // own row as the neighbour, as k_iterate_tb's LDS clamp does; no stored cell depends on them).
-constexpr int kTb4Groups = 16;   // row groups (threads per column) of a region
+constexpr int kTb4Groups = 16;   // row groups (threads per column) of a region (32: -6 %, r5)
 constexpr int kTb4RowsPerThread = 3;
 
 // The iterations of one k_iterate_tb4 region.  IN: the region lies inside the image with a

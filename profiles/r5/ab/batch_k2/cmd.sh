@@ -11,3 +11,4 @@ TVL1_BATCH_K2_W=1700 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 -
 tail -1 gpurun_out/r5_k2/parity.log
 export BENCH_FLAGS="--workload strips --steps 3"
 bash tools/ab_env.sh 2 "TVL1_BATCH_K2_W=0" "TVL1_BATCH_K2_W=700" "TVL1_BATCH_K2_W=1100" "TVL1_BATCH_K2_W=1700" > gpurun_out/r5_k2/ab.txt 2>&1
+# (the knob this A/B used was removed after it; see result.txt and DESIGN 9)

@@ -57,7 +57,7 @@ def pairs(n, w, h, seed):
 @pytest.mark.parametrize("env", ["", "TVL1_BATCH_FUSE=0", "TVL1_WI_NC=1", "TVL1_BATCH_STORE=1",
                                  "TVL1_BATCH_GROUP=0", "TVL1_BATCH_PX1_W=0",
                                  "TVL1_BATCH_PX1_W=150", "TVL1_BATCH_SEG_MIN=0",
-                                 "TVL1_BATCH_SEG_MIN=16"])
+                                 "TVL1_BATCH_SEG_MIN=16", "TVL1_BATCH_SMALL=0"])
 @pytest.mark.parametrize("math", [0, 2])
 def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw, math):
     """kb_warp_iter (fused warp + first pass; 2 consumer wavefronts, or 1 with
@@ -72,6 +72,7 @@ def test_batch_matches_oracle(built, monkeypatch, env, n, w, h, kw, math):
     monkeypatch.delenv("TVL1_BATCH_GROUP", raising=False)
     monkeypatch.delenv("TVL1_BATCH_PX1_W", raising=False)
     monkeypatch.delenv("TVL1_BATCH_SEG_MIN", raising=False)
+    monkeypatch.delenv("TVL1_BATCH_SMALL", raising=False)
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
     p = capi.make_params(fast_math=math, **kw)
@@ -145,6 +146,7 @@ def test_batch_fast_math_within_tolerance(built, monkeypatch, env):
     monkeypatch.delenv("TVL1_BATCH_FUSE", raising=False)
     monkeypatch.delenv("TVL1_BATCH_PX1_W", raising=False)
     monkeypatch.delenv("TVL1_BATCH_SEG_MIN", raising=False)
+    monkeypatch.delenv("TVL1_BATCH_SMALL", raising=False)
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("="))
     kw = dict(nscales=10, warps=5)
