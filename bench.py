@@ -506,6 +506,9 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
             roof = roofline(s0["kernel_bytes"][0], s0["kernel_hbm_bytes"][0], s0["kernel_ms"][0],
                             s0["kernel_launches"][0], TRAFFIC_STRIPS, STRIP_KERNEL)
             roof["timing"] = f"one batch of {B} strip pairs alone on the GPU, after the timed steps"
+            if s0["kernel_launches"][3] > 0:   # kb_small_level: on chip, outside the HBM class
+                roof["coarsest_level_on_chip"] = {"launches": s0["kernel_launches"][3],
+                                                  "ms": round(s0["kernel_ms"][3], 3)}
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if RED_CPU else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

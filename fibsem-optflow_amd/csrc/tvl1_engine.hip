@@ -1653,9 +1653,9 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
         }
         checks[b] += hw[(size_t)n * prm.warps + b];
       }
-      // iteration class: the SURVEY 8(d) bytes of every iteration and warp it ran; from HBM
-      // it only reads I0, I1 and writes u once
-      prof_end(c, st, tks, 0, (double)lw * lh * (64.0 * it_sum + 40.0 * n * prm.warps),
+      // its own class (3): SURVEY 8(d)'s bytes of every iteration and warp it ran, but from HBM
+      // it only reads I0, I1 and writes u once, so it would skew class 0's HBM roofline
+      prof_end(c, st, tks, 3, (double)lw * lh * (64.0 * it_sum + 40.0 * n * prm.warps),
                (double)lw * lh * 16.0 * n);
     }
     for (int wp = 0; wp < (small ? 0 : prm.warps); ++wp) {

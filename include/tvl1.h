@@ -111,7 +111,9 @@ typedef struct tvl1_stats {
   /* Filled only when profiling is enabled (tvl1_set_profiling): HIP-event time,
    * launch count and algorithmic bytes per kernel class, on the solve's stream.
    * Class 0 = fused primal-dual iteration (K6+K8+K7 partials), 1 = warpBackward
-   * (K5), 2 = everything else (convert, pyramid, gradient, upsample, output). */
+   * (K5), 2 = everything else (convert, pyramid, gradient, upsample, output), 3 = a batch's
+   * coarsest level solved on chip in one launch (warps, iterations and stopping rule; bound
+   * on chip, so it stays out of class 0's HBM roofline). */
   double kernel_ms[4];
   int64_t kernel_launches[4];
   double kernel_bytes[4];      /* SURVEY 8(d) algorithmic bytes (64 B/px per iteration for class 0) */

@@ -96,6 +96,22 @@ def test_batch_of_full_frame_geometry_pairs(built):
     check_against_oracle(p, I0s, I1s, u, v, st)
 
 
+@pytest.mark.parametrize("w,h", [(576, 15), (529, 17), (65, 17), (64, 3), (130, 1), (1, 17),
+                                 (7, 2), (300, 12)])
+@pytest.mark.parametrize("kw", [dict(nscales=1, warps=5),
+                                dict(nscales=1, warps=3, epsilon=0.0, iterations=9)])
+def test_batch_coarsest_level_on_chip_edges(built, w, h, kw):
+    """kb_small_level at the edges of what it takes (one level, so the whole solve is the
+    coarsest level): 576 px = 9 full wavefronts, 529 x 17 = its row limit, 65 = a one-lane
+    last wavefront, one row, one column; stopping rule and fixed work (epsilon 0)."""
+    p = capi.make_params(**kw)
+    eng = capi.Engine(p)
+    I0s, I1s = pairs(3, w, h, seed=w * 131 + h)
+    u, v, st = run_batch(eng, I0s, I1s)
+    eng.close()
+    check_against_oracle(p, I0s, I1s, u, v, st)
+
+
 def test_batch_larger_than_one_chunk(built):
     """260 pairs: two chunks (256 + 4), plus an identical pair (stops at n = 2 everywhere)."""
     p = capi.make_params(nscales=3, warps=2)
