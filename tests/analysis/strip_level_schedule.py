@@ -2,7 +2,7 @@
 Per level of the production strip (3072x100, nscales 10, warps 5): iterations per pair and
 the unchecked run lengths between residual checks, over the oracle's check schedules of N
 host-recipe strips, with the rounds of grouped batched passes at most 4 (shipped) or 8
-iterations long (DESIGN 4.6 / 10.-1).  Output: profiles/r5/strips_levels/schedule_model.txt."""
+iterations long (DESIGN 4.6 / 10.1).  Output: profiles/r5/strips_levels/schedule_model.txt."""
 import sys, numpy as np, collections
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[2]

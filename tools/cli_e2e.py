@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--strides", default="1",
                     help="pairs (z, z + s) for each s: a comma list, or A-B for every s in it "
                          "(gen_cross-style long-range pairs; long jobs over one stack)")
+    ap.add_argument("--ab-env", default=None,
+                    help="KEY=VAL[,KEY=VAL]: run each job twice with and twice without these "
+                         "environment settings, alternating, on the same stack")
     args = ap.parse_args()
     d = Path(args.out or tempfile.mkdtemp(prefix="cli_e2e_"))
     d.mkdir(parents=True, exist_ok=True)
@@ -142,6 +145,21 @@ def main():
                 n = len(pairs)
                 print(json.dumps({"job": name, "pinned": pinned, "pairs": n,
                                   "wall_s": round(dt, 3), "pairs_per_s": round(n / dt, 2),
+                                  "steady_pairs_per_s": steady and round(steady, 2)}), flush=True)
+        return
+    if args.ab_env:
+        ab = dict(kv.split("=", 1) for kv in args.ab_env.split(","))
+        for name, extra in jobs.items():
+            for rep in range(4):
+                env = dict(os.environ, **ab) if rep % 2 else None
+                cfg = {"output_dir": str(d / name), "output_type": "random_points",
+                       "matches_file": str(d / name / "pm"), "images": pairs, **extra}
+                (d / name).mkdir(exist_ok=True)
+                dt, steady = run(cfg, d, f"{name}_ab{rep}", env=env)
+                n = len(pairs)
+                print(json.dumps({"job": name, "env": args.ab_env if env else "default",
+                                  "pairs": n, "wall_s": round(dt, 3),
+                                  "pairs_per_s": round(n / dt, 2),
                                   "steady_pairs_per_s": steady and round(steady, 2)}), flush=True)
         return
     for name, extra in jobs.items():
