@@ -233,3 +233,53 @@ def test_postprocess_batch_and_gather_flow(built):
         with pytest.raises(capi.TVL1Error, match="outside"):
             eng.gather_flow(u0.data_ptr(), v0.data_ptr(), n * w * h, np.array([0, bad]))
     eng.close()
+
+
+def test_solve_entry_points_reject_bad_arguments(built):
+    """The reference's CV_Assert-style checks on the solve boundary (tvl1_calc,
+    tvl1_calc_f32, tvl1_calc_batch): null pointers, empty or oversized frames, pitches
+    below the width, batch strides that overlap, a non-positive batch size -- each a status
+    with a message, before any launch; the ctx then still solves a pair bit-exactly."""
+    import ctypes as C
+    eng = capi.Engine(capi.make_params(nscales=2, warps=2))
+    lib, ctx = eng.lib, eng.ctx
+    w, h = 64, 48
+    dev = torch.device("cuda", 0)
+    d0 = torch.zeros((2, h, w), dtype=torch.uint8, device=dev)
+    df = torch.zeros((4, h, w), dtype=torch.float32, device=dev)   # u fields, then v fields
+    i0, f0, g0 = d0.data_ptr(), df.data_ptr(), df[2].data_ptr()
+    EINVAL, ESIZE = 1, 2
+
+    def calc(I0=i0, p0=w, I1=i0, p1=w, W=w, H=h, u=f0, v=g0, fp=4 * w):
+        return lib.tvl1_calc(ctx, C.c_void_p(I0), p0, C.c_void_p(I1), p1, W, H, C.c_void_p(u),
+                             C.c_void_p(v), fp, None, None)
+
+    def batch(n=2, p0=w, s0=w * h, s1=w * h, fs=4 * w * h, W=w, H=h):
+        return lib.tvl1_calc_batch(ctx, n, C.c_void_p(i0), p0, s0, C.c_void_p(i0), w, s1, W, H,
+                                   C.c_void_p(f0), C.c_void_p(g0), 4 * w, fs, None, None)
+
+    cases = [
+        (lambda: calc(I0=0), EINVAL, "null"), (lambda: calc(u=0), EINVAL, "null"),
+        (lambda: calc(W=0), ESIZE, "bad size"), (lambda: calc(H=-3), ESIZE, "bad size"),
+        (lambda: calc(W=1 << 16, H=1 << 16), ESIZE, "too large"),
+        (lambda: calc(p0=w - 1), EINVAL, "pitch"), (lambda: calc(fp=4 * w - 4), EINVAL, "pitch"),
+        (lambda: calc(fp=4 * w + 2), EINVAL, "pitch"),
+        (lambda: lib.tvl1_calc_f32(ctx, C.c_void_p(f0), 4 * w - 4, C.c_void_p(f0), 4 * w, w, h,
+                                   C.c_void_p(f0), C.c_void_p(g0), 4 * w, None, None),
+         EINVAL, "pitch"),
+        (lambda: batch(n=0), EINVAL, "batch size"), (lambda: batch(n=-1), EINVAL, "batch size"),
+        (lambda: batch(s0=w * h - 1), EINVAL, "stride"),
+        (lambda: batch(fs=4 * w * h - 4), EINVAL, "stride"),
+    ]
+    for call, want, msg in cases:
+        rc = call()   # the message is the ctx's last error, so read it right after the call
+        assert rc == want, (rc, want, msg)
+        assert msg in lib.tvl1_last_error(ctx).decode(), msg
+    assert batch(s0=0, s1=0) == 0   # stride 0: every pair shares one frame
+    torch.cuda.synchronize()
+    I0, I1 = synth.gen_pair(w, h, seed=5, z=1)
+    u, v, st, wi = eng.calc_host(I0, I1)
+    eng.close()
+    ur, vr, sr, wr = checker.oracle_calc(I0, I1, eng.params)
+    assert bits_equal(u, ur) and bits_equal(v, vr)
+    np.testing.assert_array_equal(wi, wr)
