@@ -248,6 +248,21 @@ def test_benchmark_pair_bit_exact(engine):
     print(f"C2 pair: {int(wi.sum())} iterations, bit-exact vs oracle")
 
 
+def test_benchmark_pair_bit_exact_fma_mode(engine):
+    """The same C2 pair in fma mode (fast_math = 2, nvcc's -fmad=true contraction restated):
+    bit-identical to the oracle's fma mode at full size, with its own iteration schedule (the
+    bench's `math_modes.fma` leg runs this arithmetic)."""
+    I0, I1 = synth.gen_pair(6144, 4096, seed=0x5EED, z=1)
+    p = capi.make_params(nscales=5, warps=30, fast_math=2)
+    engine.set_params(p)
+    u, v, st, wi = engine.calc_host(I0, I1)
+    ur, vr, sr, wr = checker.oracle_calc(I0, I1, p)
+    assert st["levels"] == sr["levels"] == 5
+    np.testing.assert_array_equal(wi, wr)
+    assert bits_equal(u, ur) and bits_equal(v, vr)
+    print(f"C2 pair, fma mode: {int(wi.sum())} iterations, bit-exact vs the oracle's fma mode")
+
+
 # Profile 1 (SURVEY 8(f) N3): OpenCV's CPU DualTVL1OpticalFlow schedule, bit-identical to
 # its restatement (oracle/tvl1_oracle_dualtvl1.c; parity with OpenCV itself unpinned).
 P1_CASES = [
