@@ -100,11 +100,13 @@ def test_batch_of_full_frame_geometry_pairs(built):
                                  (7, 2), (300, 12)])
 @pytest.mark.parametrize("kw", [dict(nscales=1, warps=5),
                                 dict(nscales=1, warps=3, epsilon=0.0, iterations=9)])
-def test_batch_coarsest_level_on_chip_edges(built, w, h, kw):
+@pytest.mark.parametrize("math", [0, 2])
+def test_batch_coarsest_level_on_chip_edges(built, w, h, kw, math):
     """kb_small_level at the edges of what it takes (one level, so the whole solve is the
     coarsest level): 576 px = 9 full wavefronts, 529 x 17 = its row limit, 65 = a one-lane
-    last wavefront, one row, one column; stopping rule and fixed work (epsilon 0)."""
-    p = capi.make_params(**kw)
+    last wavefront, one row, one column; stopping rule and fixed work (epsilon 0); IEEE and
+    fma mode, each bit-identical to the oracle in that mode."""
+    p = capi.make_params(fast_math=math, **kw)
     eng = capi.Engine(p)
     I0s, I1s = pairs(3, w, h, seed=w * 131 + h)
     u, v, st = run_batch(eng, I0s, I1s)
