@@ -1993,8 +1993,9 @@ __device__ __forceinline__ void roll_lds_read(RollIn<false, 2> &in, unsigned add
       "ds_read_b64 %7, %9 offset:4096\n"
       "ds_read_b64 %8, %9 offset:4608\n"
       "s_waitcnt lgkmcnt(0)"
-      : "=v"(wx), "=v"(wy), "=v"(rh), "=v"(u1), "=v"(u2), "=v"(p11), "=v"(p12), "=v"(p21),
-        "=v"(p22)
+      // early-clobber: the reads after the first one still read the address operand
+      : "=&v"(wx), "=&v"(wy), "=&v"(rh), "=&v"(u1), "=&v"(u2), "=&v"(p11), "=&v"(p12), "=&v"(p21),
+        "=&v"(p22)
       : "v"(addr)
       : "memory");
   in.wx[0] = wx.x; in.wx[1] = wx.y;
