@@ -55,6 +55,11 @@ def _traffic(name="traffic.json"):
 
 TRAFFIC = _traffic()
 TRAFFIC_STRIPS = _traffic("traffic_strips.json")
+# The VALU issue model of the C2 iteration class (tools/issue_model.py --model): the cycles
+# the class keeps its SIMDs busy issuing VALU per launch, every instruction priced at its
+# measured gfx950 throughput cost (tools/issue_rate.hip), from the ISA mix and the PMC counts
+# of one pair alone (profiles/r6/issue/).
+ISSUE_MODEL = _traffic("r6/issue/model.json")
 RED_CPU = False   # reductions on CPU tensors (gloo rehearsal, BENCH_DIST_BACKEND=gloo)
 DIST_BACKEND = None   # the torch.distributed backend in use (None: no process group)
 MATH = {0: "IEEE (bit-identical to oracle/)", 1: "fast (CUDA_FAST_MATH semantics)",
@@ -72,27 +77,37 @@ STRIP_KERNEL = ("batched iteration passes of one tvl1_calc_batch call: kb_iterat
                 "(warpBackward fused with each warp's first pass)")
 
 
-def roofline(k_bytes, k_hbm, k_ms, k_launch, traffic, kernel):
-    """The dominant kernel class against HBM: achieved = the bytes these launches must move
-    (the engine's per-launch accounting of its tiling: band loads with halos + interior
-    stores, checked against the rocprofv3 FETCH_SIZE / WRITE_SIZE passes in profiles/, see
-    `traffic`) / their average HIP-event launch time.  SURVEY 8(d)'s one-pass-per-iteration
-    model (64 B/px per iteration) does not describe a temporally blocked kernel (it would
-    exceed the peak), so it is reported beside the fraction as `model_bytes_over_peak`,
-    never as `frac`."""
+def roofline(k_bytes, k_hbm, k_ms, k_launch, traffic, kernel, issue=None):
+    """The dominant kernel class against its two ceilings.
+
+    hbm: achieved = the bytes these launches must move (the engine's per-launch accounting of
+    its tiling: band loads with halos + interior stores, checked against the rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes in profiles/, see `traffic`) / their average HIP-event
+    launch time.  SURVEY 8(d)'s one-pass-per-iteration model (64 B/px per iteration) does not
+    describe a temporally blocked kernel (it would exceed the peak), so it is reported beside
+    the fraction as `model_bytes_over_peak`, never as `frac`.
+
+    valu (issue = the committed issue model, C2 class only): achieved = the SIMD cycles the
+    class's VALU instructions occupy per launch (each priced at its measured throughput cost)
+    x 1024 SIMDs / the live average launch time; peak = 1024 SIMDs x the clock the PMC run
+    held.  `bound` names the larger fraction: the ceiling the kernels sit closer to (with every
+    HBM access dropped, k_warp_iter takes the same time: DESIGN 10.1)."""
     achieved = k_hbm / (k_ms * 1e-3) / 1e9
     model = k_bytes / (k_ms * 1e-3) / 1e9
-    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+    hbm = {"achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "bytes_per_launch": round(k_hbm / k_launch),
+           "bytes_basis": "engine accounting of the tiling's compulsory HBM bytes (live)",
+           "model_bytes_per_launch": round(k_bytes / k_launch),
+           "model": "SURVEY 8(d): 64 B/px per executed iteration (+ 40 B/px for a fused "
+                    "warpBackward)",
+           "model_bytes_over_peak": round(model / HBM_PEAK_GBS, 4)}
+    r = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": hbm["frac"],
          "traffic": traffic.get("iterate_hbm_bytes_per_launch") if traffic else None,
          "kernel": kernel,
          "launches": k_launch, "avg_launch_us": round(1e3 * k_ms / k_launch, 2),
-         "bytes_per_launch": round(k_hbm / k_launch),
-         "bytes_basis": "engine accounting of the tiling's compulsory HBM bytes (live)",
-         "model_bytes_per_launch": round(k_bytes / k_launch),
-         "model": "SURVEY 8(d): 64 B/px per executed iteration (+ 40 B/px for a fused "
-                  "warpBackward)",
-         "model_bytes_over_peak": round(model / HBM_PEAK_GBS, 4)}
+         "hbm": hbm}
     if traffic:
         r["traffic_source"] = traffic.get("source")
         r["traffic_over_bytes"] = round(traffic["iterate_hbm_bytes_per_launch"] /
@@ -100,7 +115,27 @@ def roofline(k_bytes, k_hbm, k_ms, k_launch, traffic, kernel):
         if traffic.get("iterate_valu_frac") is not None:
             # SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), same class,
             # same workload alone (tools/pmc_single.sh + tools/valu_util.py)
-            r["valu_frac"] = traffic["iterate_valu_frac"]
+            hbm["valu_frac_at_2_cycles"] = traffic["iterate_valu_frac"]
+    if issue and "iteration_class" in issue:
+        ic = issue["iteration_class"]
+        live_us = 1e3 * k_ms / k_launch
+        clk = ic["class_clock_ghz"]
+        v_ach = ic["class_busy_cycles_per_launch"] * 1024 / (live_us * 1e-6) / 1e9
+        v_peak = 1024 * clk
+        valu = {"achieved": round(v_ach, 1), "peak": round(v_peak, 1),
+                "unit": "G SIMD-issue-cycles/s", "frac": round(v_ach / v_peak, 4),
+                "busy_cycles_per_launch": ic["class_busy_cycles_per_launch"],
+                "pmc_frac": ic["class_simd_valu_busy_frac"],
+                "pmc_avg_launch_us": ic["class_avg_launch_us"],
+                "frac_at_2_cycles_per_valu": ic["class_valu_frac_at_2_cycles"],
+                "dominant_kernel": {k: v["simd_valu_busy_frac"] for k, v in ic["kernels"].items()},
+                "model": "tools/issue_model.py: ISA mix x measured throughput cost per "
+                         "instruction class x PMC VALU count, over GRBM_GUI_ACTIVE / 8",
+                "source": "profiles/r6/issue/model.json"}
+        r["valu"] = valu
+        if valu["frac"] > hbm["frac"]:
+            r.update({"bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"],
+                      "unit": valu["unit"], "frac": valu["frac"]})
     return r
 
 
@@ -179,17 +214,29 @@ def cpu_allotment():
     shows the whole machine to os.cpu_count() but allots a share through the cgroup CPU
     quota and OMP_NUM_THREADS; every figure is recorded so the line explains its `cores`."""
     aff = len(os.sched_getaffinity(0))
-    quota = None
+    quota, quota_exact, source = None, None, None
     try:   # cgroup v2: "<quota> <period>" or "max <period>"
         q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        source = "cgroup v2 cpu.max"
         if q != "max":
-            quota = max(1, int(int(q) // int(per)))
+            quota_exact = int(q) / int(per)
     except (OSError, ValueError):
-        pass
+        try:   # cgroup v1: cpu.cfs_quota_us (-1: none) over cpu.cfs_period_us
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            source = "cgroup v1 cpu.cfs_quota_us"
+            if q > 0 and per > 0:
+                quota_exact = q / per
+        except (OSError, ValueError):
+            pass
+    if quota_exact is not None:
+        quota = max(1, int(quota_exact))   # whole threads; the fraction is recorded beside it
     env = os.environ.get("OMP_NUM_THREADS")
     omp = int(env) if env and env.isdigit() and int(env) > 0 else None
     threads = min(x for x in (aff, quota, omp) if x is not None)
-    return {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "omp_num_threads_env": omp,
+    return {"affinity_cpus": aff, "cgroup_quota_cpus": quota,
+            "cgroup_quota_exact": None if quota_exact is None else round(quota_exact, 3),
+            "cgroup_source": source, "omp_num_threads_env": omp,
             "machine_cpus": os.cpu_count(), "threads": threads}
 
 
@@ -624,6 +671,10 @@ def main():
         # a line claiming N GPUs must come from N ranks (n_gpus is WORLD_SIZE)
         sys.exit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE {world} "
                  f"ranks")
+    if os.environ.get("BENCH_LAUNCH_DRYRUN") == "1":   # argument handling only (tests)
+        print(json.dumps({"rank": rank, "world": world, "gpus": args.gpus,
+                          "torch_imported": "torch" in sys.modules}), flush=True)
+        return
     import numpy as np
     import torch
 
@@ -797,7 +848,9 @@ def main():
     roof = None
     if src is not None and src["kernel_ms"][0] > 0:
         roof = roofline(src["kernel_bytes"][0], src["kernel_hbm_bytes"][0], src["kernel_ms"][0],
-                        src["kernel_launches"][0], TRAFFIC, PAIR_KERNEL)
+                        src["kernel_launches"][0], TRAFFIC, PAIR_KERNEL,
+                        ISSUE_MODEL if (W, H, args.nscales, args.warps, args.fast_math,
+                                        args.profile) == (6144, 4096, 5, 30, 0, 0) else None)
         roof["timing"] = "one pair alone on the GPU (the isolated solve after the timed steps)"
     out = {
         "metric": METRIC,

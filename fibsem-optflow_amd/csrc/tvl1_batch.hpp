@@ -82,7 +82,7 @@ struct BatchRing {
 template <int M, int NW, int FM>
 __global__ __launch_bounds__(64 * NW) void kb_warp_ring(BatchRing br) {
   __shared__ float ring[warp_ring_rows<M, NW>() * ring_pitch(64 + 2 * ring_mx<M>())];
-  const int b = br.sel.idx[blockIdx.y];
+  const int b = __builtin_amdgcn_readfirstlane(br.sel.idx[blockIdx.y]);   // uniform: SGPR descriptors
   WarpRingArgs a = br.wa;
   const int us = bsel_bit(br.sel.ubit, b);
   a.I0 = br.I0 + b * br.ips;
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64 * NC + 128) void kb_warp_iter(BatchWI bw) {
   __shared__ float ring[wi_rows<M>() * ring_pitch(wi_ww<M, 128>())];
   __shared__ float cring[2 * 5 * 128];
   __shared__ float hring[NC == 2 ? 2 * kWiH * 128 : 1];
-  const int b = bw.sel.idx[blockIdx.y];
+  const int b = __builtin_amdgcn_readfirstlane(bw.sel.idx[blockIdx.y]);   // uniform: SGPR descriptors
   WarpIterArgs w = bw.w;
   IterArgs &a = w.ra.it;
   {
@@ -295,6 +295,9 @@ __global__ __launch_bounds__(64 * kSmallWaves) void kb_small_level(BatchSmall a)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = blockDim.x >> 6;
   const int W = a.W, H = a.H, P = a.P;
+  // the padded lanes must share lane W-1's wavefront (the gather is not followed by a
+  // barrier): the launch geometry is 64 * ceil(W / 64) threads, nothing else
+  if ((int)blockDim.x != 64 * ((W + 63) / 64)) return;
   const int x = threadIdx.x;
   const bool valid = x < W;
   const int xs = imin(x, W - 1);   // lanes past the level's width compute on column W - 1
@@ -350,8 +353,11 @@ __global__ __launch_bounds__(64 * kSmallWaves) void kb_small_level(BatchSmall a)
         sC[2][y * W + x] = rho_c<FM>(I1wv, I1wxv, I1wyv, cu1, cu2, I0[(size_t)y * P + x]);
       }
     }
-    // procOneScale's iterations (each thread reads only its own column's constants: no
-    // barrier needed after the gather)
+    // procOneScale's iterations.  No barrier after the gather: a lane x < W reads only the
+    // constants it wrote itself, and a padded lane (x >= W) reads column W-1, written by lane
+    // W-1 -- which sits in the same wavefront, because the block is exactly 64 * ceil(W / 64)
+    // threads (the launch; checked at kernel entry), and LDS accesses of one wavefront stay
+    // in program order
     double error = DBL_MAX, prevError = 0.0;
     int n;
     for (n = 0; error > a.thr && n < a.iterations; ++n) {

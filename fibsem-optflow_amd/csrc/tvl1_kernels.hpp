@@ -2558,11 +2558,13 @@ __device__ __forceinline__ void wi_s2_step(WiS2<PX> &S, const float *__restrict_
   }
 }
 
-// NC = 2 also moves the first iteration's TH step from the producers to stage 1's wavefront
+// NC = 2 also moves the first iteration's TH step from the producers to stage 1's wavefront.
+// One block's work: band `band`, output rows ys .. ye-1, residual partial in slot `pslot`.
 template <int M, int FM, int BW, int PRIO = 0, int NC = 1>
-__device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, float *__restrict__ ring,
-                                               float *__restrict__ cring,
-                                               float *__restrict__ hring = nullptr) {
+__device__ __forceinline__ void warp_iter_seg(const WarpIterArgs &w, int band, int ys, int ye,
+                                              int pslot, float *__restrict__ ring,
+                                              float *__restrict__ cring,
+                                              float *__restrict__ hring = nullptr) {
   constexpr int K = 2, PX = BW / 64, HALO = roll_halo<2, PX>(), WW = wi_ww<M, BW>();
   static_assert(BW == 64 || BW == 128, "one producer per 64 columns, PX = 1 or 2");
   static_assert(2 * M + 2 <= wi_rows<M>(), "window ring too small for the margin");
@@ -2577,11 +2579,9 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
   // wave 0 consumer, 1-2 producers (measured: a consumer on wave 1 or 2 of some blocks, or
   // a raised s_setprio for it, is slower).  NC = 2: waves 0 / 1 stages 1 / 2, 2-3 producers
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int band = wid % ra.bands, seg = wid / ra.bands;
   const int X0 = band * (BW - 2 * HALO) - HALO;   // the band's first px
   const unsigned nb = 4u * (unsigned)a.P * (unsigned)a.H;
   const unsigned rowb = 4u * (unsigned)a.P;
-  const int ys = seg * ra.seg_rows, ye = imin(ys + ra.seg_rows, a.H);
   const int r0 = imax(ys - K, 0);
   // consumer steps r0 .. r0 + 3*thirds - 1 >= ye - 1 + K; the producers run one row ahead
   // and 3 (thirds + 1) steps, the consumer 1 + 3 thirds + 2 barriers
@@ -2641,7 +2641,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
       if (a.calc_err) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-        if (lane == 0) a.partials[wid] = acc;
+        if (lane == 0) a.partials[pslot] = acc;
       }
     }
   } else if (NC == 1 && wv == 0) {
@@ -2699,7 +2699,7 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
     if (a.calc_err) {
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-      if (lane == 0) a.partials[wid] = acc;
+      if (lane == 0) a.partials[pslot] = acc;
     }
   } else {
     const int p = wv - NC;
@@ -2754,6 +2754,16 @@ __device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, f
       wi_prod_step<M, FM, BW, THP>(ring, cring, C, B, wa, w, g + 2, p, lane, P, xs, ys, ye, nb, rowb);
     }
   }
+}
+
+template <int M, int FM, int BW, int PRIO = 0, int NC = 1>
+__device__ __forceinline__ void warp_iter_body(const WarpIterArgs &w, int wid, float *__restrict__ ring,
+                                               float *__restrict__ cring,
+                                               float *__restrict__ hring = nullptr) {
+  const RollArgs &ra = w.ra;
+  const int band = wid % ra.bands, seg = wid / ra.bands;
+  const int ys = seg * ra.seg_rows, ye = imin(ys + ra.seg_rows, ra.it.H);
+  warp_iter_seg<M, FM, BW, PRIO, NC>(w, band, ys, ye, wid, ring, cring, hring);
 }
 
 template <int M, int FM = 0, int BW = 128, int PRIO = 1, int NC = 1>

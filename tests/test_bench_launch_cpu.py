@@ -55,10 +55,17 @@ def test_launcher_world_size_must_match_gpus():
 
 def test_launcher_without_gpus_takes_world_size():
     """`torchrun --nproc-per-node 2 bench.py` without --gpus: --gpus defaults to
-    the launcher's WORLD_SIZE, so the mismatch check does not fire (the run then fails on
-    this GPU-less host, later, for want of a device or a rendezvous)."""
-    r = run(["--steps", "1"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    the launcher's WORLD_SIZE, so the mismatch check does not fire; the dry-run switch stops
+    after the argument handling (the test must not depend on the host's GPUs)."""
+    # (tiny geometry, no side lines and the dry-run switch, so that on a host that does have a
+    # GPU the run stays an argument check and cannot start the C2 workload: ADVICE r5)
+    r = run(["--steps", "1", "--warmup", "0", "--width", "64", "--height", "48",
+             "--no-cpu-baseline", "--no-strips-line", "--no-fast-math-line"],
+            WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", BENCH_LAUNCH_DRYRUN="1")
     assert "but the launcher started" not in r.stderr
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["gpus"] == 2 and out["world"] == 2 and out["torch_imported"] is False
 
 
 def test_cpu_allotment_records_the_share(monkeypatch):
@@ -71,6 +78,9 @@ def test_cpu_allotment_records_the_share(monkeypatch):
     assert a["affinity_cpus"] == len(os.sched_getaffinity(0))
     assert a["omp_num_threads_env"] == 3
     assert a["threads"] == min(x for x in (a["affinity_cpus"], a["cgroup_quota_cpus"], 3) if x)
+    assert a["cgroup_source"] in (None, "cgroup v2 cpu.max", "cgroup v1 cpu.cfs_quota_us")
+    if a["cgroup_quota_exact"] is not None:
+        assert a["cgroup_quota_cpus"] == max(1, int(a["cgroup_quota_exact"]))
     monkeypatch.delenv("OMP_NUM_THREADS")
     b = bench.cpu_allotment()
     assert b["omp_num_threads_env"] is None and 1 <= b["threads"] <= b["affinity_cpus"]

@@ -350,3 +350,34 @@ def test_batch_constants_on_demand_regather(built, monkeypatch):
     eng.close()
     assert sum(s["speculation_misses"] for s in st) > 0
     check_against_oracle(p, I0s, I1s, u, v, st)
+
+
+@pytest.mark.parametrize("w,h", [(529, 17), (300, 12)])
+def test_batch_small_level_stopping_decisions_across_thresholds(built, monkeypatch, w, h):
+    """kb_small_level sums the residual in its own order (column sums, then lanes
+    and wavefronts in a fixed order), so its stopping decisions equal the streaming path's only
+    while every check sits further from its threshold than the two sums differ.
+    Pinned empirically here: one level (the whole solve on chip), 16 epsilons spread over
+    0.003 ... 0.06 -- each moves scaledEps, so the checks land at many different distances from
+    the thresholds -- times 6 pairs, solved with the on-chip level and with TVL1_BATCH_SMALL=0:
+    the per-warp iteration counts, the check counts and the flow bits must be identical, and
+    the same as the oracle's for the first and last epsilon."""
+    eps = np.geomspace(0.003, 0.06, 16)
+    I0s, I1s = pairs(6, w, h, seed=w + 7 * h)
+    for k, e in enumerate(eps):
+        out = {}
+        for small in ("1", "0"):
+            monkeypatch.setenv("TVL1_BATCH_SMALL", small)
+            p = capi.make_params(nscales=1, warps=5, epsilon=float(e))
+            eng = capi.Engine(p)
+            out[small] = run_batch(eng, I0s, I1s)
+            eng.close()
+        (u1, v1, s1), (u0, v0, s0) = out["1"], out["0"]
+        for b in range(I0s.shape[0]):
+            np.testing.assert_array_equal(s1[b]["warp_iters"], s0[b]["warp_iters"],
+                                          err_msg=f"eps {e:.5f} pair {b}")
+            assert s1[b]["checks_total"] == s0[b]["checks_total"], (e, b)
+        assert bits_equal(u1, u0) and bits_equal(v1, v0), f"eps {e:.5f}"
+        if k in (0, len(eps) - 1):
+            check_against_oracle(p, I0s, I1s, u1, v1, s1)
+    monkeypatch.delenv("TVL1_BATCH_SMALL", raising=False)

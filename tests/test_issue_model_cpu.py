@@ -1,0 +1,101 @@
+"""The VALU issue model of k_warp_iter and the C2 iteration class, recomputed
+on the CPU from the committed inputs under profiles/r6/issue/: the ISA of the shipped kernels,
+the per-level PMC counters of one C2 pair alone (tools/pmc_issue.sh) and the measured issue
+cost of every instruction class (tools/issue_rate.hip).  It must reproduce the committed
+report (model.json) within 10 %, its ISA-derived instruction counts must match the PMC counts,
+and it must account for the kernel's cycles."""
+import importlib.util
+import json
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+D = ROOT / "profiles" / "r6" / "issue"
+spec = importlib.util.spec_from_file_location("issue_model", ROOT / "tools" / "issue_model.py")
+im = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(im)
+
+
+@pytest.fixture(scope="module")
+def model():
+    m = im.model(D / "k_warp_iter_6_0_128_1_2.s", D / "pmc_issue_c2.csv", D / "issue_rate.txt",
+                 ROOT / "profiles" / "r5" / "wi_roles" / "roles.txt")
+    m["iteration_class"] = im.class_model(D / "pmc_issue_c2.csv", D, D / "issue_rate.txt")
+    return m
+
+
+@pytest.fixture(scope="module")
+def committed():
+    return json.loads((D / "model.json").read_text())
+
+
+def test_reproduces_the_committed_report(model, committed):
+    for lv, d in committed["levels"].items():
+        for k in ("simd_valu_busy_frac", "valu_per_wave_model", "producer_wave_issue_cycles",
+                  "step_cycles", "simd_valu_busy_while_resident"):
+            assert abs(model["levels"][lv][k] / d[k] - 1) < 0.10, (lv, k, model["levels"][lv][k], d[k])
+    a, b = model["iteration_class"], committed["iteration_class"]
+    assert abs(a["class_simd_valu_busy_frac"] / b["class_simd_valu_busy_frac"] - 1) < 0.10
+
+
+def test_three_roles_found_with_their_signatures(model):
+    r = model["roles_per_step"]
+    assert set(r) == {"producer", "stage1", "stage2"}
+    assert r["producer"]["lds_read"] > 4 * r["stage1"]["lds_read"]   # the bicubic gather
+    assert r["stage2"].get("valu_f64", 0) > 0 and r["stage1"].get("valu_f64", 0) == 0  # residual
+    assert all(c["barrier"] == 1.0 for c in r.values())   # one LDS-only barrier per step
+
+
+def test_isa_counts_match_the_pmc_counts(model):
+    """The hot paths from the ISA, times each role's steps of the launch geometry, against the
+    dynamic counts the counters saw: VALU within 8 %, transcendentals and the residual's f64
+    adds within 8 %, LDS instructions within 8 % (the remainder: prologues, epilogues, the
+    gather's out-of-window fallback and the first band's column-0 forms)."""
+    for lv, d in model["levels"].items():
+        for k in ("valu_model_over_pmc", "trans_model_over_pmc", "f64add_model_over_pmc",
+                  "lds_model_over_pmc"):
+            assert 0.92 <= d[k] <= 1.03, (lv, k, d[k])
+
+
+def test_cycles_are_accounted_for(model):
+    """SIMD VALU issue (each instruction at its measured throughput cost) + the launch's ramp
+    and tail + the named latency gap = the kernel's cycles; the issue part is the largest, and
+    while the waves are resident the SIMDs issue VALU >= 75 % of the time on levels 0-3."""
+    for lv, d in model["levels"].items():
+        total = d["simd_valu_busy_frac"] + d["launch_ramp_tail_frac"] + d["latency_gap_frac"]
+        assert abs(total - 1) < 1e-3, (lv, total)
+        assert d["simd_valu_busy_frac"] > max(d["launch_ramp_tail_frac"], d["latency_gap_frac"])
+        if lv != "L4":
+            assert d["simd_valu_busy_while_resident"] >= 0.75, (lv, d)
+    # pricing VALU at the nominal 2 cycles understates the issue load by about a third
+    d0 = model["levels"]["L0"]
+    assert d0["simd_valu_busy_frac"] > 1.4 * d0["simd_valu_frac_at_2_cycles"]
+
+
+def test_issue_cost_table_orders_the_classes():
+    r = im.load_rates(D / "issue_rate.txt")
+    simd = {k: v[8][1] for k, v in r.items()}
+    full = max(simd[k] for k in ("v_add_f32", "v_mul_f32", "v_sub_f32", "v_fmac_f32", "v_and_b32"))
+    half = min(simd[k] for k in ("v_cndmask_b32", "v_max_f32", "v_cmp_gt_f32_e64", "v_add_f64",
+                                 "v_add_f32_dpp wave_shr:1", "v_lshlrev_b32"))
+    trans = min(simd[k] for k in ("v_rcp_f32", "v_sqrt_f32", "v_rsq_f32"))
+    assert full < 3.0 < half < 5.0 < 7.5 < trans
+    assert simd["v_pk_add_f32"] > 2 * simd["v_add_f32"]   # packed f32 is an anti-lever here
+
+
+def test_bench_roofline_names_the_bound_the_model_supports(committed):
+    sys.path.insert(0, str(ROOT))
+    import bench
+    ic = committed["iteration_class"]
+    # a live launch as long as the PMC run's: the VALU fraction equals the model's
+    n = 10
+    k_ms = ic["class_avg_launch_us"] * n / 1e3
+    hbm_bytes = 0.45 * 8e12 * k_ms * 1e-3   # an HBM fraction of 0.45
+    r = bench.roofline(2 * hbm_bytes, hbm_bytes, k_ms, n, None, "class", committed)
+    assert abs(r["valu"]["frac"] / ic["class_simd_valu_busy_frac"] - 1) < 0.01
+    assert r["bound"] == "valu" and r["frac"] == r["valu"]["frac"] and r["hbm"]["frac"] == 0.45
+    # without the model, the HBM roofline as before
+    r = bench.roofline(2 * hbm_bytes, hbm_bytes, k_ms, n, None, "class")
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s"

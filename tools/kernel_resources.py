@@ -19,27 +19,46 @@ LLVM = Path("/opt/rocm/lib/llvm/bin")
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "--offload-arch=gfx950"]
 PASSFLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]   # Makefile PASSFLAGS
 FIELDS = (".vgpr_count", ".sgpr_count", ".vgpr_spill_count", ".sgpr_spill_count",
-          ".group_segment_fixed_size", ".max_flat_workgroup_size")
+          ".group_segment_fixed_size", ".max_flat_workgroup_size", ".agpr_count",
+          ".private_segment_fixed_size")
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def so_objects(so, outdir):
+    """The gfx950 code objects inside a built shared library (lib/libtvl1_hip.so): its
+    .hip_fatbin section holds one offload bundle per translation unit; each is unbundled
+    to outdir/tu<i>.o.  Returns the object paths."""
+    outdir = Path(outdir)
+    fat = outdir / "fatbin"
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", str(so)], check=True,
+                   capture_output=True)
+    data = fat.read_bytes()
+    starts = [m.start() for m in re.finditer(re.escape(BUNDLE_MAGIC), data)] + [len(data)]
+    objs = []
+    for i in range(len(starts) - 1):
+        part = outdir / f"bundle{i}"
+        part.write_bytes(data[starts[i]:starts[i + 1]])
+        obj = outdir / f"tu{i}.o"
+        subprocess.run([str(LLVM / "clang-offload-bundler"), "--unbundle", "--type=o",
+                        f"--input={part}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                        f"--output={obj}"], check=True)
+        objs.append(obj)
+    return objs
 
 
 def notes(obj):
+    """Per kernel, the code-object metadata fields in FIELDS (the AMDGPU metadata note,
+    parsed as the YAML document it is)."""
+    import yaml
     out = subprocess.run([str(LLVM / "llvm-readelf"), "--notes", str(obj)], check=True,
                          capture_output=True, text=True).stdout
-    kernels, cur = [], {}
-    # each kernel's metadata map lists its fields in alphabetical order, after its .args
-    # list (whose items also start with "- ."); a map that holds .sgpr_count is a kernel's
-    for line in out.splitlines():
-        s = line.strip()
-        if s.startswith("- .args:") or s == "- .agpr_count:" or re.match(r"^- \.\w", s):
-            if cur.get(".name") and ".sgpr_count" in cur:
-                kernels.append(cur)
-            cur = {}
-            s = s[2:]
-        m = re.match(r"^(\.[a-z_]+):\s+(\S+)$", s)
-        if m and (m.group(1) in FIELDS or m.group(1) == ".name"):
-            cur[m.group(1)] = m.group(2)
-    if cur.get(".name") and ".sgpr_count" in cur:
-        kernels.append(cur)
+    lines = out.splitlines()
+    i0 = next(i for i, l in enumerate(lines) if l.strip() == "---")
+    i1 = next((i for i in range(i0 + 1, len(lines)) if lines[i].strip() == "..."), len(lines))
+    meta = yaml.safe_load("\n".join(lines[i0 + 1:i1]))
+    kernels = []
+    for k in meta.get("amdhsa.kernels", []):
+        kernels.append({f: str(k[f]) for f in FIELDS + (".name",) if f in k})
     return kernels
 
 
