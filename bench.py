@@ -77,7 +77,7 @@ STRIP_KERNEL = ("batched iteration passes of one tvl1_calc_batch call: kb_iterat
                 "(warpBackward fused with each warp's first pass)")
 
 
-def roofline(k_bytes, k_hbm, k_ms, k_launch, traffic, kernel, issue=None):
+def roofline(k_bytes, k_hbm, k_ms, k_launch, traffic, kernel, issue=None, cls="iteration_class"):
     """The dominant kernel class against its two ceilings.
 
     hbm: achieved = the bytes these launches must move (the engine's per-launch accounting of
@@ -116,8 +116,8 @@ def roofline(k_bytes, k_hbm, k_ms, k_launch, traffic, kernel, issue=None):
             # SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), same class,
             # same workload alone (tools/pmc_single.sh + tools/valu_util.py)
             hbm["valu_frac_at_2_cycles"] = traffic["iterate_valu_frac"]
-    if issue and "iteration_class" in issue:
-        ic = issue["iteration_class"]
+    if issue and cls in issue:
+        ic = issue[cls]
         live_us = 1e3 * k_ms / k_launch
         clk = ic["class_clock_ghz"]
         v_ach = ic["class_busy_cycles_per_launch"] * 1024 / (live_us * 1e-6) / 1e9
@@ -131,7 +131,7 @@ def roofline(k_bytes, k_hbm, k_ms, k_launch, traffic, kernel, issue=None):
                 "dominant_kernel": {k: v["simd_valu_busy_frac"] for k, v in ic["kernels"].items()},
                 "model": "tools/issue_model.py: ISA mix x measured throughput cost per "
                          "instruction class x PMC VALU count, over GRBM_GUI_ACTIVE / 8",
-                "source": "profiles/r6/issue/model.json"}
+                "source": f"profiles/r6/issue/model.json ({cls})"}
         r["valu"] = valu
         if valu["frac"] > hbm["frac"]:
             r.update({"bound": "valu", "achieved": valu["achieved"], "peak": valu["peak"],
@@ -550,8 +550,10 @@ def run_strips(args, rank, world, local_rank, dist, standalone=True):
         s0 = solve(slots[0])[0]
         slots[0]["eng"].set_profiling(False)
         if s0["kernel_ms"][0] > 0:
+            prod = (W, H, args.nscales, args.warps, B, args.fast_math) == (3072, 100, 10, 5, 256, 0)
             roof = roofline(s0["kernel_bytes"][0], s0["kernel_hbm_bytes"][0], s0["kernel_ms"][0],
-                            s0["kernel_launches"][0], TRAFFIC_STRIPS, STRIP_KERNEL)
+                            s0["kernel_launches"][0], TRAFFIC_STRIPS, STRIP_KERNEL,
+                            ISSUE_MODEL if prod else None, "strips_class")
             roof["timing"] = f"one batch of {B} strip pairs alone on the GPU, after the timed steps"
             if s0["kernel_launches"][3] > 0:   # kb_small_level: on chip, outside the HBM class
                 roof["coarsest_level_on_chip"] = {"launches": s0["kernel_launches"][3],

@@ -26,7 +26,8 @@
 //   * build-only keys: "devices" (list of GPU ordinals, pairs sharded over them),
 //     "inflight" (pairs in flight per GPU, default 3), "decode_threads" (slice decode-ahead
 //     pool, default min(16, cores - 1)), "medianFiltering",
-//     "matches_file", "stats_json", "skip_existing", "pinned_host" (page-locked slices and
+//     "matches_file", "stats_json", "timing_json" (per-stage host seconds of strip jobs),
+//     "skip_existing", "pinned_host" (page-locked slices and
 //     flows, default off).
 #include <hip/hip_runtime.h>
 
@@ -159,6 +160,20 @@ struct DeviceCtx {
 };
 
 std::mutex g_io_mutex;
+
+// Per-stage host timing of a job (the build-only "timing_json" key, tools/cli_e2e.py): where
+// a strip job's wall time goes -- band reads on the decode pool, and per batch worker the
+// wait for its chunk's bands, packing, upload, solve, point sampling, flow read-back and
+// output writes.  Seconds of each thread's own clock, summed.
+using Clock = std::chrono::steady_clock;
+const Clock::time_point g_t0 = Clock::now();
+std::atomic<int64_t> g_band_read_ns{0}, g_band_reads{0};
+std::mutex g_stage_mutex;
+Value g_stage_workers;   // one object per batch worker
+
+inline double secs_since(Clock::time_point t) {
+  return std::chrono::duration<double>(Clock::now() - t).count();
+}
 
 // Page-locked host buffers for what crosses PCIe (the reference uploads
 // with GpuMat::upload, optflow.cpp:315-316): the decode pool writes each slice straight
@@ -854,6 +869,7 @@ class DecodePool {
   LoadFuture load_bands(const std::string &path, float scale, std::vector<std::string> keys,
                         int top, int bottom) {
     auto task = std::make_shared<std::packaged_task<std::shared_ptr<Loaded>()>>([=] {
+      const auto t0 = Clock::now();
       auto r = std::make_shared<Loaded>();
       r->ok = ofio::read_gray8_bands(
           path, scale,
@@ -864,9 +880,23 @@ class DecodePool {
             return b;
           },
           r->W, r->H, r->bands, r->err, &r->partial);
+      g_band_read_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+      ++g_band_reads;
       return r;
     });
     LoadFuture f = task->get_future().share();
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      q_.emplace_back([task] { (*task)(); });
+    }
+    cv_.notify_one();
+    return f;
+  }
+
+ // any host job (the strip workers' point sampling runs here while their batch solves)
+  std::shared_future<void> submit(std::function<void()> fn) {
+    auto task = std::make_shared<std::packaged_task<void()>>(std::move(fn));
+    std::shared_future<void> f = task->get_future().share();
     {
       std::lock_guard<std::mutex> lk(m_);
       q_.emplace_back([task] { (*task)(); });
@@ -1231,6 +1261,12 @@ static int from_file(Value &args, bool plan_only) {
       }
       return true;
     };
+    std::map<std::string, double> tm;   // stage -> seconds on this worker (timing_json)
+    size_t t_chunks = 0, t_pairs = 0;
+    const auto t_worker = Clock::now();
+    hipEvent_t ev_up0 = nullptr, ev_up1 = nullptr;   // the chunk's uploads on the stream
+    (void)hipEventCreate(&ev_up0);
+    (void)hipEventCreate(&ev_up1);
     std::map<std::string, LoadFuture> pending;   // path -> its bands (this chunk + the next)
     auto queue_chunk = [&](size_t start) {
       for (size_t k = start; k < std::min(batched.size(), start + bchunk); ++k)
@@ -1262,8 +1298,12 @@ static int from_file(Value &args, bool plan_only) {
         it.im["scale"] = it.im.get("scale", (double)scale).asDouble();
         it.im["output"] = it.im.get("output", args["output_dir"].asString() + "/" +
                                                   it.im["output_name"].asString() + "_" + sbuf);
-        it.p = pending.at(p).get();
-        it.q = pending.at(q).get();
+        {
+          const auto tw = Clock::now();
+          it.p = pending.at(p).get();
+          it.q = pending.at(q).get();
+          tm["wait_bands"] += secs_since(tw);
+        }
         if (!it.p->ok || !it.q->ok || it.p->W != it.q->W || it.p->H != it.q->H) {
           deferred[i] = 1;   // the per-pair path reports or aligns it as the reference does
           continue;
@@ -1332,21 +1372,44 @@ static int from_file(Value &args, bool plan_only) {
             fail("hipMalloc failed for a strip batch", TVL1_ENOMEM);
             break;
           }
+          auto ts = Clock::now();
           for (int b = 0; b < nb; ++b) {
             memcpy(hP + px * b, items[b].p->bands[kk].data.data(), px);
             memcpy(hQ + px * b, items[b].q->bands[kk].data.data(), px);
           }
+          tm["pack"] += secs_since(ts);
+          (void)hipEventRecord(ev_up0, dc.stream);
           if (hipMemcpyAsync(dP, hP, px * nb, hipMemcpyHostToDevice, dc.stream) != hipSuccess ||
               hipMemcpyAsync(dQ, hQ, px * nb, hipMemcpyHostToDevice, dc.stream) != hipSuccess) {
             fail("upload failed", TVL1_EHIP);
             break;
           }
+          (void)hipEventRecord(ev_up1, dc.stream);
           std::vector<tvl1_stats> st(nb);
           std::vector<int32_t> wi((size_t)nb * TVL1_MAX_LEVELS * std::max(1, prm.warps), -1);
           for (int b = 0; b < nb; ++b) {
             memset(&st[b], 0, sizeof st[b]);
             st[b].warp_iterations = wi.data() + (size_t)b * TVL1_MAX_LEVELS * std::max(1, prm.warps);
             st[b].warp_iterations_capacity = TVL1_MAX_LEVELS * std::max(1, prm.warps);
+          }
+          // random_points without debug: which px each pair reports depends only on its
+          // bands' masks, so the draws run on the decode pool while the batch solves (they
+          // were 16 % of a strip worker's time on the worker thread, profiles/r6/cli/)
+          const bool sampled = otype == "random_points" && !debug;
+          std::vector<std::vector<std::pair<int, int>>> pts(nb);
+          std::vector<uint64_t> tot(nb, 0);
+          std::vector<std::shared_future<void>> draws;
+          if (sampled) {
+            const int per = std::max(1, nb / 16);   // 16 jobs of the chunk's pairs
+            for (int b0 = 0; b0 < nb; b0 += per)
+              draws.push_back(pool.submit([&, b0, per, kk] {
+                for (int b = b0; b < std::min(nb, b0 + per); ++b) {
+                  const ofio::Image8 &a = items[b].p->bands[kk], &c = items[b].q->bands[kk];
+                  const int np = items[b].im.get("npoints", args.get("npoints", 25).asInt()).asInt();
+                  pts[b] = sample_points([&](int y) { return a.row(y); }, [&](int y) { return c.row(y); },
+                                         a.width, a.height, np, &tot[b]);
+                }
+              }));
           }
           const auto t0 = std::chrono::steady_clock::now();
           tvl1_status sc = tvl1_calc_batch(dc.ctx, nb, dP, W, px, dQ, W, px, W, h, dU, dV, 4 * (size_t)W,
@@ -1355,22 +1418,24 @@ static int from_file(Value &args, bool plan_only) {
             sc = tvl1_postprocess_batch(dc.ctx, nb, dU, dV, 4 * (size_t)W, 4 * px, dQ, W, px, W, h,
                                         mode, dc.stream);
           if (sc != TVL1_OK) {
+            for (auto &f : draws) f.wait();   // they read this chunk's bands
             fail("strip batch", sc);
             break;
           }
-          const bool sampled = otype == "random_points" && !debug;
+          tm["solve"] += secs_since(t0);   // the batch's host time (it syncs at every check)
+          {
+            float up_ms = 0.0f;   // the uploads, on the GPU clock (done before the first check)
+            if (hipEventElapsedTime(&up_ms, ev_up0, ev_up1) == hipSuccess) tm["upload_gpu"] += 1e-3 * up_ms;
+          }
+          ts = Clock::now();
           std::vector<float> fx, fy;   // whole flows (TIFF outputs, debug point matches)
-          std::vector<std::vector<std::pair<int, int>>> pts(nb);
-          std::vector<uint64_t> tot(nb, 0);
           if (sampled) {
+            for (auto &f : draws) f.wait();
             std::vector<int64_t> off;
-            for (int b = 0; b < nb; ++b) {
-              const ofio::Image8 &a = items[b].p->bands[kk], &c = items[b].q->bands[kk];
-              const int np = items[b].im.get("npoints", args.get("npoints", 25).asInt()).asInt();
-              pts[b] = sample_points([&](int y) { return a.row(y); }, [&](int y) { return c.row(y); },
-                                     W, h, np, &tot[b]);
+            for (int b = 0; b < nb; ++b)
               for (auto &pt : pts[b]) off.push_back((int64_t)(px * b + (size_t)pt.second * W + pt.first));
-            }
+            tm["sample_points_wait"] += secs_since(ts);
+            ts = Clock::now();
             fx.resize(off.size());
             fy.resize(off.size());
             sc = tvl1_gather_flow(dc.ctx, dU, dV, (int64_t)(px * nb), off.data(), (int32_t)off.size(),
@@ -1390,6 +1455,8 @@ static int from_file(Value &args, bool plan_only) {
             }
           }
           const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+          tm["read_back"] += secs_since(ts);
+          ts = Clock::now();
           const Rect r{0, y0, W, h};
           size_t o = 0;
           for (int b = 0; b < nb && ok; ++b) {
@@ -1429,6 +1496,7 @@ static int from_file(Value &args, bool plan_only) {
             dbg_fx[kk].swap(fx);
             dbg_fy[kk].swap(fy);
           }
+          tm["write_outputs"] += secs_since(ts);
         }
         // hP / hQ are reused page-locked buffers: after a failure the chunk's uploads from
         // them may still be queued, so the stream is drained before the retry or the next
@@ -1449,6 +1517,8 @@ static int from_file(Value &args, bool plan_only) {
             }
         }
         if (ok) {
+          ++t_chunks;
+          t_pairs += nb;
           for (int b = 0; b < nb; ++b) {
             const size_t i = items[b].i;
             for (auto &sv : solves[b]) results[i].stats["solves"].append(sv);
@@ -1489,8 +1559,20 @@ static int from_file(Value &args, bool plan_only) {
       }
     }
     if (dc.stream) (void)hipStreamSynchronize(dc.stream);
+    (void)hipEventDestroy(ev_up0);
+    (void)hipEventDestroy(ev_up1);
     release();
     close_device(dc);
+    {
+      Value w;
+      w["device"] = device;
+      w["chunks"] = (int64_t)t_chunks;
+      w["pairs"] = (int64_t)t_pairs;
+      w["worker_s"] = secs_since(t_worker);
+      for (auto &kv : tm) w["stage_s"][kv.first] = kv.second;
+      std::lock_guard<std::mutex> lk(g_stage_mutex);
+      g_stage_workers.append(w);
+    }
   };
 
   // build-only "inflight": pairs solved concurrently per GPU (one worker thread, ctx and
@@ -1573,6 +1655,9 @@ static int from_file(Value &args, bool plan_only) {
   bool any_since = false;
   size_t last_upload = 0;
   int nbatch = 0;
+  // the batches are grouped in pair order (cheap), then serialised and written on the decode
+  // pool in parallel: 40,860 strip pairs' records took 1.6 s on one thread (profiles/r6/cli/)
+  std::vector<std::shared_future<void>> writes;
   auto upload = [&]() {
     const std::string owner = args.get("owner", "flyem").asString();
     const std::string mc = args.get("matchCollection", "forgetful_owner").asString();
@@ -1580,17 +1665,27 @@ static int from_file(Value &args, bool plan_only) {
     const std::string port = args.get("port", "8080").asString();
     const std::string url = "http://" + host + ":" + port + "/render-ws/v1/owner/" + owner +
                             "/matchCollection/" + mc + "/matches";
-    const std::string payload = pending.dump(3);
-    if (debug) printf("%s\n%s", payload.c_str(), url.c_str());
     const std::string path = mfile + "_" + std::to_string(nbatch++) + ".json";
-    FILE *f = fopen(path.c_str(), "w");
-    if (!f) {
-      fprintf(stderr, "cannot write point matches to %s\n", path.c_str());
-      return;
-    }
-    fprintf(f, "%s\n", payload.c_str());
-    fclose(f);
+    auto body = std::make_shared<Value>(std::move(pending));
+    auto job = [body, path, url, debug] {
+      const std::string payload = body->dump(3);
+      if (debug) {
+        std::lock_guard<std::mutex> lk(g_io_mutex);
+        printf("%s\n%s", payload.c_str(), url.c_str());
+      }
+      FILE *f = fopen(path.c_str(), "w");
+      if (!f) {
+        std::lock_guard<std::mutex> lk(g_io_mutex);
+        fprintf(stderr, "cannot write point matches to %s\n", path.c_str());
+        return;
+      }
+      fprintf(f, "%s\n", payload.c_str());
+      fclose(f);
+    };
+    if (debug) job();   // debug prints the payloads in batch order, as the reference does
+    else writes.push_back(pool.submit(job));
   };
+  const auto t_records = Clock::now();
   for (size_t i = 0; i < n; ++i) {
     const Value &im = images[i];
     for (auto &pm : results[i].pms) pending.append(pm);
@@ -1605,6 +1700,24 @@ static int from_file(Value &args, bool plan_only) {
     }
   }
   if (any_since) upload();
+  for (auto &w : writes) w.wait();
+  const double records_s = secs_since(t_records);
+
+  if (args.isMember("timing_json")) {   // build-only: per-stage host timing (tools/cli_e2e.py)
+    Value t;
+    t["wall_s"] = secs_since(g_t0);
+    t["pairs"] = (int64_t)n;
+    t["decode"]["band_reads"] = (int64_t)g_band_reads.load();
+    t["decode"]["band_read_s"] = 1e-9 * (double)g_band_read_ns.load();
+    t["decode"]["threads"] = args.get("decode_threads", (int)std::min(16u, hc - 1)).asInt();
+    t["point_match_records_s"] = records_s;
+    t["batch_workers"] = g_stage_workers.isNull() ? Value() : g_stage_workers;
+    FILE *f = fopen(args["timing_json"].asString().c_str(), "w");
+    if (f) {
+      fprintf(f, "%s\n", t.dump(1).c_str());
+      fclose(f);
+    }
+  }
 
   if (args.isMember("stats_json")) {
     Value st;

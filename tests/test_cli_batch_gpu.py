@@ -175,3 +175,25 @@ def test_batched_strips_over_two_device_workers(stack, tmp_path):
     assert all(e["ok"] for e in s2) and len(s2) == 8
     assert sorted(r2.stdout.splitlines()) == sorted(r1.stdout.splitlines())
     assert {e["solves"][0]["batch"] for e in s2} == {4} and {e["solves"][0]["batch"] for e in s1} == {8}
+
+
+def test_strip_job_stage_timing(stack, tmp_path):
+    """The build-only "timing_json" key: a strip job reports its decode
+    pool's band reads and, per batch worker, the seconds of each stage, and the outputs are the
+    same as without it."""
+    d, _ = stack
+    t = tmp_path / "t"
+    run(job(d, "tif", "flow", t, timing_json=str(tmp_path / "timing.json")), t)
+    run(job(d, "tif", "flow", tmp_path / "u"), tmp_path / "u")
+    assert outputs(t) == outputs(tmp_path / "u")
+    tm = json.loads((tmp_path / "timing.json").read_text())
+    assert tm["pairs"] == Z - 1 + 2 and tm["wall_s"] > 0
+    assert tm["decode"]["band_reads"] >= Z and tm["decode"]["band_read_s"] > 0
+    ws = tm["batch_workers"]
+    assert len(ws) >= 1 and sum(w["pairs"] for w in ws) == tm["pairs"]
+    for w in ws:
+        if w["pairs"]:
+            st = w["stage_s"]
+            for k in ("wait_bands", "pack", "upload_gpu", "solve", "read_back", "write_outputs"):
+                assert k in st and st[k] >= 0, (k, st)
+            assert st["solve"] > 0 and w["worker_s"] >= st["solve"]

@@ -99,3 +99,19 @@ def test_bench_roofline_names_the_bound_the_model_supports(committed):
     # without the model, the HBM roofline as before
     r = bench.roofline(2 * hbm_bytes, hbm_bytes, k_ms, n, None, "class")
     assert r["bound"] == "hbm" and r["unit"] == "GB/s"
+
+
+def test_strips_class_reproduces_and_mixes_match(committed):
+    """The production strips' batched class from its own PMC file: the same report, and each
+    kernel's ISA mix against the counters' transcendental and f32 add/mul/fma shares."""
+    s = im.class_model(D / "pmc_issue_strips.csv", D, D / "issue_rate.txt", im.STRIP_CLASS_KERNELS)
+    c = committed["strips_class"]
+    assert abs(s["class_simd_valu_busy_frac"] / c["class_simd_valu_busy_frac"] - 1) < 0.10
+    for k, v in s["kernels"].items():
+        assert abs(v["trans_share_isa"] - v["trans_share_pmc"]) < 0.01, (k, v)
+        assert abs(v["f32_arith_share_isa"] - v["f32_arith_share_pmc"]) < 0.07, (k, v)
+    # no waterfall loops left in the fused batched first pass (r6): its VALU mix is the single
+    # pair kernel's (the same cost per instruction within 2 %)
+    wi = im.class_model(D / "pmc_issue_c2.csv", D, D / "issue_rate.txt")["kernels"]
+    assert abs(s["kernels"]["kb_warp_iter<6, 0, 2>"]["valu_simd_cost"] /
+               wi["k_warp_iter<6, 0, 128, 1, 2>"]["valu_simd_cost"] - 1) < 0.02

@@ -17,6 +17,12 @@ configurations, each with the decode-ahead pool and with one decode thread:
   * "production strips": scale 0.5, top/bottom 100-row ROIs, reference defaults
     (gen_cross_file_list.py's job shape).
 Output type random_points (the production output) keeps TIFF writes out of the timing.
+Every default run also asks the CLI for its per-stage host timing (the build-only
+"timing_json" key) and prints it beside the rate as `stages`: band reads on the decode pool
+(thread-seconds), and per batch worker the wait for its chunk's bands, packing, upload (GPU
+clock), the batched solve, point sampling, flow read-back and output writes; the stage that
+sets the rate is the one whose thread-seconds per pair, over the threads doing it, come
+closest to the wall time per pair.
 --ab-pinned instead runs each job with the decode pool twice with page-locked slices and
 flows and twice pageable (OPTFLOW_PINNED=1/0, alternating).
 Prints one JSON line per run."""
@@ -171,14 +177,41 @@ def main():
             (d / name).mkdir(exist_ok=True)
             for f in (d / name).glob("pm_*.json"):
                 f.unlink()
+            tj = d / f"{name}_{threads or 'pool'}_timing.json"
+            cfg["timing_json"] = str(tj)
             dt, steady = run(cfg, d, f"{name}_{threads or 'pool'}")
             n = len(pairs)
+            stages = stage_summary(json.loads(tj.read_text()), dt) if tj.exists() else None
             # every pair's point-match record was written (random_points output)
             recs = sum(len(json.loads(f.read_text())) for f in (d / name).glob("pm_*.json"))
             print(json.dumps({"job": name, "decode_threads": threads or "default (pool)",
                               "pairs": n, "point_match_records": recs, "wall_s": round(dt, 3),
                               "pairs_per_s": round(n / dt, 2),
-                              "steady_pairs_per_s": steady and round(steady, 2)}), flush=True)
+                              "steady_pairs_per_s": steady and round(steady, 2),
+                              "stages": stages}), flush=True)
+
+
+def stage_summary(t, wall):
+    """The CLI's timing_json folded into per-stage seconds and the share of the wall time each
+    stage's threads were busy: the decode pool's band reads over its threads, each batch-worker
+    stage summed over the workers and divided by their number (workers run concurrently)."""
+    out = {"wall_s": round(wall, 3), "cli_wall_s": round(t["wall_s"], 3),
+           "point_match_records_s": round(t["point_match_records_s"], 3),
+           "band_reads": t["decode"]["band_reads"],
+           "band_read_s": round(t["decode"]["band_read_s"], 3),
+           "decode_threads": t["decode"]["threads"],
+           "band_read_busy_frac": round(t["decode"]["band_read_s"] / t["decode"]["threads"] / wall, 3)}
+    ws = t.get("batch_workers") or []
+    if ws:
+        tot = {}
+        for w in ws:
+            for k, v in w.get("stage_s", {}).items():
+                tot[k] = tot.get(k, 0.0) + v
+        out["batch_workers"] = len(ws)
+        out["worker_stage_s"] = {k: round(v, 3) for k, v in sorted(tot.items())}
+        out["worker_stage_busy_frac"] = {k: round(v / len(ws) / wall, 3) for k, v in sorted(tot.items())}
+        out["worker_s"] = round(max(w["worker_s"] for w in ws), 3)
+    return out
 
 
 if __name__ == "__main__":

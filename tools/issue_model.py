@@ -617,6 +617,16 @@ def report(m):
                      f"  (@2 cycles {v['valu_frac_at_2_cycles']:.3f})  mix ISA/PMC: trans "
                      f"{v['trans_share_isa']:.3f}/{v['trans_share_pmc']:.3f}, f32 add/mul/fma "
                      f"{v['f32_arith_share_isa']:.3f}/{v['f32_arith_share_pmc']:.3f}")
+    if "strips_class" in m:
+        ic = m["strips_class"]
+        L.append("")
+        L.append("batched iteration class of one production strip batch (256 x 3072x100): SIMD VALU "
+                 f"busy {ic['class_simd_valu_busy_frac']} (priced at 2 cycles: {ic['class_valu_frac_at_2_cycles']})")
+        for k, v in ic["kernels"].items():
+            L.append(f"  {k:32s} cost/VALU {v['valu_simd_cost']:.2f}  busy {v['simd_valu_busy_frac']:.3f}"
+                     f"  (@2 cycles {v['valu_frac_at_2_cycles']:.3f})  mix ISA/PMC: trans "
+                     f"{v['trans_share_isa']:.3f}/{v['trans_share_pmc']:.3f}, f32 add/mul/fma "
+                     f"{v['f32_arith_share_isa']:.3f}/{v['f32_arith_share_pmc']:.3f}")
     if "barrier_share_level0" in m:
         L.append("")
         L.append("barrier share of wave life at level 0 (r5 probe): " +
@@ -644,6 +654,9 @@ if __name__ == "__main__":
     elif a.model:
         m = model(a.isa, a.pmc, a.rates, a.roles)
         m["iteration_class"] = class_model(a.pmc, Path(a.isa).parent, a.rates)
+        sp = Path(a.pmc).parent / "pmc_issue_strips.csv"
+        if sp.exists():   # one production strip batch alone (tools/pmc_issue.sh --strips)
+            m["strips_class"] = class_model(sp, Path(a.isa).parent, a.rates, STRIP_CLASS_KERNELS)
         if a.json:
             Path(a.json).write_text(json.dumps(m, indent=1) + "\n")
         sys.stdout.write(report(m))
