@@ -429,9 +429,9 @@ __global__ __launch_bounds__(64 * kSmallWaves) void kb_small_level(BatchSmall a)
         const float d2 = has_down ? u2[imin(y + 1, R - 1)] : u2[y];
         float q11, q12, q21, q22;
         dual_px<false, false, FM>(u1[y], r1, d1, xs + 1 < W, has_down, a.it.taut, p11[y], p12[y],
-                                  q11, q12);
+                                  q11, q12, a.it.taut_small);
         dual_px<false, false, FM>(u2[y], r2, d2, xs + 1 < W, has_down, a.it.taut, p21[y], p22[y],
-                                  q21, q22);
+                                  q21, q22, a.it.taut_small);
         p11[y] = q11; p12[y] = q12;
         p21[y] = q21; p22[y] = q22;
         __builtin_amdgcn_sched_barrier(0);

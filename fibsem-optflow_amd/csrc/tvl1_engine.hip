@@ -56,6 +56,9 @@ constexpr int kWiMargin = TVL1_WI_M;
 constexpr int kBatchPx1W = 1700;
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+// IterArgs::taut_small: the projection's ng = 1 + taut*g ignores g below 2^-48 when |taut|
+// <= 2^20, so sqrt_nn may skip its (0, 2^-96) form (tvl1_kernels.hpp, sqrt_nn); NaN: false
+inline int taut_small(float taut) { return std::fabs(taut) <= 0x1p20f ? 1 : 0; }
 
 struct Geometry {
   int W = 0, H = 0, L = 0;
@@ -678,6 +681,7 @@ static tvl1_status solve_dualtvl1(tvl1_ctx *c, const Frames &in, int W, int H, f
     a.theta = (float)prm.theta;
     a.gamma = (float)prm.gamma;
     a.taut = taut;
+    a.taut_small = taut_small(taut);
     a.partials = c->partials;
     a.calc_err = 1;
     a.I1wx = c->C[0][0];
@@ -950,6 +954,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     a.theta = theta_f;
     a.gamma = gamma_f;
     a.taut = taut;
+    a.taut_small = taut_small(taut);
     a.partials = c->partials;
     const int nblk = iterate_blocks(lw, lh);
     // Pass kernels: 2-iteration passes (HBM-bound) stream through k_iterate_roll's x-only
@@ -1601,6 +1606,7 @@ static tvl1_status solve_batch_chunk(tvl1_ctx *c, int n, const uint8_t *I0, size
     it.theta = (float)prm.theta;
     it.gamma = 0.0f;
     it.taut = taut;
+    it.taut_small = taut_small(taut);
     // The coarsest level on chip (kb_small_level, one workgroup per pair: every warp's gather,
     // iterations, residuals and stopping rule without leaving the workgroup) when it fits one
     // workgroup's registers and LDS; u enters as 0 in set 0 and leaves there, and p is reset

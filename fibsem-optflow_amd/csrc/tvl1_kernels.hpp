@@ -864,6 +864,7 @@ struct IterArgs {
   int segs, strip_rows;
   float l_t, theta, gamma, taut;
   int calc_err, p_zero;
+  int taut_small;   // host: |taut| <= 2^20, so sqrt_nn may skip its (0, 2^-96) form (0: never)
   // speculation gate: a launch enqueued behind a residual check runs only if
   // that check's k_reduce found the predicted schedule (*gate == gate_seq); null: always
   const unsigned long long *gate;
@@ -1096,10 +1097,36 @@ __device__ __forceinline__ float sqrt_rn_core(float xs) {
 // wavefront into the scaled form, which made the branch slower than a select in the
 // unrolled pipelines (r2).  One unsigned compare finds (0, 2^-96): bits(x) - 1 wraps +0 (and
 // keeps NaN) above bits(2^-96) - 1.
+// The same correctly rounded sqrt from full-rate instructions only (r6): y0 = v_rsq_f32(x +
+// 2^-126), g0 = x*y0, h0 = y0/2, one fma residual d = x - g0^2 and g = g0 + d*h0.  Exhaustive
+// on gfx950 (tools/sqrt_fma_check.hip, candidate C3): equal to RN(sqrt(x)) for every float in
+// [2^-96, 2^128) and for +0 (x + 2^-126 == x from 2^-96 up; at +0 the rsq input is finite and
+// g0 = +0 * y0 = +0, so no select).  It replaces sqrt_rn_core's two neighbour tests -- two
+// half-rate compares and two half-rate selects per sqrt -- with two full-rate instructions:
+// ~15 of the ~35 SIMD issue cycles of a sqrt.  Not for +inf (an inf residual
+// gives NaN), which a sum of squares of finite flow differences cannot reach; the scaled form
+// of (0, 2^-96) keeps sqrt_rn_core (C3 is off by one ulp for 7 of those inputs).
+__device__ __forceinline__ float sqrt_rn_fma(float x) {
+  const float y0 = __builtin_amdgcn_rsqf(x + 0x1p-126f);
+  const float g0 = x * y0;
+  const float h0 = 0.5f * y0;
+  const float d = __builtin_fmaf(-g0, g0, x);
+  return __builtin_fmaf(d, h0, g0);
+}
+
+#ifndef TVL1_SQRT_FMA
+#define TVL1_SQRT_FMA 1   // 0: r5's neighbour-test core on every lane (A/B builds only)
+#endif
+// tiny_exact (wave-uniform): whether x in (0, 2^-96) must get its correctly rounded root.  The
+// only consumer, the projection's ng = 1 + taut*g (dual_px), is exactly 1 whenever |taut*g| <
+// 2^-25, and below 2^-96 both RN(sqrt(x)) and sqrt_rn_fma(x) are under 1.5 * 2^-48 (rsq within
+// 1 ulp, g0 <= sqrt(x), |d*h0| <= sqrt(x)/2): with |taut| <= 2^20 the scaled form cannot change
+// a bit of ng, so dual_px skips its compare and branch then (r6).
 template <bool BR>
-__device__ __forceinline__ float sqrt_nn(float x) {
+__device__ __forceinline__ float sqrt_nn(float x, bool tiny_exact = true) {
   (void)BR;
-  float r = sqrt_rn_core(x);
+  float r = TVL1_SQRT_FMA ? sqrt_rn_fma(x) : sqrt_rn_core(x);
+  if (TVL1_SQRT_FMA && !tiny_exact) return r;
   const bool tiny = __float_as_uint(x) - 1u < __float_as_uint(0x1p-96f) - 1u;
   if (__ballot(tiny)) {
     asm volatile("" ::: "memory");   // keep it a branch (see divergence)
@@ -1109,7 +1136,9 @@ __device__ __forceinline__ float sqrt_nn(float x) {
 }
 
 template <bool BR = false>
-__device__ __forceinline__ float hypot_f(float a, float b) { return sqrt_nn<BR>(a * a + b * b); }
+__device__ __forceinline__ float hypot_f(float a, float b, bool tiny_exact = true) {
+  return sqrt_nn<BR>(a * a + b * b, tiny_exact);
+}
 
 // Correctly rounded a / d for the projection's d = ng = 1 + taut * |grad u| >= 1 (taut >= 0):
 // the compiler's IEEE division sequence (div_scale, refined reciprocal, two fma
@@ -1165,7 +1194,7 @@ __device__ __forceinline__ float th_quot(float rho, float gradv, bool mid) {
 template <bool EXACT = false, bool BR = false, int FM = 0, bool CPUP = false>
 __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_right,
                                         bool has_down, float taut, float pa, float pb, float &oa,
-                                        float &ob) {
+                                        float &ob, bool taut_small = false) {
   const float right = has_right ? ur : uc;
   const float down = has_down ? ud : uc;
   const float ux = right - uc;
@@ -1179,9 +1208,11 @@ __device__ __forceinline__ void dual_px(float uc, float ur, float ud, bool has_r
     ob = fm_fma(taut, uy, pb) * r;
     return;
   }
+  // taut_small (IterArgs, a kernel argument: wave-uniform): |taut| <= 2^20 (see sqrt_nn)
+  const bool tiny_exact = !taut_small;
   const float g = CPUP ? (float)__builtin_sqrt((double)ux * ux + (double)uy * uy)
-                  : contracts(FM) ? sqrt_nn<BR>(fm_fma(ux, ux, uy * uy))
-                                  : hypot_f<BR>(ux, uy);
+                  : contracts(FM) ? sqrt_nn<BR>(fm_fma(ux, ux, uy * uy), tiny_exact)
+                                  : hypot_f<BR>(ux, uy, tiny_exact);
   const float ng = contracts(FM) ? fm_fma(taut, g, 1.0f) : 1.0f + taut * g;
   if (EXACT) {
     oa = (pa + taut * ux) / ng;
@@ -1208,7 +1239,8 @@ template <int PX, bool EXACT = false, int FM = 0, bool CPUP = false>
 __device__ __forceinline__ void dual_component(const float (&uc)[PX], const float (&un)[PX],
                                                bool has_down, int X0, int W, float taut,
                                                const float (&pa)[PX], const float (&pb)[PX],
-                                               float (&oa)[PX], float (&ob)[PX]) {
+                                               float (&oa)[PX], float (&ob)[PX],
+                                               bool taut_small = false) {
   float ur[PX];
   ur[PX - 1] = __shfl_down(uc[0], 1);
 #pragma unroll
@@ -1216,7 +1248,7 @@ __device__ __forceinline__ void dual_component(const float (&uc)[PX], const floa
 #pragma unroll
   for (int k = 0; k < PX; ++k)
     dual_px<EXACT, true, FM, CPUP>(uc[k], ur[k], un[k], X0 + k + 1 < W, has_down, taut, pa[k], pb[k],
-                         oa[k], ob[k]);
+                         oa[k], ob[k], taut_small);
 }
 
 template <bool G, bool EXACT = false, bool CPUP = false>
@@ -1260,10 +1292,10 @@ __global__ __launch_bounds__(kBlock) void k_iterate(IterArgs a) {
         for (int k = 0; k < 4; ++k) { n1[k] = c1[k]; n2[k] = c2[k]; n3[k] = c3[k]; }
       }
       float q11[4], q12[4], q21[4], q22[4], q31[4], q32[4];
-      dual_component<4, EXACT, false, CPUP>(c1, n1, has_down, X0, a.W, a.taut, cur.p11, cur.p12, q11, q12);
-      dual_component<4, EXACT, false, CPUP>(c2, n2, has_down, X0, a.W, a.taut, cur.p21, cur.p22, q21, q22);
+      dual_component<4, EXACT, false, CPUP>(c1, n1, has_down, X0, a.W, a.taut, cur.p11, cur.p12, q11, q12, a.taut_small);
+      dual_component<4, EXACT, false, CPUP>(c2, n2, has_down, X0, a.W, a.taut, cur.p21, cur.p22, q21, q22, a.taut_small);
       if (G)
-        dual_component<4, EXACT, false, CPUP>(c3, n3, has_down, X0, a.W, a.taut, cur.p31, cur.p32, q31, q32);
+        dual_component<4, EXACT, false, CPUP>(c3, n3, has_down, X0, a.W, a.taut, cur.p31, cur.p32, q31, q32, a.taut_small);
       if (writer) {
         const size_t off = (size_t)y * a.P + xa;
         st4(a.u1d, off, c1);
@@ -1408,11 +1440,11 @@ __device__ __forceinline__ void tb_iterate_store(const TBArgs &t,
       unpack(d1, L(2, rowd));
       unpack(d2, L(3, rowd));
       float q11[PX], q12[PX], q21[PX], q22[PX], q31[PX], q32[PX];
-      dual_component<PX, false, FM>(r[g].u1, d1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12);
-      dual_component<PX, false, FM>(r[g].u2, d2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22);
+      dual_component<PX, false, FM>(r[g].u1, d1, has_down, X, a.W, a.taut, r[g].p11, r[g].p12, q11, q12, a.taut_small);
+      dual_component<PX, false, FM>(r[g].u2, d2, has_down, X, a.W, a.taut, r[g].p21, r[g].p22, q21, q22, a.taut_small);
       if (G) {
         unpack(d3, L(5, rowd));
-        dual_component<PX, false, FM>(r[g].u3, d3, has_down, X, a.W, a.taut, r[g].p31, r[g].p32, q31, q32);
+        dual_component<PX, false, FM>(r[g].u3, d3, has_down, X, a.W, a.taut, r[g].p31, r[g].p32, q31, q32, a.taut_small);
       }
 #pragma unroll
       for (int k = 0; k < PX; ++k) {
@@ -1578,11 +1610,11 @@ __device__ __forceinline__ void tb4_iterations(Row<false, 2> (&r)[NR], const int
       const int xd = IN ? 0 : X, wd = IN ? 64 : a.W;   // IN: has_right holds for both px
       float q11[PX], q12[PX], q21[PX], q22[PX];
       if (g < NR - 1) {
-        dual_component<PX, false, FM>(r[g].u1, r[g + 1].u1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12);
-        dual_component<PX, false, FM>(r[g].u2, r[g + 1].u2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22);
+        dual_component<PX, false, FM>(r[g].u1, r[g + 1].u1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12, a.taut_small);
+        dual_component<PX, false, FM>(r[g].u2, r[g + 1].u2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22, a.taut_small);
       } else {
-        dual_component<PX, false, FM>(r[g].u1, d1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12);
-        dual_component<PX, false, FM>(r[g].u2, d2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22);
+        dual_component<PX, false, FM>(r[g].u1, d1, has_down, xd, wd, a.taut, r[g].p11, r[g].p12, q11, q12, a.taut_small);
+        dual_component<PX, false, FM>(r[g].u2, d2, has_down, xd, wd, a.taut, r[g].p21, r[g].p22, q21, q22, a.taut_small);
       }
 #pragma unroll
       for (int k = 0; k < PX; ++k) {
@@ -1904,13 +1936,13 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
       const bool has_right = L.X + j + 1 < a.W;
       dual_px<false, false, FM>(S.U1p[n][j], right_of<PX>(S.U1p[n], j), S.U1c[n][j], has_right,
                                 true, a.taut, S.P11p[n - 1][j], S.P12p[n - 1][j],
-                                S.P11c[n][j], S.P12c[n][j]);
+                                S.P11c[n][j], S.P12c[n][j], a.taut_small);
       dual_px<false, false, FM>(S.U2p[n][j], right_of<PX>(S.U2p[n], j), S.U2c[n][j], has_right,
                                 true, a.taut, S.P21p[n - 1][j], S.P22p[n - 1][j],
-                                S.P21c[n][j], S.P22c[n][j]);
+                                S.P21c[n][j], S.P22c[n][j], a.taut_small);
       if (G)
         dual_px<false, false, FM>(S.U3p[n][j], right_of<PX>(S.U3p[n], j), S.U3c[n][j], has_right, true,
-                a.taut, S.P31p[n - 1][j], S.P32p[n - 1][j], S.P31c[n][j], S.P32c[n][j]);
+                a.taut, S.P31p[n - 1][j], S.P32p[n - 1][j], S.P31c[n][j], S.P32c[n][j], a.taut_small);
     }
     // above the image: p^n(yD < 0) := +0, the p2u the next stage's divergence reads on row 0
     // (divergence<YZ>; OpenCV's y == 0 form).  Only the first K steps of a segment that
@@ -2465,9 +2497,9 @@ __device__ __forceinline__ void wi_s1_step(WiS1<PX> &S, const float *__restrict_
   for (int j = 0; j < PX; ++j) {
     const bool has_right = L.X + j + 1 < a.W;
     dual_px<false, false, FM>(S.U1p[j], right_of<PX>(S.U1p, j), S.U1c[j], has_right, true,
-                              a.taut, S.P11p[j], S.P12p[j], q11[j], q12[j]);
+                              a.taut, S.P11p[j], S.P12p[j], q11[j], q12[j], a.taut_small);
     dual_px<false, false, FM>(S.U2p[j], right_of<PX>(S.U2p, j), S.U2c[j], has_right, true,
-                              a.taut, S.P21p[j], S.P22p[j], q21[j], q22[j]);
+                              a.taut, S.P21p[j], S.P22p[j], q21[j], q22[j], a.taut_small);
     float t3;
     th_px<false, FM>(wx[j], wy[j], rh[j], S.U1c[j], S.U2c[j], 0.0f, a, t1[j], t2[j], t3);
   }
@@ -2540,9 +2572,9 @@ __device__ __forceinline__ void wi_s2_step(WiS2<PX> &S, const float *__restrict_
   for (int j = 0; j < PX; ++j) {
     const bool has_right = L.X + j + 1 < a.W;
     dual_px<false, false, FM>(S.U1p[j], right_of<PX>(S.U1p, j), S.U1c[j], has_right, true,
-                              a.taut, S.Q11p[j], S.Q12p[j], o11[j], o12[j]);
+                              a.taut, S.Q11p[j], S.Q12p[j], o11[j], o12[j], a.taut_small);
     dual_px<false, false, FM>(S.U2p[j], right_of<PX>(S.U2p, j), S.U2c[j], has_right, true,
-                              a.taut, S.Q21p[j], S.Q22p[j], o21[j], o22[j]);
+                              a.taut, S.Q21p[j], S.Q22p[j], o21[j], o22[j], a.taut_small);
   }
   {
     const unsigned vo = L.out && yD >= L.ys && yD < L.ye ? (unsigned)yD * rowb + L.vst : kOOB;

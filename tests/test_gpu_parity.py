@@ -75,6 +75,22 @@ def test_negative_taut_takes_exact_division_path(engine, tau, theta):
     assert bits_equal(u[fin], ur[fin]) and bits_equal(v[fin], vr[fin])
 
 
+@pytest.mark.parametrize("theta", [2.0 ** -22, 1e-7])
+def test_large_taut_bit_exact(engine, theta):
+    """tau/theta = 2^20, the largest |taut| for which the host lets the projection's sqrt skip
+    its scaled form for x in (0, 2^-96) (IterArgs::taut_small), and 2.5e6, which keeps it:
+    bit-exact either way (tools/sqrt_fma_check.hip proves ng unchanged up to 2^20)."""
+    I0, I1 = synth.gen_pair(96, 64, seed=12)
+    p = capi.make_params(nscales=3, warps=2, iterations=12, tau=0.25, theta=theta)
+    engine.set_params(p)
+    u, v, _, wi = engine.calc_host(I0, I1)
+    ur, vr, _, wr = checker.oracle_calc(I0, I1, p)
+    np.testing.assert_array_equal(wi, wr)
+    fin = np.isfinite(ur) & np.isfinite(vr)
+    assert np.array_equal(fin, np.isfinite(u) & np.isfinite(v))
+    assert bits_equal(u[fin], ur[fin]) and bits_equal(v[fin], vr[fin])
+
+
 def test_identity_pair_gives_zero_flow(engine):
     I0, _ = synth.gen_pair(80, 60, seed=3)
     engine.set_params(capi.make_params(nscales=4, warps=3))
