@@ -101,6 +101,16 @@ def test_bench_roofline_names_the_bound_the_model_supports(committed):
     assert r["bound"] == "hbm" and r["unit"] == "GB/s"
 
 
+def test_c2_class_mixes_match(model):
+    """Each C2 iteration-class kernel's hot-path mix (tools/issue_model.py loop_mix) against
+    its counters: transcendental share within 0.01 and f32 add/mul/fma share within 0.03 (r6:
+    loop_mix no longer takes an out-of-line border block's branch back into the body for a
+    loop, which had walked kb_iterate_roll<2, 2> through its division fallbacks)."""
+    for k, v in model["iteration_class"]["kernels"].items():
+        assert abs(v["trans_share_isa"] - v["trans_share_pmc"]) < 0.01, (k, v)
+        assert abs(v["f32_arith_share_isa"] - v["f32_arith_share_pmc"]) < 0.03, (k, v)
+
+
 def test_strips_class_reproduces_and_mixes_match(committed):
     """The production strips' batched class from its own PMC file: the same report, and each
     kernel's ISA mix against the counters' transcendental and f32 add/mul/fma shares."""
@@ -109,7 +119,7 @@ def test_strips_class_reproduces_and_mixes_match(committed):
     assert abs(s["class_simd_valu_busy_frac"] / c["class_simd_valu_busy_frac"] - 1) < 0.10
     for k, v in s["kernels"].items():
         assert abs(v["trans_share_isa"] - v["trans_share_pmc"]) < 0.01, (k, v)
-        assert abs(v["f32_arith_share_isa"] - v["f32_arith_share_pmc"]) < 0.07, (k, v)
+        assert abs(v["f32_arith_share_isa"] - v["f32_arith_share_pmc"]) < 0.03, (k, v)
     # no waterfall loops left in the fused batched first pass (r6): its VALU mix is the single
     # pair kernel's (the same cost per instruction within 2 %)
     wi = im.class_model(D / "pmc_issue_c2.csv", D, D / "issue_rate.txt")["kernels"]

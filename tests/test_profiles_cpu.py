@@ -64,7 +64,7 @@ def test_bench_line_carries_the_contract_fields(bench):
 # ---- rounds 3 and 4: one box, one evidence set each (tools/final_profile.sh ->
 # profiles/r3/final/, profiles/r4/final/): the default bench line, one C2 pair alone and one
 # production strip batch alone
-FINALS = [PROF / "r3" / "final", PROF / "r4" / "final", PROF / "r5" / "final"]
+FINALS = [PROF / "r3" / "final", PROF / "r4" / "final", PROF / "r5" / "final", PROF / "r6" / "final"]
 
 
 def _class_avg_us(stats_csv, prefixes):
@@ -77,7 +77,7 @@ def _class_avg_us(stats_csv, prefixes):
     return ns / calls / 1e3, calls
 
 
-@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4", "r5"])
+@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4", "r5", "r6"])
 @pytest.mark.parametrize("which", ["pair", "strips"])
 def test_final_roofline_reproduces_by_hand(FINAL, which):
     """The bench line's `roofline.frac` (live byte accounting / HIP-event launch time) by hand
@@ -94,6 +94,13 @@ def test_final_roofline_reproduces_by_hand(FINAL, which):
         traffic = json.loads((FINAL / "traffic_strips.json").read_text())
         avg_us, calls = _class_avg_us(FINAL / "kernel_stats_strip_batch.csv",
                                       ("kb_iterate", "kb_warp_iter"))
+    if roof.get("bound") == "valu":
+        # r6: the bound is the VALU issue model's; the same hand check of its timing, then the
+        # HBM roofline beside it as in earlier rounds
+        v = roof["valu"]
+        by_hand = v["busy_cycles_per_launch"] * 1024 / (avg_us * 1e-6) / 1e9 / v["peak"]
+        assert abs(v["frac"] / by_hand - 1) < 0.05, (which, v["frac"], by_hand)
+        roof = roof["hbm"]
     assert calls > 0 and roof["unit"] == "GB/s" and roof["peak"] == 8000.0
     # the timing: the same bytes over the kernel trace's launch average
     by_hand = roof["bytes_per_launch"] / (avg_us * 1e-6) / 8e12
@@ -108,7 +115,7 @@ def test_final_roofline_reproduces_by_hand(FINAL, which):
     assert roof["model_bytes_over_peak"] > 1.0 > roof["frac"]
 
 
-@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4", "r5"])
+@pytest.mark.parametrize("FINAL", FINALS, ids=["r3", "r4", "r5", "r6"])
 def test_final_bench_line_fields(FINAL):
     d = json.loads((FINAL / "bench_c2.json").read_text().splitlines()[-1])
     assert d["config"]["workload"].startswith("C2") and d["n_gpus"] == 1
@@ -117,12 +124,22 @@ def test_final_bench_line_fields(FINAL):
     assert d["production_strips"]["roofline"]["launches"] > 0
 
 
-def test_bench_reads_the_r5_traffic_record():
-    """profiles/traffic*.json (bench.py's `traffic`) are the r5 evidence set's records."""
+def test_bench_reads_the_r6_traffic_record():
+    """profiles/traffic*.json (bench.py's `traffic`) are the r6 evidence set's records."""
     for name in ("traffic.json", "traffic_strips.json"):
         top = json.loads((PROF / name).read_text())
-        r5 = json.loads((PROF / "r5" / "final" / name).read_text())
-        assert top == r5 and "profiles/r5/final/" in top["source"]
+        r6 = json.loads((PROF / "r6" / "final" / name).read_text())
+        assert top == r6 and "profiles/r6/final/" in top["source"]
+
+
+def test_r6_bench_line_names_the_valu_bound():
+    """The r6 evidence line: `roofline.bound` is `valu` from the committed issue model
+    (profiles/r6/issue/model.json), with the HBM roofline beside it, for C2 and the strips."""
+    d = json.loads((PROF / "r6" / "final" / "bench_c2.json").read_text().splitlines()[-1])
+    for r in (d["roofline"], d["production_strips"]["roofline"]):
+        assert r["bound"] == "valu" and r["frac"] == r["valu"]["frac"] > r["hbm"]["frac"]
+        assert "profiles/r6/issue/model.json" in r["valu"]["source"]
+        assert abs(r["valu"]["frac"] / r["valu"]["pmc_frac"] - 1) < 0.10
 
 
 def test_r5_bench_line_carries_rank_records_and_allotment():

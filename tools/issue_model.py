@@ -513,6 +513,11 @@ def loop_mix(ins):
             path = hot_path(ins, h, i)
         except RuntimeError:   # an outer loop: its trip holds an inner loop
             continue
+        if min(path) < h or max(path) > i:
+            # not a loop: an out-of-line block (a border form) branching back into the body,
+            # whose "trip" runs on through the real loop's back edge and around it (r6:
+            # kb_iterate_roll<2, 2> once the sqrt's uniform taut test reshaped the layout)
+            continue
         c = defaultdict(int)
         for k in path:
             c[ins[k][1]] += 1
