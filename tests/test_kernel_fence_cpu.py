@@ -46,6 +46,18 @@ def kernels(objects):
     return ks
 
 
+def test_reading_the_library_leaves_it_untouched(tmp_path):
+    """so_objects must not write the library: objcopy given only an input rewrites it in place,
+    which made a pytest process that had the engine loaded (tests/test_homography_cpu.py) die
+    with SIGSEGV at exit after every test passed (r6)."""
+    if not LIB.exists():
+        pytest.skip("lib/libtvl1_hip.so not built")
+    before = LIB.stat()
+    kr.so_objects(LIB, tmp_path)
+    after = LIB.stat()
+    assert (after.st_mtime_ns, after.st_size) == (before.st_mtime_ns, before.st_size)
+
+
 def test_two_translation_units(objects):
     # tvl1_engine.hip and tvl1_passes.hip (DESIGN 4.10): both bundles must be read
     assert len(objects) == 2

@@ -30,8 +30,10 @@ def so_objects(so, outdir):
     to outdir/tu<i>.o.  Returns the object paths."""
     outdir = Path(outdir)
     fat = outdir / "fatbin"
-    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", str(so)], check=True,
-                   capture_output=True)
+    # an explicit output file: given only the input, objcopy rewrites it in place -- the
+    # library the calling process (or another) may have mapped, which then faulted at exit
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", str(so),
+                    str(outdir / "so_copy")], check=True, capture_output=True)
     data = fat.read_bytes()
     starts = [m.start() for m in re.finditer(re.escape(BUNDLE_MAGIC), data)] + [len(data)]
     objs = []
