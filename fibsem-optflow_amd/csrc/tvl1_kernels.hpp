@@ -1101,11 +1101,12 @@ __device__ __forceinline__ float sqrt_rn_core(float xs) {
 // 2^-126), g0 = x*y0, h0 = y0/2, one fma residual d = x - g0^2 and g = g0 + d*h0.  Exhaustive
 // on gfx950 (tools/sqrt_fma_check.hip, candidate C3): equal to RN(sqrt(x)) for every float in
 // [2^-96, 2^128) and for +0 (x + 2^-126 == x from 2^-96 up; at +0 the rsq input is finite and
-// g0 = +0 * y0 = +0, so no select).  It replaces sqrt_rn_core's two neighbour tests -- two
-// half-rate compares and two half-rate selects per sqrt -- with two full-rate instructions:
-// ~15 of the ~35 SIMD issue cycles of a sqrt.  Not for +inf (an inf residual
-// gives NaN), which a sum of squares of finite flow differences cannot reach; the scaled form
-// of (0, 2^-96) keeps sqrt_rn_core (C3 is off by one ulp for 7 of those inputs).
+// g0 = +0 * y0 = +0, so no select).  sqrt_rn_core issues v_sqrt, two integer adds, two fmas,
+// two half-rate compares and two half-rate selects; this issues v_rsq and five full-rate
+// instructions: ~15 of a sqrt's ~35 SIMD issue cycles (DESIGN.md §4.7 of r6).  Not for +inf
+// (an inf residual gives NaN), which a sum of squares of finite flow differences cannot
+// reach; the scaled form of (0, 2^-96) keeps sqrt_rn_core (C3 is off by one ulp for 7 of
+// those inputs).
 __device__ __forceinline__ float sqrt_rn_fma(float x) {
   const float y0 = __builtin_amdgcn_rsqf(x + 0x1p-126f);
   const float g0 = x * y0;
@@ -1121,7 +1122,7 @@ __device__ __forceinline__ float sqrt_rn_fma(float x) {
 // only consumer, the projection's ng = 1 + taut*g (dual_px), is exactly 1 whenever |taut*g| <
 // 2^-25, and below 2^-96 both RN(sqrt(x)) and sqrt_rn_fma(x) are under 1.5 * 2^-48 (rsq within
 // 1 ulp, g0 <= sqrt(x), |d*h0| <= sqrt(x)/2): with |taut| <= 2^20 the scaled form cannot change
-// a bit of ng, so dual_px skips its compare and branch then (r6).
+// a bit of ng, so dual_px skips its compare and branch then (DESIGN.md §4.7 of r6).
 template <bool BR>
 __device__ __forceinline__ float sqrt_nn(float x, bool tiny_exact = true) {
   (void)BR;
