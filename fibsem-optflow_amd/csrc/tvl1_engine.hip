@@ -86,6 +86,7 @@ struct tvl1_ctx {
   float *U[2][3] = {};   // u1, u2, u3
   float *Pd[2][6] = {};  // p11, p12, p21, p22, p31, p32
   float *C[2][3] = {};   // two sets of warp constants I1wx, I1wy, rho_c (speculation)
+  float *Mid = nullptr;  // k_iterate_roll_mid's state after 2 iterations: u1, u2, p11..p22
   uint8_t *in0 = nullptr, *in1 = nullptr;   // staging for tvl1_calc_host
   float *outu = nullptr, *outv = nullptr;
   double *partials = nullptr;
@@ -135,6 +136,11 @@ struct tvl1_ctx {
                              // run past the first check).  4 M since the two-consumer form
                              // (C2's 4.2 Mpx level 4: one pair alone -3.7 %, in flight +0.3 %)
   int witer_slots = 0;       // resident k_warp_iter<6, -, 128, 1, wi_nc> blocks per device
+  int mid = 0;               // TVL1_MID=1: mid-check passes (k_iterate_roll_mid, DESIGN.md
+                             // §4.1 of r6): two 2-iteration passes of a converging warp as one
+  double mid_min = 1.1;      // TVL1_MID_MIN: ... when the check before them read at least this
+                             // many eps^2 W H (the first of the two checks then rarely stops)
+  int mid_slots = 0;         // resident k_iterate_roll_mid wavefronts
   int wi_nc = 2;             // TVL1_WI_NC: k_warp_iter consumer wavefronts (2: one per
                              // iteration of the pass; 1: both on one wave)
   // batch arena (tvl1_calc_batch): per logical plane, kBatchMax pairs' copies
@@ -455,6 +461,7 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H, hipStream_t st) {
   bytes += 2 * 3 * plane;                   // U[2][3]
   bytes += 2 * 6 * plane;                   // Pd[2][6]
   bytes += 2 * 3 * plane;                   // C[2]
+  bytes += 6 * plane;                       // Mid
   bytes += 2 * align_up(P0 * H, 256);       // in0, in1 (u8)
   bytes += 2 * plane;                       // outu, outv
   // residual partials: k_iterate_tb worst case (RH 32 at 4 iterations: 56 x 24 px per
@@ -489,6 +496,7 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H, hipStream_t st) {
     for (int k = 0; k < 6; ++k) c->Pd[b][k] = (float *)take(plane);
   for (int b = 0; b < 2; ++b)
     for (int k = 0; k < 3; ++k) c->C[b][k] = (float *)take(plane);
+  c->Mid = (float *)take(6 * plane);        // six planes at the plane stride (one RollBufs group)
   c->in0 = (uint8_t *)take(P0 * H);
   c->in1 = (uint8_t *)take(P0 * H);
   c->outu = (float *)take(plane);
@@ -562,11 +570,12 @@ static double survey_bytes(const Geometry &g, int warps, const int64_t *iters) {
 // it (speculation): launch_check enqueues k_reduce (residual slot and event by the
 // parity of its sequence number, so the next check cannot overwrite a residual the host has
 // not read yet), wait_check reads it.
+// (first: the partials start there: a mid-check pass's first check, k_iterate_roll_mid)
 static tvl1_status launch_check(tvl1_ctx *c, hipStream_t st, int nparts, const CheckGate &g,
-                                unsigned long long *seq_out) {
+                                unsigned long long *seq_out, int first = 0) {
   unsigned long long *seq_dev = (unsigned long long *)(c->pinned_dev + 1);
   const unsigned long long seq = ++c->check_seq;
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials, nparts,
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kBlock), 0, st, c->partials + first, nparts,
                      c->pinned_dev + ((seq & 1) ? 2 : 0), c->poll ? seq_dev : nullptr, seq, g);
   HIP_TRY(c, hipGetLastError());
   if (!c->poll) HIP_TRY(c, hipEventRecord(c->ev_check[seq & 1], st));
@@ -844,6 +853,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
   int64_t level_iters[TVL1_MAX_LEVELS] = {};
   int64_t checks = 0;
   int32_t spec_misses = 0;   // speculative launches that ran empty
+  int mid_passes = 0, mid_taken = 0;   // mid-check passes; of those, ended on the mid state
   // share of the resident slots a streaming launch is sized for: all of them for a solve
   // alone on its device, fill_shared while other solves are in progress (their blocks fill
   // the rest instead of waiting for this launch's last round).  Segmentation never changes
@@ -874,6 +884,8 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     b.cb = (unsigned)group_bytes(s, 3);
     b.ub = (unsigned)group_bytes(s, gam ? 3 : 2);
     b.pb = (unsigned)group_bytes(s, gam ? 6 : 4);
+    b.m = c->Mid;
+    b.mb = (unsigned)group_bytes(s, 6);
     return b;
   };
   auto gather = [&](int s, int uset, int cbuf, int wp) -> tvl1_status {  // K5 warpBackward
@@ -970,7 +982,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     // (storing the constants if store_c).  gate: a speculative launch
     auto launch_pass = [&](int k, bool calc_end, bool witer, bool store_c, int ui, int pi, int cb,
                            bool p_zero, const unsigned long long *gate, unsigned long long gseq,
-                           int wp, int n, int &blocks_out) -> tvl1_status {
+                           int wp, int n, int &blocks_out, bool midp = false) -> tvl1_status {
         a.u1s = c->U[ui][0]; a.u2s = c->U[ui][1]; a.u3s = c->U[ui][2];
         a.u1d = c->U[ui ^ 1][0]; a.u2d = c->U[ui ^ 1][1]; a.u3d = c->U[ui ^ 1][2];
         a.p11s = c->Pd[pi][0]; a.p12s = c->Pd[pi][1]; a.p21s = c->Pd[pi][2];
@@ -1047,15 +1059,18 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           const int halo = (k + px - 1) / px * px;   // roll_halo<K, PX>
           const int out_w = 64 * px - 2 * halo;
           ra.bands = (lw + out_w - 1) / out_w;
+          const int slots = midp ? c->mid_slots : c->roll_slots[k][gam][px];
           const int seg = c->roll_seg > 0 ? std::max(c->roll_seg, kRollMinSeg)
-                                           : roll_segment(ra.bands, lh, k, c->roll_slots[k][gam][px] * fill_now() / 100);
+                                           : roll_segment(ra.bands, lh, k, slots * fill_now() / 100);
           ra.seg_rows = seg;
           const int segs = (lh + seg - 1) / seg;
           ra.waves = ra.bands * segs;
-          blocks = ra.waves;  // one residual partial per wavefront
-          if (blocks > c->partials_cap)
+          blocks = ra.waves;  // one residual partial per wavefront (two for the mid pass)
+          if ((midp ? 2 : 1) * blocks > c->partials_cap)
             return set_err(c, TVL1_EHIP, "internal: %d wavefronts > partials capacity %d", blocks,
                            c->partials_cap);
+          if (midp && (k != 4 || px != 2 || gam || !calc_end))
+            return set_err(c, TVL1_EHIP, "internal: mid-check pass of k = %d, px = %d", k, px);
           const dim3 grid((ra.waves + 3) / 4);
 #define ROLL_G(K, PX) \
   hipLaunchKernelGGL((k_iterate_roll<true, K, PX>), grid, dim3(256), 0, st, ra);
@@ -1074,7 +1089,10 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
   } else {                              \
     ROLL_M(kIEEE, K, PX)                \
   }
-          if (px == 4) {   // k <= 2
+#define MID_M(FM) hipLaunchKernelGGL((k_iterate_roll_mid<FM>), grid, dim3(256), 0, st, ra);
+          if (midp) {
+            MATH_SWITCH(math, MID_M)
+          } else if (px == 4) {   // k <= 2
             if (k == 1) {
               ROLL(1, 4)
             } else {
@@ -1088,6 +1106,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
               default: ROLL(4, 2) break;
             }
           }
+#undef MID_M
 #undef ROLL
 #undef ROLL_M
 #undef ROLL_G
@@ -1097,7 +1116,8 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
             const int ys = sg * seg, ye = std::min(ys + seg, lh);
             rows += std::min(ye - 1 + k, lh - 1) - std::max(ys - k, 0) + 1;
           }
-          hbm = (double)ra.bands * 64.0 * px * rows * 4.0 * ld_planes + Nl * 4.0 * st_planes;
+          hbm = (double)ra.bands * 64.0 * px * rows * 4.0 * ld_planes + Nl * 4.0 * st_planes *
+                (midp ? 2.0 : 1.0);
         } else if (c->tb4 && !gam) {   // 64 x 48 regions, 3 rows x 2 px per thread
           TBArgs t;
           t.it = a;
@@ -1152,6 +1172,9 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     const bool fuse = c->fuse && !gam && !exact_div && roll_ok && prm.epsilon > 0 &&
                       prm.iterations >= 2 && (long)lw * lh >= c->fuse_min;
     const int kmax = exact_div ? 1 : roll_ok ? kRollMax : kTbMax;
+    // the mid-check pass (k_iterate_roll_mid) where a 4-iteration pass streams
+    const bool mid_ok = !gam && !exact_div && roll_long && prm.epsilon > 0 && kRollMax >= 4 &&
+                        group_bytes(s, 6) < c->buf_limit;
     // Speculation: behind each residual check the host enqueues the launch it
     // expects to follow, gated on the device by the check's own evaluation of the stopping
     // rule, and only then waits for the residual.  A right guess hides the host round trip;
@@ -1284,6 +1307,60 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
           double prev_sim = prevError;
           const int k = sched_after(prevError, scaledEps, n, prm.iterations, kmax,
                                     prm.epsilon > 0, &calc_end, &prev_sim);
+          // A converging warp (a check every second iteration, the error just above eps^2 W H)
+          // runs its next two 2-iteration passes as one k_iterate_roll_mid pass: both checks'
+          // residuals, the state after 2 iterations in c->Mid and after 4 in the usual set.
+          // The host reads the first check as procOneScale does; if the warp stops there (or
+          // its schedule is not a second 2-iteration pass) the mid state is taken instead
+          // (DESIGN.md §4.1 of r6).  Not for a warp's first check (n = 2: its error drops the
+          // most), nor where the 4-iteration pass does not stream.
+          if (c->mid && mid_ok && k == 2 && calc_end && n > 2 && n + 4 <= prm.iterations &&
+              prevError >= c->mid_min * scaledEps) {
+            int blocks = 0;
+            TRY(launch_pass(4, true, false, false, ui, pi, cb, p_zero, nullptr, 0, wp, n, blocks, true));
+            unsigned long long seq_mid = 0, seq_end = 0;
+            TRY(launch_check(c, st, blocks, CheckGate{}, &seq_mid, blocks));
+            TRY(launch_check(c, st, blocks, CheckGate{}, &seq_end));
+            auto note = [&](double e, int nn) {   // the bookkeeping of a check read below
+              ++checks;
+              h.r0 = h.r1;
+              h.n0 = h.n_last;
+              h.r1 = e / scaledEps;
+              h.n_last = nn;
+              if ((size_t)nn < nact) act_cur[nn] = act_of(e, nn);
+            };
+            double e_mid = 0.0;
+            TRY(wait_check(c, st, seq_mid, &e_mid));
+            n += 2;
+            note(e_mid, n);
+            ++mid_passes;
+            bool ce2 = false;
+            double prev2 = 0.0;
+            const bool stop = !(e_mid > scaledEps && n < prm.iterations);
+            if (!stop &&
+                sched_after(e_mid, scaledEps, n, prm.iterations, kmax, 1, &ce2, &prev2) == 2 && ce2) {
+              double e_end = 0.0;   // the second check: the next pass's own
+              TRY(wait_check(c, st, seq_end, &e_end));
+              n += 2;
+              note(e_end, n);
+              error = e_end;
+              prevError = e_end;
+            } else {   // the state after the first 2 iterations: the set a 2-iteration pass writes
+              ++mid_taken;
+              const size_t bytes = (size_t)P * lh * sizeof(float);
+              float *dst[6] = {c->U[ui ^ 1][0], c->U[ui ^ 1][1], c->Pd[pi ^ 1][0],
+                               c->Pd[pi ^ 1][1], c->Pd[pi ^ 1][2], c->Pd[pi ^ 1][3]};
+              for (int q = 0; q < 6; ++q)
+                HIP_TRY(c, hipMemcpyAsync(dst[q], (const char *)c->Mid + q * pstride, bytes,
+                                          hipMemcpyDeviceToDevice, st));
+              error = e_mid;
+              prevError = e_mid;
+            }
+            p_zero = false;
+            ui ^= 1;
+            pi ^= 1;
+            continue;
+          }
           const bool witer = fuse && n == 0 && k == 2 && calc_end;
           // the constants go to HBM only when the warp may run further passes: always for
           // a level's first warp, else when the previous warp did not stop at its first
@@ -1456,6 +1533,8 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     stats->speculation_misses = spec_misses;
     stats->algorithmic_bytes = survey_bytes(g, prm.warps, level_iters);
   }
+  if (c->spec_trace && mid_passes)
+    fprintf(stderr, "mid-check passes %d, ended on the mid state %d\n", mid_passes, mid_taken);
   return TVL1_OK;
 }
 
@@ -2338,6 +2417,8 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
   if (const char *m = getenv("TVL1_ROLL_SEG")) c->roll_seg = atoi(m);
   if (const char *m = getenv("TVL1_ROLL_PX4_MIN")) c->roll_px4_min = atol(m);
   if (const char *m = getenv("TVL1_FUSE")) c->fuse = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_MID")) c->mid = atoi(m) != 0;
+  if (const char *m = getenv("TVL1_MID_MIN")) c->mid_min = atof(m);
   if (const char *m = getenv("TVL1_WI_NC")) c->wi_nc = atoi(m) == 1 ? 1 : 2;
   if (const char *m = getenv("TVL1_TB4")) c->tb4 = atoi(m) != 0;
   if (const char *m = getenv("TVL1_POLL")) c->poll = atoi(m);
@@ -2387,6 +2468,7 @@ tvl1_status tvl1_create(tvl1_ctx **out, int device, const tvl1_params *params) {
     ROLL_SLOTS(true, 1, 2) ROLL_SLOTS(true, 2, 2) ROLL_SLOTS(true, 3, 2) ROLL_SLOTS(true, 4, 2)
     ROLL_SLOTS(false, 1, 4) ROLL_SLOTS(false, 2, 4) ROLL_SLOTS(true, 1, 4) ROLL_SLOTS(true, 2, 4)
 #undef ROLL_SLOTS
+    c->mid_slots = 4 * blocks_of((const void *)k_iterate_roll_mid<kIEEE>, 256);
     c->kb1_slots[1] = 4 * blocks_of((const void *)kb_iterate_roll<1, 1, kIEEE>, 256);
     c->kb1_slots[2] = 4 * blocks_of((const void *)kb_iterate_roll<2, 1, kIEEE>, 256);
     c->kb1_slots[3] = 4 * blocks_of((const void *)kb_iterate_roll<3, 1, kIEEE>, 256);

@@ -1739,6 +1739,8 @@ struct RollBufs {
   float *ud, *pd;          // u, p written
   unsigned cb, ub, pb;     // group bytes (descriptor records) of c, u, p
   unsigned pstride;        // bytes between the planes of a group
+  float *m;                // k_iterate_roll_mid: u1, u2, p11, p12, p21, p22 after 2 iterations
+  unsigned mb;             // its group bytes
 };
 
 struct RollArgs {
@@ -1836,10 +1838,13 @@ __device__ __forceinline__ float right_of(const float (&v)[PX], int j) {
 // the dependency list above; the border forms select, never combine).
 // VIN: in.u1 / u2 / u3 hold stage 1's v = u^0 + TH step (th_px, computed by the caller)
 // instead of u^0
-template <bool G, int K, int PX, bool VIN = false, int FM = 0>
+// MID (k_iterate_roll_mid): stage 2 also sums its residual into *accm and stores u^2 / p^2 to
+// the mid group B.m
+template <bool G, int K, int PX, bool VIN = false, int FM = 0, bool MID = false>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                              const IterArgs &a, const RollBufs &B, int r,
-                                             const RollLane &L, unsigned rowb, double &acc);
+                                             const RollLane &L, unsigned rowb, double &acc,
+                                             double *accm = nullptr);
 
 template <bool G, int K, int PX, int FM, int AH>
 __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
@@ -1856,12 +1861,14 @@ __device__ __forceinline__ void roll_step(RollPipe<G, K, PX> &S, const RollIn<G,
 
 // The compute and stores of one step: input row r (in `in`) enters stage 0 and every
 // stage advances one row.
-template <bool G, int K, int PX, bool VIN, int FM>
+template <bool G, int K, int PX, bool VIN, int FM, bool MID>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                              const IterArgs &a, const RollBufs &B, int r,
-                                             const RollLane &L, unsigned rowb, double &acc) {
+                                             const RollLane &L, unsigned rowb, double &acc,
+                                             double *accm) {
   const unsigned ps = B.pstride;
   static_assert(!VIN || K >= 2, "stage 1's u^0 (replaced by v) is the K = 1 residual's input");
+  static_assert(!MID || (!G && K == 4 && !VIN), "the mid check: the 4-iteration pass, gamma = 0");
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     // shift every stage one row down
@@ -1912,6 +1919,10 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
         const float e = residual_px<FM>(S.U1p[n - 1][j] - n1, S.U2p[n - 1][j] - n2);
         acc += stU && L.X + j < a.W ? (double)e : 0.0;
       }
+      if (MID && n == 2) {   // the check after this pass's first 2 iterations
+        const float e = residual_px<FM>(S.U1p[n - 1][j] - n1, S.U2p[n - 1][j] - n2);
+        *accm += stU && L.X + j < a.W ? (double)e : 0.0;
+      }
       S.U1c[n][j] = n1; S.U2c[n][j] = n2; if (G) S.U3c[n][j] = n3;
     }
     // below the image: u^n(yU) := u^n(yU - 1), so the projection's y-difference at row H-1
@@ -1922,6 +1933,11 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
       for (int j = 0; j < PX; ++j) {
         S.U1c[n][j] = S.U1p[n][j]; S.U2c[n][j] = S.U2p[n][j]; if (G) S.U3c[n][j] = S.U3p[n][j];
       }
+    }
+    if (MID && n == 2) {   // u^2 to mid planes 0, 1
+      const unsigned vo = stU ? (unsigned)yU * rowb + L.vst : kOOB;
+      bstorev<PX>(B.m, B.mb, vo, S.U1c[n]);
+      bstorev<PX>(B.m, B.mb, vo, S.U2c[n], ps);
     }
     if (n == K) {
       const unsigned vo = stU ? (unsigned)yU * rowb + L.vst : kOOB;
@@ -1954,6 +1970,13 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
         S.P11c[n][j] = S.P12c[n][j] = S.P21c[n][j] = S.P22c[n][j] = 0.0f;
         if (G) S.P31c[n][j] = S.P32c[n][j] = 0.0f;
       }
+    }
+    if (MID && n == 2) {   // p^2 to mid planes 2 .. 5
+      const unsigned vo = L.out && yD >= L.ys && yD < L.ye ? (unsigned)yD * rowb + L.vst : kOOB;
+      bstorev<PX>(B.m, B.mb, vo, S.P11c[n], 2 * ps);
+      bstorev<PX>(B.m, B.mb, vo, S.P12c[n], 3 * ps);
+      bstorev<PX>(B.m, B.mb, vo, S.P21c[n], 4 * ps);
+      bstorev<PX>(B.m, B.mb, vo, S.P22c[n], 5 * ps);
     }
     if (n == K) {
       const unsigned vo = L.out && yD >= L.ys && yD < L.ye ? (unsigned)yD * rowb + L.vst : kOOB;
@@ -2048,18 +2071,23 @@ __device__ __forceinline__ void roll_lds_read(RollIn<false, 2> &in, unsigned add
 // One step at input row r from LDS slot `slot` (LDS byte address `addr` + 8 * lane): wait for
 // the row's DMA (issued 2 steps ago: the stores of that step, the next row's pieces and the
 // stores of the step between are younger), read it, refill the slot with row r + 2, advance.
-template <int K, int FM>
+// MID: 6 more stores per step (the mid group), so 29 VMEM instructions are younger than the row
+template <int K, int FM, bool MID = false>
 __device__ __forceinline__ void roll_step_lds(RollPipe<false, K, 2> &S, float *slot, unsigned addr,
                                               const IterArgs &a, const RollBufs &B, int r,
                                               const RollLane &L, unsigned rowb, const RollDma &D,
-                                              double &acc) {
+                                              double &acc, double *accm = nullptr) {
   static_assert(2 * kRollStPerStep + kRollDmaPerRow == 17, "the vmcnt below");
-  asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+  static_assert(2 * 2 * kRollStPerStep + kRollDmaPerRow == 29, "the MID vmcnt below");
+  if constexpr (MID)
+    asm volatile("s_waitcnt vmcnt(29)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
   RollIn<false, 2> in;
   roll_lds_read(in, addr, a.p_zero != 0);
   roll_dma_row(slot, B, (unsigned)imin(r + 2, a.H - 1) * rowb, D);
   __builtin_amdgcn_sched_barrier(0);
-  roll_advance<false, K, 2, false, FM>(S, in, a, B, r, L, rowb, acc);
+  roll_advance<false, K, 2, false, FM, MID>(S, in, a, B, r, L, rowb, acc, accm);
 }
 
 // halo of a band: K px, rounded up to whole lanes' worth of px (8-byte aligned loads)
@@ -2075,9 +2103,12 @@ constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
 // measured -0.7 %: profiles/r3/ab_roll_prio.txt)
 // AH: input rows loaded ahead (1: a 2-row ring, 2: a 3-row ring); LDSR: rows staged in
 // LDS (lds: this wavefront's kRollLdsWave floats), see roll_step_lds
+// MID (k_iterate_roll_mid, LDSR only): the state and residual after the first 2 of the 4
+// iterations too, to B.m and partials[waves + wid]
 template <bool G, int K, int PX, int FM, int PRIO = 0, int AH = roll_ahead<K, PX>(),
-          bool LDSR = false>
+          bool LDSR = false, bool MID = false>
 __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid, float *lds = nullptr) {
+  static_assert(!MID || LDSR, "the mid check rides on the LDS-staged 4-iteration pass");
   constexpr int HALO = roll_halo<K, PX>();
   constexpr int BW = 64 * PX;            // band width (px)
   // The long pipelines (and the gamma ones) run at 2 waves/SIMD with VGPRs to spare but
@@ -2141,8 +2172,16 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid, float *ld
       bstorev<PX>(B.pd, B.pb, kOOB, z, 4 * ps);
       bstorev<PX>(B.pd, B.pb, kOOB, z, 5 * ps);
     }
+    if constexpr (MID) {
+      bstorev<PX>(B.m, B.mb, kOOB, z);
+      bstorev<PX>(B.m, B.mb, kOOB, z, ps);
+      bstorev<PX>(B.m, B.mb, kOOB, z, 2 * ps);
+      bstorev<PX>(B.m, B.mb, kOOB, z, 3 * ps);
+      bstorev<PX>(B.m, B.mb, kOOB, z, 4 * ps);
+      bstorev<PX>(B.m, B.mb, kOOB, z, 5 * ps);
+    }
   };
-  double acc = 0.0;
+  double acc = 0.0, accm = 0.0;
   if constexpr (LDSR) {   // two LDS slots, steps unrolled by 2
     static_assert(!G && PX == 2, "LDS-staged rows: the 9 planes of G = false, 2 px per lane");
     const int X0 = band * (BW - 2 * HALO) - HALO;
@@ -2166,8 +2205,8 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid, float *ld
     const int halves = (L.ye + K - r0 + 1) / 2;
     for (int h = 0, r = r0; h < halves; ++h, r += 2) {
       progress_prio<PRIO>(h, halves);
-      roll_step_lds<K, FM>(S, s0, a0, a, B, r, L, rowb, D, acc);
-      roll_step_lds<K, FM>(S, s1, a1, a, B, r + 1, L, rowb, D, acc);
+      roll_step_lds<K, FM, MID>(S, s0, a0, a, B, r, L, rowb, D, acc, &accm);
+      roll_step_lds<K, FM, MID>(S, s1, a1, a, B, r + 1, L, rowb, D, acc, &accm);
     }
     // the last steps' refills (rows past the segment) land before the block's LDS is
     // released to another block
@@ -2203,6 +2242,11 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid, float *ld
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) a.partials[wid] = acc;
   }
+  if constexpr (MID) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) accm += __shfl_xor(accm, o);
+    if (lane == 0) a.partials[ra.waves + wid] = accm;
+  }
 }
 
 template <bool G, int K, int PX, int FM = 0>
@@ -2215,6 +2259,24 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
   if (wid >= ra.waves || gated_off(ra.it.gate, ra.it.gate_seq)) return;   // whole wavefronts
   roll_body<G, K, PX, FM, 1, roll_ahead<K, PX>(), LDSR>(
       ra, wid, lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (LDSR ? kRollLdsWave : 0));
+}
+
+// k_iterate_roll_mid<FM>: k_iterate_roll<false, 4, 2> that also keeps the check after its
+// first 2 iterations -- u^2, p^2 to the mid group (RollBufs::m) and that check's residual
+// partials to partials[waves + wid] -- so that two 2-iteration passes of a warp that is
+// converging (procOneScale checking every second iteration, error just above eps^2 W H) run
+// as one 4-iteration pass and one launch (DESIGN.md §4.1 of r6).  Stage 2's values are the
+// ones a 2-iteration pass stores (same operations on the same operands: same bits), and its
+// residual covers the same px; the host reads the mid check first and takes the mid state
+// when the warp stops there.  The end check must be a calc_err pass.
+template <int FM>
+__global__ __launch_bounds__(256) void k_iterate_roll_mid(RollArgs ra) {
+  __shared__ float lds[4 * kRollLdsWave];
+  const int wid =
+      __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+  if (wid >= ra.waves || gated_off(ra.it.gate, ra.it.gate_seq)) return;   // whole wavefronts
+  roll_body<false, 4, 2, FM, 1, roll_ahead<4, 2>(), true, true>(
+      ra, wid, lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kRollLdsWave);
 }
 
 // ---------------------------------------------------------------- K5 + first pass, two roles

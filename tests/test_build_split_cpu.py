@@ -26,6 +26,7 @@ def _expected():
         for k in (1, 2):
             ks.add(f"k_iterate_roll<false, {k}, 4, {fm}>(tvl1k::RollArgs)")
         ks.add(f"k_iterate_tb4<{fm}, 3>(tvl1k::TBArgs)")
+        ks.add(f"k_iterate_roll_mid<{fm}>(tvl1k::RollArgs)")
     return ks
 
 
@@ -35,7 +36,7 @@ def _kernels(obj, kinds):
     for line in out.splitlines():
         # the kernel handle or its host launch stub (__device_stub__<kernel>)
         m = re.match(r"^\s*[0-9a-f]*\s+([A-Za-z])\s+void tvl1k::(?:__device_stub__)?"
-                     r"((?:k|kb)_iterate_(?:roll|tb4)<.*)$", line)
+                     r"((?:k|kb)_iterate_(?:roll|roll_mid|tb4)<.*)$", line)
         if m and m.group(1) in kinds:
             found[m.group(2)] = found.get(m.group(2), 0) + 1
     return found
@@ -45,7 +46,7 @@ def _kernels(obj, kinds):
 def test_passes_defined_once_in_their_own_unit():
     exp = _expected()
     inc = (PKG / "csrc" / "tvl1_passes.inc").read_text()
-    assert inc.count("TVL1_PASS_INSTANCE(") == 6 + 15   # 6 gamma forms, 15 per arithmetic mode
+    assert inc.count("TVL1_PASS_INSTANCE(") == 6 + 16   # 6 gamma forms, 16 per arithmetic mode
     defined = _kernels(LIB / "tvl1_passes.o", "VvWw")
     assert exp <= set(defined), sorted(exp - set(defined))
     assert all(n == 2 for k, n in defined.items() if k in exp)   # handle + stub, once each
@@ -55,7 +56,7 @@ def test_passes_defined_once_in_their_own_unit():
     eng_undef = set(_kernels(LIB / "tvl1_engine.o", "U"))
     hot = {"k_iterate_roll<false, 4, 2, 0>(tvl1k::RollArgs)", "k_iterate_roll<false, 2, 4, 0>(tvl1k::RollArgs)",
            "k_iterate_roll<false, 2, 2, 0>(tvl1k::RollArgs)", "k_iterate_tb4<0, 3>(tvl1k::TBArgs)",
-           "kb_iterate_roll<4, 2, 0>(tvl1k::BatchRoll)"}
+           "kb_iterate_roll<4, 2, 0>(tvl1k::BatchRoll)", "k_iterate_roll_mid<0>(tvl1k::RollArgs)"}
     assert hot <= eng_undef, sorted(hot - eng_undef)
 
 

@@ -123,17 +123,22 @@ def test_constant_images_give_zero_flow(engine):
 #                         (the default is k_iterate_tb4<FM>, 64 x 48; gamma != 0 always takes
 #                         k_iterate_tb<true,...>)
 # k_iterate<G, true> (tau/theta < 0) and the profile-1 kernels have their own tests below.
+MID_ALL = "TVL1_ROLL_LONG_MIN=0,TVL1_SPEC=0,TVL1_MID=1,TVL1_MID_MIN=1"
 MODES = ["", "TVL1_ROLL_LONG_MIN=0", "TVL1_ROLL_LONG_MIN=0,TVL1_ROLL_SEG=8", "TVL1_ROLL_SEG=8",
          "TVL1_ROLL_SEG=64", "TVL1_ROLL_PX4_MIN=0", "TVL1_ROLL_PX4_MIN=0,TVL1_ROLL_SEG=8",
          "TVL1_FUSE_MIN=0", "TVL1_FUSE_MIN=0,TVL1_ROLL_SEG=8", "TVL1_FUSE_MIN=0,TVL1_ROLL_PX4_MIN=0",
          "TVL1_FUSE=0,TVL1_ROLL_LONG_MIN=0", "TVL1_BUF_LIMIT=100000", "TVL1_BUF_LIMIT=0",
          "TVL1_POLL=0", "TVL1_POLL=0,TVL1_FUSE_MIN=0", "TVL1_SPEC=0", "TVL1_SPEC=0,TVL1_FUSE_MIN=0",
          "TVL1_FUSE_MIN=0,TVL1_WI_NC=1", "TVL1_FUSE_MIN=0,TVL1_WI_NC=1,TVL1_ROLL_SEG=8",
-         "TVL1_TB4=0", "TVL1_TB4=0,TVL1_BUF_LIMIT=0"]
+         "TVL1_TB4=0", "TVL1_TB4=0,TVL1_BUF_LIMIT=0",
+         MID_ALL, MID_ALL + ",TVL1_ROLL_SEG=8", "TVL1_MID=0,TVL1_SPEC=0,TVL1_ROLL_LONG_MIN=0"]
 # (TVL1_POLL=0: residuals read after an event instead of the poll; TVL1_SPEC=0: nothing
-# enqueued behind a check before the host reads it)
+# enqueued behind a check before the host reads it; MID_ALL: every 2-iteration
+# continuation after a warp's first check as a mid-check pass, k_iterate_roll_mid, whatever
+# the error -- so some end on the mid state, DESIGN.md §4.1 of r6)
 KNOBS = ("TVL1_ROLL_SEG", "TVL1_ROLL_PX4_MIN", "TVL1_ROLL_LONG_MIN", "TVL1_FUSE", "TVL1_FUSE_MIN",
-         "TVL1_BUF_LIMIT", "TVL1_BATCH_FUSE", "TVL1_POLL", "TVL1_SPEC", "TVL1_WI_NC", "TVL1_TB4")
+         "TVL1_BUF_LIMIT", "TVL1_BATCH_FUSE", "TVL1_POLL", "TVL1_SPEC", "TVL1_WI_NC", "TVL1_TB4",
+         "TVL1_MID", "TVL1_MID_MIN", "TVL1_SPEC_TRACE")
 CONFIG_CASES = [
     (250, 131, 21, dict(nscales=5, warps=5)),
     (97, 201, 22, dict(nscales=4, warps=3, gamma=0.1)),
@@ -250,18 +255,79 @@ def test_large_flow_uses_global_gather_fallback(built, monkeypatch, env, math):
     assert bits_equal(u, ur) and bits_equal(v, vr)
 
 
-def test_benchmark_pair_bit_exact(engine):
-    """The bench workload itself (BASELINE configs[1], C2): one 6144x4096 synthetic pair,
-    5 scales, 30 warps -- the same bits and the same 880-odd iterations as the oracle."""
+MID_RE = __import__("re").compile(r"mid-check passes (\d+), ended on the mid state (\d+)")
+
+
+# The mid-check pass (k_iterate_roll_mid): two 2-iteration passes of a converging warp as one
+# 4-iteration launch that keeps the state and residual after its first 2 iterations.  Cases
+# whose schedules hold such runs (checks every second iteration at 1 < error / eps^2 W H < 2),
+# with every continuation taken as a mid-check pass (MID_MIN=1: some end on the mid state)
+# and at the default threshold: the same bits, per-warp counts and number of checks as without.
+@pytest.mark.parametrize("mid_min", ["1", "1.1"])
+@pytest.mark.parametrize("W,H,seed,kw", [(250, 131, 21, dict(nscales=5, warps=5)),
+                                         (320, 240, 31, dict(nscales=4, warps=10)),
+                                         (256, 200, 32, dict(nscales=3, warps=6, epsilon=0.002)),
+                                         (640, 480, 42, dict(nscales=4, warps=10, epsilon=0.003))])
+def test_mid_check_passes(built, monkeypatch, capfd, mid_min, W, H, seed, kw):
+    p = capi.make_params(**kw)
+    I0, I1 = synth.gen_pair(W, H, seed=seed)
+    res = {}
+    for mid in ("1", "0"):
+        set_knobs(monkeypatch, f"TVL1_ROLL_LONG_MIN=0,TVL1_SPEC=0,TVL1_SPEC_TRACE=1,TVL1_MID={mid},"
+                               f"TVL1_MID_MIN={mid_min}")
+        capfd.readouterr()
+        eng = capi.Engine(p)
+        res[mid] = eng.calc_host(I0, I1)
+        eng.close()
+        res[mid + "err"] = capfd.readouterr().err
+    m = MID_RE.search(res["1err"])
+    assert m and int(m.group(1)) > 0, "no mid-check pass ran"
+    assert not MID_RE.search(res["0err"])
+    (u, v, st, wi), (u0, v0, st0, wi0) = res["1"], res["0"]
+    np.testing.assert_array_equal(wi, wi0)
+    assert bits_equal(u, u0) and bits_equal(v, v0)
+    assert st["checks_total"] == st0["checks_total"]
+    ur, vr, _, wr = checker.oracle_calc(I0, I1, p)
+    np.testing.assert_array_equal(wi, wr)
+    assert bits_equal(u, ur) and bits_equal(v, vr)
+    print(f"mid-check passes {m.group(1)}, ended on the mid state {m.group(2)}")
+    if mid_min == "1" and (W, H) == (250, 131):
+        assert int(m.group(2)) > 0, "no mid-check pass ended on its first check"
+
+
+@pytest.fixture(scope="module")
+def c2_oracle():
     I0, I1 = synth.gen_pair(6144, 4096, seed=0x5EED, z=1)
     p = capi.make_params(nscales=5, warps=30)
+    return I0, I1, p, checker.oracle_calc(I0, I1, p)
+
+
+def test_benchmark_pair_bit_exact(engine, c2_oracle):
+    """The bench workload itself (BASELINE configs[1], C2): one 6144x4096 synthetic pair,
+    5 scales, 30 warps -- the same bits and the same 880-odd iterations as the oracle."""
+    I0, I1, p, (ur, vr, sr, wr) = c2_oracle
     engine.set_params(p)
     u, v, st, wi = engine.calc_host(I0, I1)
-    ur, vr, sr, wr = checker.oracle_calc(I0, I1, p)
     assert st["levels"] == sr["levels"] == 5
     np.testing.assert_array_equal(wi, wr)
     assert bits_equal(u, ur) and bits_equal(v, vr)
     print(f"C2 pair: {int(wi.sum())} iterations, bit-exact vs oracle")
+
+
+def test_benchmark_pair_bit_exact_mid_checks(built, monkeypatch, capfd, c2_oracle):
+    """The C2 pair as the bench's in-flight solves run it (nothing enqueued behind a check, so
+    its converging warps' 2-iteration passes run as mid-check passes): the same bits."""
+    I0, I1, p, (ur, vr, sr, wr) = c2_oracle
+    set_knobs(monkeypatch, "TVL1_SPEC=0,TVL1_SPEC_TRACE=1,TVL1_MID=1")
+    capfd.readouterr()
+    eng = capi.Engine(p)
+    u, v, st, wi = eng.calc_host(I0, I1)
+    eng.close()
+    m = MID_RE.search(capfd.readouterr().err)
+    assert m and int(m.group(1)) >= 4, "the C2 pair's level-0 run took no mid-check passes"
+    np.testing.assert_array_equal(wi, wr)
+    assert bits_equal(u, ur) and bits_equal(v, vr)
+    print(f"C2 pair: mid-check passes {m.group(1)}, ended on the mid state {m.group(2)}")
 
 
 def test_benchmark_pair_bit_exact_fma_mode(engine):

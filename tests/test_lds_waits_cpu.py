@@ -21,8 +21,10 @@ FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "--offl
 PIECES, WAIT = 5, 17
 # mangled-name fragments of the kernels with LDS-staged rows (G = 0, K = 3, 4, PX = 2; every
 # arithmetic mode)
-LDS_KERNELS = [f"k_iterate_rollILb0ELi{k}ELi2ELi{fm}E" for k in (3, 4) for fm in (0, 1, 2)] + \
-              [f"kb_iterate_rollILi{k}ELi2ELi{fm}E" for k in (3, 4) for fm in (0, 1, 2)]
+# (fragment, counted wait, stores per step)
+LDS_KERNELS = [(f"k_iterate_rollILb0ELi{k}ELi2ELi{fm}E", WAIT, 6) for k in (3, 4) for fm in (0, 1, 2)] + \
+              [(f"kb_iterate_rollILi{k}ELi2ELi{fm}E", WAIT, 6) for k in (3, 4) for fm in (0, 1, 2)] + \
+              [(f"k_iterate_roll_midILi{fm}E", 29, 12) for fm in (0, 1, 2)]   # + the mid group's 6
 
 
 @pytest.fixture(scope="module")
@@ -63,13 +65,13 @@ def vmem_events(body):
     return ev
 
 
-@pytest.mark.parametrize("frag", LDS_KERNELS)
-def test_row_waits_cover_the_rows_pieces(asm, frag):
+@pytest.mark.parametrize("frag,wait,stores", LDS_KERNELS)
+def test_row_waits_cover_the_rows_pieces(asm, frag, wait, stores):
     ev = vmem_events(kernel_body(asm, frag))
-    kinds = "".join("C" if k == "W" and t == f"s_waitcnt vmcnt({WAIT})" else k for k, t in ev)
+    kinds = "".join("C" if k == "W" and t == f"s_waitcnt vmcnt({wait})" else k for k, t in ev)
     # C = the counted wait of a step.  The step loop is unrolled by 2 (one step per LDS
     # slot); the compiler may emit more than one copy of it (alternative paths), each entered
-    # from the prologue.  Every step: the wait, the next row's PIECES loads, 6 stores.
+    # from the prologue.  Every step: the wait, the next row's PIECES loads, the stores.
     counted = [i for i, k in enumerate(kinds) if k == "C"]
     assert counted and len(counted) % 2 == 0, kinds
     prologue = kinds[kinds.index("D"):counted[0]]
@@ -82,7 +84,7 @@ def test_row_waits_cover_the_rows_pieces(asm, frag):
         body = kinds[counted[c]:end]
         steps = re.findall(r"C([^C]*)", body)
         assert len(steps) == 2, (frag, body)
-        step = "D" * PIECES + "S" * 6
+        step = "D" * PIECES + "S" * stores
         for st in steps:
             assert st.replace("W", "").startswith(step), (frag, body)
         # Row k is the k-th group of PIECES loads (the prologue's rows r0, r0 + 1, then one
@@ -98,7 +100,7 @@ def test_row_waits_cover_the_rows_pieces(asm, frag):
                     d_end.append(i)
         for row, w in enumerate(i for i, k in enumerate(seq) if k == "C"):
             after = sum(1 for k in seq[d_end[row] + 1:w] if k in "DSL")
-            assert after >= WAIT, (frag, row, after, seq)
+            assert after >= wait, (frag, row, after, seq)
 
 
 def test_only_lds_kernels_stage_rows(asm):

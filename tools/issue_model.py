@@ -99,6 +99,7 @@ ISA_KERNELS = {
     "14k_iterate_rollILb0ELi4ELi2ELi0E": "k_iterate_roll_0_4_2_0.s",
     "14k_iterate_rollILb0ELi2ELi4ELi0E": "k_iterate_roll_0_2_4_0.s",
     "14k_iterate_rollILb0ELi2ELi2ELi0E": "k_iterate_roll_0_2_2_0.s",
+    "18k_iterate_roll_midILi0E": "k_iterate_roll_mid_0.s",
     "13k_iterate_tb4ILi0ELi3E": "k_iterate_tb4_0_3.s",
     "12kb_warp_iterILi6ELi0ELi2E": "kb_warp_iter_6_0_2.s",
     "15kb_iterate_rollILi4ELi2ELi0E": "kb_iterate_roll_4_2_0.s",
@@ -112,6 +113,7 @@ CLASS_KERNELS = {
     "k_iterate_roll<false, 4, 2, 0>": "k_iterate_roll_0_4_2_0.s",
     "k_iterate_roll<false, 2, 4, 0>": "k_iterate_roll_0_2_4_0.s",
     "k_iterate_roll<false, 2, 2, 0>": "k_iterate_roll_0_2_2_0.s",
+    "k_iterate_roll_mid<0>": "k_iterate_roll_mid_0.s",   # r6: absent from runs before it
     "k_iterate_tb4<0, 3>": "k_iterate_tb4_0_3.s",
 }
 # the production strips' batched iteration class (the kernels that hold 98 % of its time)
@@ -538,6 +540,9 @@ def class_model(pmc_path, isa_dir, rates_path, kernels=CLASS_KERNELS):
     out = {"kernels": {}}
     tb = tc = tv = tv2 = 0.0
     for kname, fname in kernels.items():
+        if not any(r["kernel"] == kname and r["dispatches"] and int(r["dispatches"]) > 0
+                   for r in rows):
+            continue   # not dispatched in this run (e.g. the mid-check pass before r6's last engine)
         if kname.startswith(("k_warp_iter", "kb_warp_iter")):
             c = defaultdict(int)
             for r, cc in role_loops(load_isa(Path(isa_dir) / fname)).items():
