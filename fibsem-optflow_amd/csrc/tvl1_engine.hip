@@ -1208,8 +1208,8 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     };
     // what to predict after a check at iteration count n of warp wp: pk = 0 the warp stops
     // (its successor's first pass follows), pk > 0 it continues with (pk, pcalc), -1 nothing
-    auto predict = [&](int wp, int n, bool nostore, int last_n, const Hist &h,
-                       const std::vector<int> *prevw, int &pk, int &pcalc) {
+    auto predict0 = [&](int wp, int n, bool nostore, int last_n, const Hist &h,
+                        const std::vector<int> *prevw, int &pk, int &pcalc) {
       pk = -1;
       pcalc = 0;
       if (!spec_ok) return;
@@ -1240,6 +1240,13 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
       } else if (can_stop) {
         pk = 0;
       }
+    };
+    // a predicted 2-iteration continuation after a warp's first check is left to the host,
+    // which may run it as a mid-check pass (less GPU work than the pass enqueued ahead)
+    auto predict = [&](int wp, int n, bool nostore, int last_n, const Hist &h,
+                       const std::vector<int> *prevw, int &pk, int &pcalc) {
+      predict0(wp, n, nostore, last_n, h, prevw, pk, pcalc);
+      if (c->mid && mid_ok && pk == 2 && pcalc && n > 2) pk = -1;
     };
     auto gate_of = [&](int wp, int n, int pk, int pcalc, unsigned long long gin_seq, bool gated) {
       CheckGate gt{};
