@@ -86,7 +86,6 @@ struct tvl1_ctx {
   float *U[2][3] = {};   // u1, u2, u3
   float *Pd[2][6] = {};  // p11, p12, p21, p22, p31, p32
   float *C[2][3] = {};   // two sets of warp constants I1wx, I1wy, rho_c (speculation)
-  float *Mid = nullptr;  // k_iterate_roll_mid's state after 2 iterations: u1, u2, p11..p22
   uint8_t *in0 = nullptr, *in1 = nullptr;   // staging for tvl1_calc_host
   float *outu = nullptr, *outv = nullptr;
   double *partials = nullptr;
@@ -462,7 +461,6 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H, hipStream_t st) {
   bytes += 2 * 3 * plane;                   // U[2][3]
   bytes += 2 * 6 * plane;                   // Pd[2][6]
   bytes += 2 * 3 * plane;                   // C[2]
-  bytes += 6 * plane;                       // Mid
   bytes += 2 * align_up(P0 * H, 256);       // in0, in1 (u8)
   bytes += 2 * plane;                       // outu, outv
   // residual partials: k_iterate_tb worst case (RH 32 at 4 iterations: 56 x 24 px per
@@ -497,7 +495,6 @@ static tvl1_status ensure_geometry(tvl1_ctx *c, int W, int H, hipStream_t st) {
     for (int k = 0; k < 6; ++k) c->Pd[b][k] = (float *)take(plane);
   for (int b = 0; b < 2; ++b)
     for (int k = 0; k < 3; ++k) c->C[b][k] = (float *)take(plane);
-  c->Mid = (float *)take(6 * plane);        // six planes at the plane stride (one RollBufs group)
   c->in0 = (uint8_t *)take(P0 * H);
   c->in1 = (uint8_t *)take(P0 * H);
   c->outu = (float *)take(plane);
@@ -885,8 +882,6 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
     b.cb = (unsigned)group_bytes(s, 3);
     b.ub = (unsigned)group_bytes(s, gam ? 3 : 2);
     b.pb = (unsigned)group_bytes(s, gam ? 6 : 4);
-    b.m = c->Mid;
-    b.mb = (unsigned)group_bytes(s, 6);
     return b;
   };
   auto gather = [&](int s, int uset, int cbuf, int wp) -> tvl1_status {  // K5 warpBackward
@@ -1174,8 +1169,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
                       prm.iterations >= 2 && (long)lw * lh >= c->fuse_min;
     const int kmax = exact_div ? 1 : roll_ok ? kRollMax : kTbMax;
     // the mid-check pass (k_iterate_roll_mid) where a 4-iteration pass streams
-    const bool mid_ok = !gam && !exact_div && roll_long && prm.epsilon > 0 && kRollMax >= 4 &&
-                        group_bytes(s, 6) < c->buf_limit;
+    const bool mid_ok = !gam && !exact_div && roll_long && prm.epsilon > 0 && kRollMax >= 4;
     // Speculation: behind each residual check the host enqueues the launch it
     // expects to follow, gated on the device by the check's own evaluation of the stopping
     // rule, and only then waits for the residual.  A right guess hides the host round trip;
@@ -1317,10 +1311,11 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
                                     prm.epsilon > 0, &calc_end, &prev_sim);
           // A converging warp (a check every second iteration, the error just above eps^2 W H)
           // runs its next two 2-iteration passes as one k_iterate_roll_mid pass: both checks'
-          // residuals, the state after 2 iterations in c->Mid and after 4 in the usual set.
-          // The host reads the first check as procOneScale does; if the warp stops there (or
-          // its schedule is not a second 2-iteration pass) the mid state is taken instead
-          // (DESIGN.md §4.1 of r6).  Not for a warp's first check (n = 2: its error drops the
+          // residuals and the state after 4 iterations in the usual set.  The host reads the
+          // first check as procOneScale does; if the warp stops there (or its schedule is not
+          // a second 2-iteration pass) a 2-iteration pass from the same input set, which the
+          // mid-check pass leaves as it was, recomputes the state at that check (DESIGN.md
+          // §4.1 of r6).  Not for a warp's first check (n = 2: its error drops the
           // most), nor where the 4-iteration pass does not stream.
           if (c->mid && mid_ok && k == 2 && calc_end && n > 2 && n + 4 <= prm.iterations &&
               prevError >= c->mid_min * scaledEps) {
@@ -1353,14 +1348,9 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
               note(e_end, n);
               error = e_end;
               prevError = e_end;
-            } else {   // the state after the first 2 iterations: the set a 2-iteration pass writes
+            } else {   // the state at the first check: its 2 iterations again, no residual
               ++mid_taken;
-              const size_t bytes = (size_t)P * lh * sizeof(float);
-              float *dst[6] = {c->U[ui ^ 1][0], c->U[ui ^ 1][1], c->Pd[pi ^ 1][0],
-                               c->Pd[pi ^ 1][1], c->Pd[pi ^ 1][2], c->Pd[pi ^ 1][3]};
-              for (int q = 0; q < 6; ++q)
-                HIP_TRY(c, hipMemcpyAsync(dst[q], (const char *)c->Mid + q * pstride, bytes,
-                                          hipMemcpyDeviceToDevice, st));
+              TRY(launch_pass(2, false, false, false, ui, pi, cb, false, nullptr, 0, wp, n - 2, blocks));
               error = e_mid;
               prevError = e_mid;
             }

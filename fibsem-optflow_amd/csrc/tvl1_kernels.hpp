@@ -1739,8 +1739,6 @@ struct RollBufs {
   float *ud, *pd;          // u, p written
   unsigned cb, ub, pb;     // group bytes (descriptor records) of c, u, p
   unsigned pstride;        // bytes between the planes of a group
-  float *m;                // k_iterate_roll_mid: u1, u2, p11, p12, p21, p22 after 2 iterations
-  unsigned mb;             // its group bytes
 };
 
 struct RollArgs {
@@ -1838,8 +1836,7 @@ __device__ __forceinline__ float right_of(const float (&v)[PX], int j) {
 // the dependency list above; the border forms select, never combine).
 // VIN: in.u1 / u2 / u3 hold stage 1's v = u^0 + TH step (th_px, computed by the caller)
 // instead of u^0
-// MID (k_iterate_roll_mid): stage 2 also sums its residual into *accm and stores u^2 / p^2 to
-// the mid group B.m
+// MID (k_iterate_roll_mid): stage 2 also sums its residual into *accm
 template <bool G, int K, int PX, bool VIN = false, int FM = 0, bool MID = false>
 __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn<G, PX> &in,
                                              const IterArgs &a, const RollBufs &B, int r,
@@ -1934,11 +1931,6 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
         S.U1c[n][j] = S.U1p[n][j]; S.U2c[n][j] = S.U2p[n][j]; if (G) S.U3c[n][j] = S.U3p[n][j];
       }
     }
-    if (MID && n == 2) {   // u^2 to mid planes 0, 1
-      const unsigned vo = stU ? (unsigned)yU * rowb + L.vst : kOOB;
-      bstorev<PX>(B.m, B.mb, vo, S.U1c[n]);
-      bstorev<PX>(B.m, B.mb, vo, S.U2c[n], ps);
-    }
     if (n == K) {
       const unsigned vo = stU ? (unsigned)yU * rowb + L.vst : kOOB;
       bstorev<PX>(B.ud, B.ub, vo, S.U1c[n]);
@@ -1970,13 +1962,6 @@ __device__ __forceinline__ void roll_advance(RollPipe<G, K, PX> &S, const RollIn
         S.P11c[n][j] = S.P12c[n][j] = S.P21c[n][j] = S.P22c[n][j] = 0.0f;
         if (G) S.P31c[n][j] = S.P32c[n][j] = 0.0f;
       }
-    }
-    if (MID && n == 2) {   // p^2 to mid planes 2 .. 5
-      const unsigned vo = L.out && yD >= L.ys && yD < L.ye ? (unsigned)yD * rowb + L.vst : kOOB;
-      bstorev<PX>(B.m, B.mb, vo, S.P11c[n], 2 * ps);
-      bstorev<PX>(B.m, B.mb, vo, S.P12c[n], 3 * ps);
-      bstorev<PX>(B.m, B.mb, vo, S.P21c[n], 4 * ps);
-      bstorev<PX>(B.m, B.mb, vo, S.P22c[n], 5 * ps);
     }
     if (n == K) {
       const unsigned vo = L.out && yD >= L.ys && yD < L.ye ? (unsigned)yD * rowb + L.vst : kOOB;
@@ -2071,18 +2056,13 @@ __device__ __forceinline__ void roll_lds_read(RollIn<false, 2> &in, unsigned add
 // One step at input row r from LDS slot `slot` (LDS byte address `addr` + 8 * lane): wait for
 // the row's DMA (issued 2 steps ago: the stores of that step, the next row's pieces and the
 // stores of the step between are younger), read it, refill the slot with row r + 2, advance.
-// MID: 6 more stores per step (the mid group), so 29 VMEM instructions are younger than the row
 template <int K, int FM, bool MID = false>
 __device__ __forceinline__ void roll_step_lds(RollPipe<false, K, 2> &S, float *slot, unsigned addr,
                                               const IterArgs &a, const RollBufs &B, int r,
                                               const RollLane &L, unsigned rowb, const RollDma &D,
                                               double &acc, double *accm = nullptr) {
   static_assert(2 * kRollStPerStep + kRollDmaPerRow == 17, "the vmcnt below");
-  static_assert(2 * 2 * kRollStPerStep + kRollDmaPerRow == 29, "the MID vmcnt below");
-  if constexpr (MID)
-    asm volatile("s_waitcnt vmcnt(29)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
   RollIn<false, 2> in;
   roll_lds_read(in, addr, a.p_zero != 0);
   roll_dma_row(slot, B, (unsigned)imin(r + 2, a.H - 1) * rowb, D);
@@ -2103,8 +2083,8 @@ constexpr int roll_halo() { return (K + PX - 1) / PX * PX; }
 // measured -0.7 %: profiles/r3/ab_roll_prio.txt)
 // AH: input rows loaded ahead (1: a 2-row ring, 2: a 3-row ring); LDSR: rows staged in
 // LDS (lds: this wavefront's kRollLdsWave floats), see roll_step_lds
-// MID (k_iterate_roll_mid, LDSR only): the state and residual after the first 2 of the 4
-// iterations too, to B.m and partials[waves + wid]
+// MID (k_iterate_roll_mid, LDSR only): the residual after the first 2 of the 4 iterations
+// too, to partials[waves + wid]
 template <bool G, int K, int PX, int FM, int PRIO = 0, int AH = roll_ahead<K, PX>(),
           bool LDSR = false, bool MID = false>
 __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid, float *lds = nullptr) {
@@ -2171,14 +2151,6 @@ __device__ __forceinline__ void roll_body(const RollArgs &ra, int wid, float *ld
     if (G) {
       bstorev<PX>(B.pd, B.pb, kOOB, z, 4 * ps);
       bstorev<PX>(B.pd, B.pb, kOOB, z, 5 * ps);
-    }
-    if constexpr (MID) {
-      bstorev<PX>(B.m, B.mb, kOOB, z);
-      bstorev<PX>(B.m, B.mb, kOOB, z, ps);
-      bstorev<PX>(B.m, B.mb, kOOB, z, 2 * ps);
-      bstorev<PX>(B.m, B.mb, kOOB, z, 3 * ps);
-      bstorev<PX>(B.m, B.mb, kOOB, z, 4 * ps);
-      bstorev<PX>(B.m, B.mb, kOOB, z, 5 * ps);
     }
   };
   double acc = 0.0, accm = 0.0;
@@ -2261,16 +2233,19 @@ __global__ __launch_bounds__(256) void k_iterate_roll(RollArgs ra) {
       ra, wid, lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (LDSR ? kRollLdsWave : 0));
 }
 
-// k_iterate_roll_mid<FM>: k_iterate_roll<false, 4, 2> that also keeps the check after its
-// first 2 iterations -- u^2, p^2 to the mid group (RollBufs::m) and that check's residual
-// partials to partials[waves + wid] -- so that two 2-iteration passes of a warp that is
-// converging (procOneScale checking every second iteration, error just above eps^2 W H) run
-// as one 4-iteration pass and one launch (DESIGN.md §4.1 of r6).  Stage 2's values are the
-// ones a 2-iteration pass stores (same operations on the same operands: same bits), and its
-// residual covers the same px; the host reads the mid check first and takes the mid state
-// when the warp stops there.  The end check must be a calc_err pass.
+// k_iterate_roll_mid<FM>: k_iterate_roll<false, 4, 2> that also sums the residual of the
+// check after its first 2 iterations (partials[waves + wid]), so that two 2-iteration passes
+// of a warp that is converging (procOneScale checking every second iteration, error just
+// above eps^2 W H) run as one 4-iteration pass and one launch (DESIGN.md §4.1 of r6).  Stage
+// 2's values are the ones a 2-iteration pass computes (same operations on the same operands),
+// so its residual is that pass's over the same px; the host reads it first, and when the warp
+// stops there it recomputes the 2-iteration state from the pass's input set, which the pass
+// leaves untouched.  The end check must be a calc_err pass.
+#ifndef TVL1_MID_MINW   // minimum waves per SIMD the mid-check pass is compiled for (A/B)
+#define TVL1_MID_MINW 1
+#endif
 template <int FM>
-__global__ __launch_bounds__(256) void k_iterate_roll_mid(RollArgs ra) {
+__global__ __launch_bounds__(256, TVL1_MID_MINW) void k_iterate_roll_mid(RollArgs ra) {
   __shared__ float lds[4 * kRollLdsWave];
   const int wid =
       __builtin_amdgcn_readfirstlane(xcd_chunk(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));

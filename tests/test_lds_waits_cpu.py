@@ -24,7 +24,7 @@ PIECES, WAIT = 5, 17
 # (fragment, counted wait, stores per step)
 LDS_KERNELS = [(f"k_iterate_rollILb0ELi{k}ELi2ELi{fm}E", WAIT, 6) for k in (3, 4) for fm in (0, 1, 2)] + \
               [(f"kb_iterate_rollILi{k}ELi2ELi{fm}E", WAIT, 6) for k in (3, 4) for fm in (0, 1, 2)] + \
-              [(f"k_iterate_roll_midILi{fm}E", 29, 12) for fm in (0, 1, 2)]   # + the mid group's 6
+              [(f"k_iterate_roll_midILi{fm}E", WAIT, 6) for fm in (0, 1, 2)]
 
 
 @pytest.fixture(scope="module")
