@@ -137,7 +137,7 @@ struct tvl1_ctx {
   int witer_slots = 0;       // resident k_warp_iter<6, -, 128, 1, wi_nc> blocks per device
   int mid = 1;               // TVL1_MID=0: no mid-check passes (k_iterate_roll_mid, DESIGN.md
                              // §4.1 of r6): two 2-iteration passes of a converging warp as one
-                             // (C2 in flight +1.5 %, profiles/r6/mid/)
+                             // (C2 in flight +2.5 %, profiles/r6/final_mid/)
   double mid_min = 1.1;      // TVL1_MID_MIN: ... when the check before them read at least this
                              // many eps^2 W H (the first of the two checks then rarely stops)
   int mid_slots = 0;         // resident k_iterate_roll_mid wavefronts

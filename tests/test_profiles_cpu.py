@@ -125,21 +125,24 @@ def test_final_bench_line_fields(FINAL):
 
 
 def test_bench_reads_the_r6_traffic_record():
-    """profiles/traffic*.json (bench.py's `traffic`) are the r6 evidence set's records."""
-    for name in ("traffic.json", "traffic_strips.json"):
+    """profiles/traffic*.json (bench.py's `traffic`) are the r6 evidence sets' records: the C2
+    class from the last engine (the mid-check pass changed its launch mix), the strips' from
+    profiles/r6/final/ (the batched path did not change)."""
+    for name, d in (("traffic.json", "final_mid"), ("traffic_strips.json", "final")):
         top = json.loads((PROF / name).read_text())
-        r6 = json.loads((PROF / "r6" / "final" / name).read_text())
-        assert top == r6 and "profiles/r6/final/" in top["source"]
+        r6 = json.loads((PROF / "r6" / d / name).read_text())
+        assert top == r6 and f"profiles/r6/{d}/" in top["source"]
 
 
 def test_r6_bench_line_names_the_valu_bound():
     """The r6 evidence line: `roofline.bound` is `valu` from the committed issue model
     (profiles/r6/issue/model.json), with the HBM roofline beside it, for C2 and the strips."""
-    d = json.loads((PROF / "r6" / "final" / "bench_c2.json").read_text().splitlines()[-1])
-    for r in (d["roofline"], d["production_strips"]["roofline"]):
-        assert r["bound"] == "valu" and r["frac"] == r["valu"]["frac"] > r["hbm"]["frac"]
-        assert "profiles/r6/issue/model.json" in r["valu"]["source"]
-        assert abs(r["valu"]["frac"] / r["valu"]["pmc_frac"] - 1) < 0.10
+    for d in ("final", "final_mid"):
+        d = json.loads((PROF / "r6" / d / "bench_c2.json").read_text().splitlines()[-1])
+        for r in (d["roofline"], d["production_strips"]["roofline"]):
+            assert r["bound"] == "valu" and r["frac"] == r["valu"]["frac"] > r["hbm"]["frac"]
+            assert "profiles/r6/issue/model.json" in r["valu"]["source"]
+            assert abs(r["valu"]["frac"] / r["valu"]["pmc_frac"] - 1) < 0.10
 
 
 def test_r5_bench_line_carries_rank_records_and_allotment():
