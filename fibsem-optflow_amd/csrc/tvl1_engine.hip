@@ -1112,8 +1112,7 @@ static tvl1_status solve(tvl1_ctx *c, const Frames &in, int W, int H, float *u, 
             const int ys = sg * seg, ye = std::min(ys + seg, lh);
             rows += std::min(ye - 1 + k, lh - 1) - std::max(ys - k, 0) + 1;
           }
-          hbm = (double)ra.bands * 64.0 * px * rows * 4.0 * ld_planes + Nl * 4.0 * st_planes *
-                (midp ? 2.0 : 1.0);
+          hbm = (double)ra.bands * 64.0 * px * rows * 4.0 * ld_planes + Nl * 4.0 * st_planes;
         } else if (c->tb4 && !gam) {   // 64 x 48 regions, 3 rows x 2 px per thread
           TBArgs t;
           t.it = a;
