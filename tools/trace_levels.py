@@ -18,10 +18,12 @@ import sqlite3
 def family(name):
     m = re.match(r"_ZN5tvl1k\d+(\w+?)I", name) or re.match(r"_ZN5tvl1k\d+(\w+?)E", name)
     base = m.group(1) if m else name
-    if "Li4E" in name and "iterate_roll" in name:
-        base += "<4>"
-    elif "Li2E" in name and "iterate_roll" in name:
-        base += "<2>"
+    # the streaming passes by their iteration count K: k_iterate_roll<G, K, PX, FM> and
+    # kb_iterate_roll<K, PX, FM> (r6: the old test for "Li4E" anywhere in the name also
+    # counted k_iterate_roll<G, 2, 4> as a 4-iteration pass)
+    k = re.search(r"k_iterate_rollILb[01]ELi(\d)E", name) or re.search(r"kb_iterate_rollILi(\d)E", name)
+    if k:
+        base += f"<{k.group(1)}>"
     return base
 
 
